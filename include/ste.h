@@ -1,0 +1,257 @@
+/*
+ * ste.h — C ABI of libste.so, the MI355X (gfx950) kernels behind the
+ * speech<->transcript contrastive training step.
+ *
+ * Every entry point takes plain device pointers, sizes and a hipStream_t (passed
+ * as void*), enqueues work on that stream and returns 0 or a ste/hip error code.
+ * Nothing here allocates, frees or synchronises, so every call is hipGraph
+ * capturable.  Inputs are borrowed; outputs are caller-allocated.
+ *
+ * Each declaration cites the reference interface it replaces.  "tf:" paths are
+ * relative to transformers/ (the reference pins transformers 4.50.2, uv.lock:1813);
+ * "ref:" paths are relative to /root/reference.
+ */
+#ifndef STE_H_
+#define STE_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STE_OK 0
+#define STE_ERR_ARG 1001
+#define STE_ERR_SHAPE 1002
+
+/* ------------------------------------------------------------------ GEMM --
+ * Replaces nn.Linear / kernel-size-1 nn.Conv1d forward and both backward
+ * products: tf:models/wav2vec2_bert/modeling_wav2vec2_bert.py:119-226,229-337,
+ * tf:models/xlm_roberta/modeling_xlm_roberta.py:186-398,
+ * ref:training/trainer_unfreeze.py:66-310 (projection / attention / fusion heads).
+ *
+ * C = epilogue(alpha * A.B), bf16 operands, fp32 accumulation.
+ *   a_kc=1: A[m*lda+k]   a_kc=0: A[k*lda+m]
+ *   b_kc=1: B[n*ldb+k]   b_kc=0: B[k*ldb+n]
+ * Epilogue, in order: v = alpha*acc + bias[n];
+ *   act in {SWISH,GELU,TANH,RELU}: C2 <- v (bf16, pre-activation, optional); v = act(v)
+ *   act in {*_BWD}: v *= act'(Z[m,n])           (Z: bf16, row stride ldz)
+ *   drop_p>0: v *= keep(seed, m*drop_ld+n)/(1-drop_p)
+ *   row_scale: v *= row_scale[m]
+ *   colsum: colsum[n] += v                      (fp32 atomics; bias gradients)
+ *   R: v += R[m,n]                              (fp32, or bf16 if r_bf16)
+ *   beta != 0: v += beta*C[m,n]
+ *   C <- v (fp32, or bf16 if c_bf16);  C3 <- bf16(v) (optional)
+ * Contract: N%4==0; KC operands need K%8==0 and ld%8==0; KM operands need
+ * (M or N)%8==0 and ld%8==0.
+ */
+enum {
+  STE_ACT_NONE = 0,
+  STE_ACT_SWISH = 1,
+  STE_ACT_GELU = 2,
+  STE_ACT_TANH = 3,
+  STE_ACT_RELU = 4,
+  STE_ACT_SWISH_BWD = 11,
+  STE_ACT_GELU_BWD = 12,
+  STE_ACT_TANH_BWD_OUT = 13,
+  STE_ACT_RELU_BWD = 14
+};
+
+typedef struct {
+  int M, N, K, batch;
+  const void* A; int64_t lda; int a_kc;
+  const void* B; int64_t ldb; int b_kc;
+  int64_t strideA, strideB, strideC, strideR;
+  void* C; int64_t ldc; int c_bf16;
+  void* C2; int64_t ldc2;
+  void* C3; int64_t ldc3;
+  const float* bias;
+  const void* R; int64_t ldr; int r_bf16;
+  const void* Z; int64_t ldz;
+  float* colsum;
+  const float* row_scale;
+  float alpha, beta;
+  int act;
+  float drop_p; uint64_t seed; int64_t drop_ld;
+} ste_gemm_args;
+
+int ste_gemm(const ste_gemm_args* args, void* stream);
+
+/* ------------------------------------------------------------- LayerNorm --
+ * Replaces nn.LayerNorm forward/backward (every LN of both encoders and the
+ * heads: tf:…wav2vec2_bert…:122,169,181,381-394; tf:…xlm_roberta…:64,333,389;
+ * ref:training/trainer_unfreeze.py:97,475,477,244).
+ * Row-wise over `cols`; fp32 statistics saved as mean/rstd [rows].
+ * Forward options: row_scale (multiply output rows, e.g. the conformer conv
+ * module's masked_fill, tf:…wav2vec2_bert…:194-196), post-activation (swish:
+ * conv module's depthwise LN + activation, :209-211), fp32 and/or bf16 outputs,
+ * dropout on the output (XLM-R embeddings, tf:…xlm_roberta…:119-120).
+ */
+typedef struct {
+  int rows, cols;
+  const void* x; int64_t ldx; int x_bf16;
+  const float* gamma; const float* beta; float eps;
+  float* y; int64_t ldy;            /* fp32 output (optional) */
+  void* yb; int64_t ldyb;           /* bf16 output (optional) */
+  float* mean; float* rstd;         /* saved statistics (required) */
+  const float* row_scale;           /* optional */
+  int act;                          /* STE_ACT_NONE or STE_ACT_SWISH */
+  float drop_p; uint64_t seed;      /* dropout on the output (index row*cols+col) */
+} ste_ln_fwd_args;
+int ste_layernorm_fwd(const ste_ln_fwd_args* a, void* stream);
+
+/* Backward: g = dy (fp32 or bf16; times row_scale; through swish' if act==SWISH,
+ * recomputing the pre-activation from x/mean/rstd), dx = LN'(g) (+ dres),
+ * dgamma/dbeta += (fp32 atomics, optional).  Outputs: dx fp32 (optional),
+ * dxb = bf16(dx * dropmask(drop_seed) * out_scale) (optional). */
+typedef struct {
+  int rows, cols;
+  const void* dy; int64_t lddy; int dy_bf16;
+  const void* x; int64_t ldx; int x_bf16;
+  const float* mean; const float* rstd;
+  const float* gamma; const float* beta;
+  const float* row_scale;
+  int act;
+  const float* dres; int64_t lddres;
+  float* dx; int64_t lddx;
+  void* dxb; int64_t lddxb;
+  float* dgamma; float* dbeta;
+  float drop_p; uint64_t seed; float out_scale;   /* dropout/scale applied to the dxb copy only */
+  float in_drop_p; uint64_t in_seed;              /* forward output dropout to undo on dy */
+} ste_ln_bwd_args;
+int ste_layernorm_bwd(const ste_ln_bwd_args* a, void* stream);
+
+/* ------------------------------------------------------------- Attention --
+ * Multi-head self-attention core, softmax(QKᵀ·scale + relbias + mask)·V, fused
+ * (scores never reach HBM).  Replaces:
+ *   audio: Wav2Vec2BertSelfAttention relative_key path,
+ *          tf:…wav2vec2_bert…:285-327 (bias[l,r] = q_l·E[clamp(r-l,-left,right)+left]·scale)
+ *   text:  XLM-R SDPA attention with key-padding mask and probs dropout,
+ *          tf:…xlm_roberta…:186-250.
+ * q/k/v/o are bf16 [B*T, *] with row strides ldq/ldk/ldv/ldo; head h uses
+ * columns h*64..h*64+63 (head_dim fixed at 64).  key_mask [B*T] (nonzero = valid)
+ * may be NULL.  rel_E [left+right+1, 64] bf16 may be NULL (no relative bias).
+ * lse [B*H*T] fp32 is saved for backward.
+ */
+typedef struct {
+  int B, T, H;
+  const void* q; int64_t ldq;
+  const void* k; int64_t ldk;
+  const void* v; int64_t ldv;
+  void* o; int64_t ldo;
+  float* lse;
+  const int32_t* key_mask;
+  const void* rel_E; int rel_left, rel_right;
+  float scale;
+  float drop_p; uint64_t seed;
+  /* backward */
+  const void* dout; int64_t lddo;
+  void* dq; int64_t lddq;
+  void* dk; int64_t lddk;
+  void* dv; int64_t lddv;
+  float* delta;       /* workspace [B*H*T] */
+  float* dE;          /* fp32 [left+right+1, 64], accumulated (may be NULL) */
+} ste_attn_args;
+int ste_attention_fwd(const ste_attn_args* a, void* stream);
+int ste_attention_bwd(const ste_attn_args* a, void* stream);
+
+/* ----------------------------------------------- Conformer conv module core --
+ * GLU over channels then causal depthwise conv (left pad K-1), no bias.
+ * Replaces tf:…wav2vec2_bert…:198-207 (glu, F.pad(K-1,0), depthwise_conv).
+ * pre: bf16 [B*T, 2C]; w: fp32 [C, K]; out: bf16 [B*T, C].
+ * Backward: dout bf16 [B*T, C] -> dpre bf16 [B*T, 2C]; dw fp32 [C,K] += (optional).
+ */
+int ste_glu_dwconv_fwd(const void* pre, const float* w, void* out, int B, int T, int C, int K, void* stream);
+int ste_glu_dwconv_bwd(const void* pre, const float* w, const void* dout, void* dpre, float* dw,
+                       int B, int T, int C, int K, void* stream);
+
+/* ------------------------------------------------------------------ fbank --
+ * Batched Kaldi-style log-mel fbank + per-utterance CMVN + stride-2 stacking:
+ * the arithmetic of SeamlessM4TFeatureExtractor.__call__
+ * (tf:models/seamless_m4t/feature_extraction_seamless_m4t.py:112-138,140-301,
+ * tf:audio_utils.py:809-1017) fused with ref:training/trainer_unfreeze.py:880-921
+ * (custom_collate_fn padding).  wav fp32 [B, ld_wav]; lengths int32 [B].
+ * feats fp32 [B, Tmax, 160]; mask int64 [B, Tmax]; work fp32 >= B*Fmax*80 with
+ * Fmax = 2*Tmax.  mask_mode 0: collate semantics (1 for t < T_b);
+ * mask_mode 1: extractor semantics (0 for a padded odd frame).
+ */
+int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* lengths, int B, int Tmax, float pad_value,
+              float* feats, int64_t* mask, int mask_mode, float* work, void* stream);
+
+/* ------------------------------------------------------------------ heads --
+ * AttentivePooling (ref:training/trainer_unfreeze.py:171-211) after its first
+ * Linear+tanh has run through ste_gemm: score = t·w2 + b2, masked softmax over
+ * the sequence (-1e9 fill), pooled = Σ w·h.
+ * t bf16 [B*L, Hh]; h bf16 [B*L, H]; mask int32 [B*L] (NULL = all valid);
+ * outputs: weights fp32 [B*L], pooled fp32 [B,H] and bf16 [B,H] (optional).
+ */
+int ste_attn_pool_fwd(const void* t, const float* w2, const float* b2, const void* h, const int32_t* mask,
+                      int B, int L, int Hh, int H, float* weights, float* pooled, void* pooled_bf16,
+                      void* stream);
+/* Backward: dpooled fp32 [B,H] -> dh fp32 [B*L,H] (+=), dt bf16 [B*L,Hh]
+ * (= dscore*w2, before tanh'), dw2 fp32 [Hh] (+=), db2 fp32 [1] (+=). */
+int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float* weights, const float* dpooled,
+                      int B, int L, int Hh, int H, float* dh, void* dt, float* dw2, float* db2, void* stream);
+
+/* CrossModalAttention with a single query vector per sample
+ * (ref:training/trainer_unfreeze.py:125-168 called with x.unsqueeze(1) at :653-667):
+ * q fp32 [B,P]; k,v bf16 [B*S, P] (row stride ldkv); mask int32 [B*S] (NULL = all);
+ * nh heads of P/nh; softmax(q·kᵀ·scale, masked -1e9), dropout, ·v -> out fp32 [B,P].
+ * probs fp32 [B*nh*S] saved for backward. */
+int ste_xattn1_fwd(const float* q, const void* k, const void* v, int64_t ldkv, const int32_t* mask, int B, int S,
+                   int P, int nh, float scale, float drop_p, uint64_t seed, float* probs, float* out, void* stream);
+int ste_xattn1_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs, const float* dout,
+                   int B, int S, int P, int nh, float scale, float drop_p, uint64_t seed, float* dq, float* dk,
+                   float* dv, void* stream);
+
+/* ------------------------------------------------------------------- loss --
+ * F.normalize(p=2, dim=1, eps=1e-12) rows (ref:training/trainer_unfreeze.py:561-563). */
+int ste_l2norm_fwd(const float* x, int rows, int cols, float* y, float* norms, void* stream);
+int ste_l2norm_bwd(const float* y, const float* norms, const float* dy, int rows, int cols, float* dx,
+                   void* stream);
+/* Batch similarity matrix S = A·[Tpos;Tneg]ᵀ in exact fp32 on the f32 MFMA
+ * (v_mfma_f32_32x32x2_f32): a [B,P], t [2B,P] -> S [B,2B].  s_pos = diag(S[:, :B]),
+ * s_neg = diag(S[:, B:]) reproduce ref:training/trainer_unfreeze.py:1073-1074. */
+int ste_similarity(const float* a, const float* t, int B, int NT, int P, float* S, void* stream);
+/* AlignmentAwareInfoNCE (ref:training/trainer_unfreeze.py:702-742):
+ * loss = mean_i softplus((s_neg-s_pos)/tau) * (1 - aw*sigmoid(mean_l align[i,l]))
+ *        + gamma*mean_i relu(s_neg).  s_pos/s_neg are read from S's diagonals
+ * (ldS = row stride, pos at column i, neg at column off_neg+i); align may be NULL.
+ * Backward writes ds_pos, ds_neg [B] and dalign [B*L] (optional), scaled by gscale. */
+int ste_pair_loss_fwd(const float* S, int64_t ldS, int off_neg, const float* align, int B, int L, float tau,
+                      float aw, float gamma, float* s_pos, float* s_neg, float* loss, void* stream);
+int ste_pair_loss_bwd(const float* s_pos, const float* s_neg, const float* align, int B, int L, float tau,
+                      float aw, float gamma, const float* gscale, float* ds_pos, float* ds_neg, float* dalign,
+                      void* stream);
+
+/* --------------------------------------------------------------- embedding --
+ * XLMRobertaEmbeddings (tf:…xlm_roberta…:75-121,142-155): position ids
+ * cumsum(ids!=pad)*(ids!=pad)+pad, word+pos+type(0) gather.  Output fp32 sum
+ * [B*L, D] (LayerNorm runs through ste_layernorm_fwd).  pos_ids int32 [B*L] saved. */
+int ste_text_embed_fwd(const int64_t* ids, int B, int L, int D, int pad_idx, const float* word, const float* pos,
+                       const float* type0, float* out, int32_t* pos_ids, void* stream);
+/* Backward scatter-add (nn.Embedding padding_idx rows get no gradient). */
+int ste_text_embed_bwd(const int64_t* ids, const int32_t* pos_ids, const float* dout, int B, int L, int D,
+                       int pad_idx, float* dword, float* dpos, float* dtype0, void* stream);
+
+/* ------------------------------------------------------------- optimizer --
+ * torch.nn.utils.clip_grad_norm_ + torch.optim.AdamW.step
+ * (ref:training/trainer_unfreeze.py:1108-1110, groups :1487-1511).
+ * ste_sumsq accumulates Σg² of n fp32 values into *acc (fp32 atomics).
+ * ste_adamw: reads clip coefficient min(1, max_norm/(sqrt(*sumsq)+1e-6)) on device
+ * when sumsq != NULL, then decoupled-decay AdamW; writes bf16 shadow if non-NULL. */
+int ste_sumsq(const float* g, int64_t n, float* acc, void* stream);
+int ste_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
+              float beta2, float eps, float wd, int step, const float* sumsq, float max_norm, void* stream);
+
+/* ------------------------------------------------------------ elementwise -- */
+int ste_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+/* y[r, c] = x[r, c] * scale[r]  (fp32, row stride ld) */
+int ste_scale_rows(float* x, const float* scale, int64_t rows, int cols, int64_t ld, void* stream);
+int ste_mask_i64_to_f32(const int64_t* m, float* f, int32_t* i32, int64_t n, void* stream);
+
+const char* ste_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STE_H_ */

@@ -1,0 +1,102 @@
+// Device-side helpers shared by every ste kernel (gfx950 / CDNA4 only).
+//
+// Conventions used throughout csrc/:
+//   * activations that feed MFMA are bf16 (`bf16` = clang's __bf16), accumulation is fp32;
+//   * the residual stream, LayerNorm statistics, softmax and loss math are fp32;
+//   * a wavefront is 64 lanes (never 32);
+//   * every launcher takes the HIP stream it must run on and never synchronises.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define STE_WAVE 64
+#define STE_DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------- conversions
+STE_DEV float bf2f(bf16 x) { return (float)x; }
+STE_DEV bf16 f2bf(float x) { return (bf16)x; }  // RNE, NaN-preserving (v_cvt_pk_bf16_f32)
+
+STE_DEV f32x4 load_bf16x4(const bf16* p) {
+  bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+STE_DEV void store_bf16x4(bf16* p, f32x4 v) {
+  bf16x4 o;
+  o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
+  *reinterpret_cast<bf16x4*>(p) = o;
+}
+
+// ---------------------------------------------------------------- wave reductions
+STE_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+STE_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+STE_DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------- activations
+STE_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+STE_DEV float swish_f(float x) { return x * sigmoidf_(x); }
+STE_DEV float swish_d(float x) {
+  float s = sigmoidf_(x);
+  return s * (1.0f + x * (1.0f - s));
+}
+// exact erf GELU (torch nn.GELU() default, approximate='none')
+STE_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+STE_DEV float gelu_d(float x) {
+  float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// ---------------------------------------------------------------- dropout RNG
+// Counter-based: keep(seed, idx) is a pure function, so backward regenerates the
+// forward mask bit-for-bit without storing it.  murmur3 fmix64 on (seed, idx).
+STE_DEV uint32_t ste_hash(uint64_t seed, uint64_t idx) {
+  uint64_t x = seed ^ (idx * 0x9E3779B97F4A7C15ull);
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+// returns scale (0 or 1/(1-p)) for element idx
+STE_DEV float drop_scale(uint64_t seed, uint64_t idx, uint32_t thresh, float inv_keep) {
+  return ste_hash(seed, idx) >= thresh ? inv_keep : 0.0f;
+}
+
+// ---------------------------------------------------------------- MFMA wrappers
+STE_DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// ds_read_b64_tr_b16: see cdna_hip_programming.md T10.  Within each 16-lane group,
+// lane 4q+p passes the address of row q, columns 4p..4p+3; lane i receives
+// column i of the 4 rows (row q in element q).
+STE_DEV s16x4 ds_read_tr16(const void* lds_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_ptr));
+}
+STE_DEV bf16x8 join_tr(s16x4 lo, s16x4 hi) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+#define STE_CHECK_LAUNCH() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)

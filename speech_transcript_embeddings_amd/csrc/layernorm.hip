@@ -1,0 +1,194 @@
+// LayerNorm forward/backward, one wavefront per row, fp32 statistics.
+// Replaces nn.LayerNorm in both encoders and the heads (see include/ste.h).
+// HBM-bound: forward reads x once and writes y once; backward reads dy, x once.
+// Rows are processed grid-stride so the dgamma/dbeta partials of a whole block
+// are reduced in LDS and flushed with one atomic per column per block.
+#include "common.h"
+#include "../../include/ste.h"
+
+namespace {
+
+constexpr int NT = 256;  // 4 waves = 4 rows in flight per block
+
+template <int MAXC>
+STE_DEV void load_row(const void* base, bool is_bf16, int64_t ld, int row, int cols, int lane, float (&v)[MAXC * 4]) {
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int col = (lane + c * 64) * 4;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (col < cols) {
+      if (is_bf16) x = load_bf16x4((const bf16*)base + (int64_t)row * ld + col);
+      else x = *reinterpret_cast<const f32x4*>((const float*)base + (int64_t)row * ld + col);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[c * 4 + e] = x[e];
+  }
+}
+
+template <int MAXC>
+__global__ __launch_bounds__(NT) void ln_fwd_kernel(ste_ln_fwd_args a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * (NT / 64);
+  const float inv_n = 1.0f / (float)a.cols;
+  const uint32_t thresh = (uint32_t)(a.drop_p * 4294967296.0);
+  const float inv_keep = a.drop_p > 0.f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  for (int row = wave; row < a.rows; row += nwaves) {
+    float v[MAXC * 4];
+    load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, v);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXC * 4; ++i) s += v[i];
+    const float mean = wave_sum(s) * inv_n;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      int col = (lane + c * 64) * 4;
+      if (col < a.cols) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { float d = v[c * 4 + e] - mean; q += d * d; }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(q) * inv_n + a.eps);
+    if (lane == 0) { a.mean[row] = mean; a.rstd[row] = rstd; }
+    const float rs = a.row_scale ? a.row_scale[row] : 1.0f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      int col = (lane + c * 64) * 4;
+      if (col >= a.cols) continue;
+      f32x4 g = *reinterpret_cast<const f32x4*>(a.gamma + col);
+      f32x4 b = *reinterpret_cast<const f32x4*>(a.beta + col);
+      f32x4 y;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = ((v[c * 4 + e] - mean) * rstd * g[e] + b[e]) * rs;
+        if (a.act == STE_ACT_SWISH) t = swish_f(t);
+        if (a.drop_p > 0.f) t *= drop_scale(a.seed, (uint64_t)row * a.cols + col + e, thresh, inv_keep);
+        y[e] = t;
+      }
+      if (a.y) *reinterpret_cast<f32x4*>(a.y + (int64_t)row * a.ldy + col) = y;
+      if (a.yb) store_bf16x4((bf16*)a.yb + (int64_t)row * a.ldyb + col, y);
+    }
+  }
+}
+
+template <int MAXC>
+__global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
+  __shared__ float red[2][NT / 64][MAXC * 4 * 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wave = blockIdx.x * (NT / 64) + wid;
+  const int nwaves = gridDim.x * (NT / 64);
+  const float inv_n = 1.0f / (float)a.cols;
+  const uint32_t thresh = (uint32_t)(a.drop_p * 4294967296.0);
+  const float inv_keep = a.drop_p > 0.f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  const uint32_t in_thresh = (uint32_t)(a.in_drop_p * 4294967296.0);
+  const float in_inv_keep = a.in_drop_p > 0.f ? 1.0f / (1.0f - a.in_drop_p) : 1.0f;
+  float dg[MAXC * 4], db[MAXC * 4];
+#pragma unroll
+  for (int i = 0; i < MAXC * 4; ++i) { dg[i] = 0.f; db[i] = 0.f; }
+
+  for (int row = wave; row < a.rows; row += nwaves) {
+    float x[MAXC * 4], g[MAXC * 4];
+    load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, x);
+    load_row<MAXC>(a.dy, a.dy_bf16, a.lddy, row, a.cols, lane, g);
+    const float mean = a.mean[row], rstd = a.rstd[row];
+    const float rs = a.row_scale ? a.row_scale[row] : 1.0f;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      int col = (lane + c * 64) * 4;
+      if (col >= a.cols) continue;
+      f32x4 gm = *reinterpret_cast<const f32x4*>(a.gamma + col);
+      f32x4 bt = {0.f, 0.f, 0.f, 0.f};
+      if (a.act == STE_ACT_SWISH) bt = *reinterpret_cast<const f32x4*>(a.beta + col);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = c * 4 + e;
+        const float xh = (x[i] - mean) * rstd;
+        float gi = g[i];
+        if (a.in_drop_p > 0.f) gi *= drop_scale(a.in_seed, (uint64_t)row * a.cols + col + e, in_thresh, in_inv_keep);
+        if (a.act == STE_ACT_SWISH) gi *= swish_d((xh * gm[e] + bt[e]) * rs);
+        gi *= rs;
+        dg[i] += gi * xh;
+        db[i] += gi;
+        const float gg = gi * gm[e];
+        g[i] = gg;
+        x[i] = xh;
+        s1 += gg;
+        s2 += gg * xh;
+      }
+    }
+    s1 = wave_sum(s1) * inv_n;
+    s2 = wave_sum(s2) * inv_n;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      int col = (lane + c * 64) * 4;
+      if (col >= a.cols) continue;
+      f32x4 d;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = c * 4 + e;
+        d[e] = rstd * (g[i] - s1 - x[i] * s2);
+      }
+      if (a.dres) d += *reinterpret_cast<const f32x4*>(a.dres + (int64_t)row * a.lddres + col);
+      if (a.dx) *reinterpret_cast<f32x4*>(a.dx + (int64_t)row * a.lddx + col) = d;
+      if (a.dxb) {
+        f32x4 o = d * a.out_scale;
+        if (a.drop_p > 0.f) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] *= drop_scale(a.seed, (uint64_t)row * a.cols + col + e, thresh, inv_keep);
+        }
+        store_bf16x4((bf16*)a.dxb + (int64_t)row * a.lddxb + col, o);
+      }
+    }
+  }
+  if (!a.dgamma) return;
+#pragma unroll
+  for (int i = 0; i < MAXC * 4; ++i) {
+    red[0][wid][(i >> 2) * 256 + lane * 4 + (i & 3)] = dg[i];
+    red[1][wid][(i >> 2) * 256 + lane * 4 + (i & 3)] = db[i];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < MAXC * 256; j += NT) {
+    // j = c*256 + lane*4 + e  -> column (lane + c*64)*4 + e
+    const int c = j >> 8, rem = j & 255;
+    const int col = (c * 64 + (rem >> 2)) * 4 + (rem & 3);
+    if (col >= a.cols) continue;
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) { sg += red[0][w][j]; sb += red[1][w][j]; }
+    atomicAdd(a.dgamma + col, sg);
+    if (a.dbeta) atomicAdd(a.dbeta + col, sb);
+  }
+}
+
+inline int grid_for(int rows) {
+  int g = (rows + 3) / 4;
+  return g < 1024 ? g : 1024;
+}
+
+}  // namespace
+
+extern "C" int ste_layernorm_fwd(const ste_ln_fwd_args* a, void* stream) {
+  if (!a || a->rows <= 0 || a->cols <= 0 || (a->cols & 3) || a->cols > 2048 || !a->mean || !a->rstd)
+    return STE_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(grid_for(a->rows));
+  if (a->cols <= 256) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(NT), 0, s, *a);
+  else if (a->cols <= 1024) hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(NT), 0, s, *a);
+  else hipLaunchKernelGGL(ln_fwd_kernel<8>, grid, dim3(NT), 0, s, *a);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_layernorm_bwd(const ste_ln_bwd_args* a, void* stream) {
+  if (!a || a->rows <= 0 || a->cols <= 0 || (a->cols & 3) || a->cols > 1024) return STE_ERR_ARG;
+  if (a->act == STE_ACT_SWISH && !a->beta) return STE_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  int g = (a->rows + 3) / 4;
+  if (g > 256) g = 256;
+  if (a->cols <= 256) hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(g), dim3(NT), 0, s, *a);
+  else hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(g), dim3(NT), 0, s, *a);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
