@@ -341,3 +341,98 @@ def linear_warmup_lr(base_lr, step, warmup, total):
     if step < warmup:
         return base_lr * step / max(1, warmup)
     return base_lr * max(0.0, (total - step) / max(1, total - warmup))
+
+
+# ------------------------------------------------------- module-tree shapes
+def param_shapes(cfg: ModelCfg, spec_augment: bool = True):
+    """Ordered (state_dict key, shape) of the reference EnhancedAudioTextModel (ref:315-491 +
+    XLMRobertaModel / Wav2Vec2BertModel trees).  spec_augment: w2v config has mask_time_prob>0
+    (w2v:930-931 creates masked_spec_embed)."""
+    t, a, P = cfg.text, cfg.audio, cfg.projection_dim
+    out = []
+    add = lambda n, *s: out.append((n, tuple(s)))  # noqa: E731
+    e = "text_encoder.embeddings."
+    add(e + "word_embeddings.weight", t.vocab, t.hidden)
+    add(e + "token_type_embeddings.weight", 1, t.hidden)
+    add(e + "LayerNorm.weight", t.hidden); add(e + "LayerNorm.bias", t.hidden)
+    add(e + "position_embeddings.weight", t.max_pos, t.hidden)
+    for i in range(t.layers):
+        pre = f"text_encoder.encoder.layer.{i}."
+        for n in ("query", "key", "value"):
+            add(pre + f"attention.self.{n}.weight", t.hidden, t.hidden); add(pre + f"attention.self.{n}.bias", t.hidden)
+        add(pre + "attention.output.dense.weight", t.hidden, t.hidden); add(pre + "attention.output.dense.bias", t.hidden)
+        add(pre + "attention.output.LayerNorm.weight", t.hidden); add(pre + "attention.output.LayerNorm.bias", t.hidden)
+        add(pre + "intermediate.dense.weight", t.inter, t.hidden); add(pre + "intermediate.dense.bias", t.inter)
+        add(pre + "output.dense.weight", t.hidden, t.inter); add(pre + "output.dense.bias", t.hidden)
+        add(pre + "output.LayerNorm.weight", t.hidden); add(pre + "output.LayerNorm.bias", t.hidden)
+    add("text_encoder.pooler.dense.weight", t.hidden, t.hidden); add("text_encoder.pooler.dense.bias", t.hidden)
+    if spec_augment:
+        add("audio_encoder.masked_spec_embed", a.hidden)
+    f = "audio_encoder.feature_projection."
+    add(f + "layer_norm.weight", a.feat_in); add(f + "layer_norm.bias", a.feat_in)
+    add(f + "projection.weight", a.hidden, a.feat_in); add(f + "projection.bias", a.hidden)
+    dh = a.hidden // a.heads
+    for i in range(a.layers):
+        pre = f"audio_encoder.encoder.layers.{i}."
+        ln = lambda n: (add(pre + n + ".weight", a.hidden), add(pre + n + ".bias", a.hidden))  # noqa: E731
+        ln("ffn1_layer_norm")
+        add(pre + "ffn1.intermediate_dense.weight", a.inter, a.hidden); add(pre + "ffn1.intermediate_dense.bias", a.inter)
+        add(pre + "ffn1.output_dense.weight", a.hidden, a.inter); add(pre + "ffn1.output_dense.bias", a.hidden)
+        ln("self_attn_layer_norm")
+        for n in ("linear_q", "linear_k", "linear_v", "linear_out"):
+            add(pre + f"self_attn.{n}.weight", a.hidden, a.hidden); add(pre + f"self_attn.{n}.bias", a.hidden)
+        add(pre + "self_attn.distance_embedding.weight", a.left + a.right + 1, dh)
+        ln("conv_module.layer_norm")
+        add(pre + "conv_module.pointwise_conv1.weight", 2 * a.hidden, a.hidden, 1)
+        add(pre + "conv_module.depthwise_conv.weight", a.hidden, 1, a.conv_k)
+        ln("conv_module.depthwise_layer_norm")
+        add(pre + "conv_module.pointwise_conv2.weight", a.hidden, a.hidden, 1)
+        ln("ffn2_layer_norm")
+        add(pre + "ffn2.intermediate_dense.weight", a.inter, a.hidden); add(pre + "ffn2.intermediate_dense.bias", a.inter)
+        add(pre + "ffn2.output_dense.weight", a.hidden, a.inter); add(pre + "ffn2.output_dense.bias", a.hidden)
+        ln("final_layer_norm")
+    for side, H in (("text", t.hidden), ("audio", a.hidden)):
+        pre = f"{side}_projection.projection."
+        add(pre + "0.weight", 2 * P, H); add(pre + "0.bias", 2 * P)
+        add(pre + "3.weight", P, 2 * P); add(pre + "3.bias", P)
+        add(pre + "4.weight", P); add(pre + "4.bias", P)
+    if cfg.use_cross_modal:
+        add("text_seq_to_projection.weight", P, t.hidden); add("text_seq_to_projection.bias", P)
+        add("audio_seq_to_projection.weight", P, a.hidden); add("audio_seq_to_projection.bias", P)
+        for m in ("text_to_audio_attention", "audio_to_text_attention"):
+            for n in ("query", "key", "value", "out_proj"):
+                add(f"{m}.{n}.weight", P, P); add(f"{m}.{n}.bias", P)
+        for m in ("text_fusion", "audio_fusion"):
+            add(f"{m}.0.weight", P, 2 * P); add(f"{m}.0.bias", P)
+            add(f"{m}.1.weight", P); add(f"{m}.1.bias", P)
+    if cfg.use_attentive_pooling:
+        for side, H in (("text", t.hidden), ("audio", a.hidden)):
+            pre = f"{side}_pooling.attention."
+            add(pre + "0.weight", H // 2, H); add(pre + "0.bias", H // 2)
+            add(pre + "2.weight", 1, H // 2); add(pre + "2.bias", 1)
+    if cfg.use_word_alignment:
+        w = "word_level_alignment."
+        add(w + "text_projection.weight", P, t.hidden); add(w + "text_projection.bias", P)
+        add(w + "audio_projection.weight", P, a.hidden); add(w + "audio_projection.bias", P)
+        add(w + "alignment_attention.in_proj_weight", 3 * P, P); add(w + "alignment_attention.in_proj_bias", 3 * P)
+        add(w + "alignment_attention.out_proj.weight", P, P); add(w + "alignment_attention.out_proj.bias", P)
+        add(w + "output_projection.weight", P, P); add(w + "output_projection.bias", P)
+        add(w + "layer_norm.weight", P); add(w + "layer_norm.bias", P)
+        add(w + "alignment_confidence.0.weight", P // 2, P); add(w + "alignment_confidence.0.bias", P // 2)
+        add(w + "alignment_confidence.2.weight", 1, P // 2); add(w + "alignment_confidence.2.bias", 1)
+    return out
+
+
+def mini_cfg(golden_json: dict) -> ModelCfg:
+    m = golden_json["mini"]
+    au, tx = m["audio"], m["text"]
+    return ModelCfg(
+        audio=AudioCfg(hidden=au["hidden_size"], layers=au["num_hidden_layers"], heads=au["num_attention_heads"],
+                       inter=au["intermediate_size"], feat_in=au["feature_projection_input_dim"],
+                       left=au["left_max_position_embeddings"], right=au["right_max_position_embeddings"],
+                       conv_k=au["conv_depthwise_kernel_size"]),
+        text=TextCfg(hidden=tx["hidden_size"], layers=tx["num_hidden_layers"], heads=tx["num_attention_heads"],
+                     inter=tx["intermediate_size"], vocab=tx["vocab_size"], max_pos=tx["max_position_embeddings"],
+                     pad_id=tx["pad_token_id"]),
+        projection_dim=m["projection_dim"], use_word_alignment=golden_json["use_word_alignment"],
+        text_layers_to_unfreeze=m["unfreeze"], audio_layers_to_unfreeze=m["unfreeze"])

@@ -1,0 +1,137 @@
+"""Pin the CPU oracle (oracle/) to the reference's own outputs (tests/golden/, made by
+tests/golden/make_golden.py from /root/reference + transformers in the build container)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import det_init, fbank_ref, ref_model as R
+
+
+# ------------------------------------------------------------------ fbank
+@pytest.fixture(scope="module")
+def fb():
+    return np.load(GOLDEN / "fbank_golden.npz")
+
+
+@pytest.mark.parametrize("case", ["2s", "odd", "short", "1p3s"])
+def test_fbank_oracle_matches_reference_extractor(fb, case):
+    feats, mask = fbank_ref.extract(fb[f"{case}_wave"], padding_value=1.0)
+    ref_f, ref_m = fb[f"{case}_feats"], fb[f"{case}_mask"]
+    assert feats.shape == ref_f.shape
+    np.testing.assert_array_equal(mask, ref_m)
+    np.testing.assert_allclose(feats, ref_f, atol=2e-4, rtol=0)
+
+
+def test_fbank_oracle_collate_matches_reference(fb):
+    items = [fbank_ref.extract(fb[f"{c}_wave"])[0] for c in fb["cases"]]
+    feats, mask = fbank_ref.collate(items)
+    np.testing.assert_array_equal(mask, fb["batch_mask"])
+    np.testing.assert_allclose(feats, fb["batch_feats"], atol=2e-4, rtol=0)
+
+
+def test_num_stacked_frames_survey_values():
+    assert fbank_ref.num_stacked_frames(32000) == 99
+    assert fbank_ref.num_stacked_frames(160000) == 499
+    assert fbank_ref.num_stacked_frames(480000) == 1499
+
+
+# ------------------------------------------------------------------ model
+def _load(tag):
+    meta = json.loads((GOLDEN / f"model_golden_{tag}.json").read_text())
+    return meta, np.load(GOLDEN / f"model_golden_{tag}.npz")
+
+
+def oracle_params(cfg, requires_grad_names=()):
+    shapes = R.param_shapes(cfg, spec_augment=False)
+    vals = det_init.state_dict_values(shapes)
+    return {n: torch.from_numpy(v).requires_grad_(n in requires_grad_names) for n, v in vals.items()}
+
+
+def golden_batch(z):
+    keys = ["input_ids_pos", "attention_mask_pos", "input_ids_neg", "attention_mask_neg", "input_values",
+            "attention_mask_audio"]
+    return {k: torch.from_numpy(z[k]) for k in keys}
+
+
+@pytest.mark.parametrize("tag", ["noalign", "align"])
+def test_param_tree_matches_reference(tag):
+    meta, _ = _load(tag)
+    cfg = R.mini_cfg(meta)
+    names = [n for n, _ in R.param_shapes(cfg, spec_augment=False)]
+    assert names == meta["names"]
+    trainable = R.trainable_names(names, cfg)
+    assert sorted(trainable) == sorted(meta["trainable"])
+
+
+def test_full_size_param_counts_match_reference_logs():
+    """training.log:857 (877,571,651 total / 305,994,755 trainable) and :486 (368,531,075 at k=5)."""
+    counts = json.loads((GOLDEN / "param_counts.json").read_text())
+    for key, (align, k) in {"align=False,k=3": (False, 3), "align=True,k=3": (True, 3),
+                            "align=True,k=5": (True, 5)}.items():
+        cfg = R.ModelCfg(use_word_alignment=align, text_layers_to_unfreeze=k, audio_layers_to_unfreeze=k)
+        shapes = R.param_shapes(cfg, spec_augment=True)
+        ref = counts[key]
+        assert [n for n, _ in shapes] == list(ref["shapes"])
+        assert all(list(s) == ref["shapes"][n] for n, s in shapes)
+        total = sum(int(np.prod(s)) for _, s in shapes)
+        tr = R.trainable_names([n for n, _ in shapes], cfg)
+        assert total == ref["total"]
+        assert sorted(tr) == sorted(ref["trainable_names"])
+
+
+@pytest.mark.parametrize("tag", ["noalign", "align"])
+def test_model_oracle_matches_reference(tag):
+    meta, z = _load(tag)
+    cfg = R.mini_cfg(meta)
+    p = oracle_params(cfg, set(meta["trainable"]))
+    batch = golden_batch(z)
+    loss, s_pos, s_neg, (tpn, tnn, an, align) = R.step_loss(p, batch, cfg)
+    np.testing.assert_allclose(tpn.detach().numpy(), z["txt_pos"], atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(tnn.detach().numpy(), z["txt_neg"], atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(an.detach().numpy(), z["aud"], atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(s_pos.detach().numpy(), z["s_pos"], atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(loss.item(), float(z["loss"]), rtol=1e-5)
+    if "align" in z:
+        np.testing.assert_allclose(align.detach().numpy(), z["align"], atol=2e-6, rtol=1e-5)
+    loss.backward()
+    with_grad = set(meta["with_grad"])
+    for n, t in p.items():
+        if n not in with_grad:
+            assert t.grad is None or not t.requires_grad, n
+            continue
+        g = t.grad.reshape(-1).numpy()
+        gn = np.linalg.norm(g.astype(np.float64))
+        assert abs(gn - float(z[f"gnorm::{n}"])) <= 1e-4 * max(1.0, gn), n
+        idx = det_init.sample_indices(n, g.size)
+        np.testing.assert_allclose(g[idx], z[f"gsamp::{n}"], atol=1e-6, rtol=1e-4, err_msg=n)
+
+
+@pytest.mark.parametrize("tag", ["noalign", "align"])
+def test_optimizer_oracle_matches_reference(tag):
+    """clip_grad_norm_(1.0) + two-group AdamW at scheduler step 1 (ref:1108-1113, 1487-1541)."""
+    meta, z = _load(tag)
+    cfg = R.mini_cfg(meta)
+    p = oracle_params(cfg, set(meta["trainable"]))
+    loss, *_ = R.step_loss(p, golden_batch(z), cfg)
+    loss.backward()
+    grads = {n: t.grad for n, t in p.items() if t.grad is not None}
+    total = float(torch.sqrt(sum((g.double() ** 2).sum() for g in grads.values())))
+    np.testing.assert_allclose(total, float(z["clip_total_norm"]), rtol=1e-5)
+    coef = min(1.0, 1.0 / (total + 1e-6))
+    lr_enc = R.linear_warmup_lr(meta["lr"] / 50, meta["sched_step"], meta["warmup"], meta["total_steps"])
+    lr_head = R.linear_warmup_lr(meta["lr"], meta["sched_step"], meta["warmup"], meta["total_steps"])
+    np.testing.assert_allclose([lr_enc, lr_head], [float(z["lr_enc"]), float(z["lr_head"])], rtol=1e-12)
+    for n, g in grads.items():
+        lr = lr_enc if ("text_encoder" in n or "audio_encoder" in n) else lr_head
+        pn, _, _ = R.adamw_step(p[n].detach(), g * coef, torch.zeros_like(g), torch.zeros_like(g), lr=lr, step=1)
+        idx = det_init.sample_indices(n, pn.numel())
+        # analytically-zero gradient entries (attention key biases: softmax shift invariance) are
+        # rounding noise that Adam normalises to ±lr, so for them only the bound is reproducible.
+        noise = np.abs(z[f"gsamp::{n}"]) < 1e-6
+        decayed = p[n].detach().reshape(-1).numpy()[idx] * (1 - lr * 0.01)
+        assert np.all(np.abs(z[f"pnew::{n}"][noise] - decayed[noise]) <= lr * 1.001 + 1e-7), n
+        np.testing.assert_allclose(pn.reshape(-1).numpy()[idx][~noise], z[f"pnew::{n}"][~noise], atol=1e-6,
+                                   rtol=1e-5, err_msg=n)
