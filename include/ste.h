@@ -32,7 +32,7 @@ extern "C" {
  * C = epilogue(alpha * A.B), bf16 operands, fp32 accumulation.
  *   a_kc=1: A[m*lda+k]   a_kc=0: A[k*lda+m]
  *   b_kc=1: B[n*ldb+k]   b_kc=0: B[k*ldb+n]
- * Epilogue, in order: v = alpha*acc + bias[n];
+ * Epilogue, in order: v = alpha*(acc + bias[n]);
  *   act in {SWISH,GELU,TANH,RELU}: C2 <- v (bf16, pre-activation, optional); v = act(v)
  *   act in {*_BWD}: v *= act'(Z[m,n])           (Z: bf16, row stride ldz)
  *   drop_p>0: v *= keep(seed, m*drop_ld+n)/(1-drop_p)
@@ -117,6 +117,9 @@ typedef struct {
   float* dgamma; float* dbeta;
   float drop_p; uint64_t seed; float out_scale;   /* dropout/scale applied to the dxb copy only */
   float in_drop_p; uint64_t in_seed;              /* forward output dropout to undo on dy */
+  const float* out_row_scale;                     /* multiplies the dxb copy rows (optional) */
+  float* dsum;                                    /* += column sums of the dxb values (fp32, optional):
+                                                     the bias gradient of the Linear feeding this residual */
 } ste_ln_bwd_args;
 int ste_layernorm_bwd(const ste_ln_bwd_args* a, void* stream);
 
@@ -150,6 +153,7 @@ typedef struct {
   void* dv; int64_t lddv;
   float* delta;       /* workspace [B*H*T] */
   float* dE;          /* fp32 [left+right+1, 64], accumulated (may be NULL) */
+  float* gwork;       /* workspace [B*H*T*80] fp32, required when dE != NULL */
 } ste_attn_args;
 int ste_attention_fwd(const ste_attn_args* a, void* stream);
 int ste_attention_bwd(const ste_attn_args* a, void* stream);
@@ -188,7 +192,8 @@ int ste_attn_pool_fwd(const void* t, const float* w2, const float* b2, const voi
                       int B, int L, int Hh, int H, float* weights, float* pooled, void* pooled_bf16,
                       void* stream);
 /* Backward: dpooled fp32 [B,H] -> dh fp32 [B*L,H] (+=), dt bf16 [B*L,Hh]
- * (= dscore*w2, before tanh'), dw2 fp32 [Hh] (+=), db2 fp32 [1] (+=). */
+ * (= dscore*w2*(1-t^2): the gradient at the scorer's first Linear output, tanh'
+ * included), dw2 fp32 [Hh] (+=), db2 fp32 [1] (+=). */
 int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float* weights, const float* dpooled,
                       int B, int L, int Hh, int H, float* dh, void* dt, float* dw2, float* db2, void* stream);
 
@@ -222,6 +227,9 @@ int ste_pair_loss_fwd(const float* S, int64_t ldS, int off_neg, const float* ali
 int ste_pair_loss_bwd(const float* s_pos, const float* s_neg, const float* align, int B, int L, float tau,
                       float aw, float gamma, const float* gscale, float* ds_pos, float* ds_neg, float* dalign,
                       void* stream);
+/* Gradients of s_pos[i] = <a_i, tp_i>, s_neg[i] = <a_i, tn_i> (the diagonals of S). */
+int ste_pair_sim_bwd(const float* a, const float* tp, const float* tn, const float* ds_pos, const float* ds_neg,
+                     int B, int P, float* da, float* dtp, float* dtn, void* stream);
 
 /* --------------------------------------------------------------- embedding --
  * XLMRobertaEmbeddings (tf:…xlm_roberta…:75-121,142-155): position ids
@@ -236,15 +244,17 @@ int ste_text_embed_bwd(const int64_t* ids, const int32_t* pos_ids, const float* 
 /* ------------------------------------------------------------- optimizer --
  * torch.nn.utils.clip_grad_norm_ + torch.optim.AdamW.step
  * (ref:training/trainer_unfreeze.py:1108-1110, groups :1487-1511).
- * ste_sumsq accumulates Σg² of n fp32 values into *acc (fp32 atomics).
+ * ste_sumsq accumulates Σg² of n fp32 values into *acc (fp64 atomics).
  * ste_adamw: reads clip coefficient min(1, max_norm/(sqrt(*sumsq)+1e-6)) on device
  * when sumsq != NULL, then decoupled-decay AdamW; writes bf16 shadow if non-NULL. */
-int ste_sumsq(const float* g, int64_t n, float* acc, void* stream);
+int ste_sumsq(const float* g, int64_t n, double* acc, void* stream);
 int ste_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
-              float beta2, float eps, float wd, int step, const float* sumsq, float max_norm, void* stream);
+              float beta2, float eps, float wd, int step, const double* sumsq, float max_norm, void* stream);
 
 /* ------------------------------------------------------------ elementwise -- */
 int ste_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+/* out[c] += Σ_r x[r, c] over a row-major [rows, cols] fp32/bf16 matrix (bias gradients). */
+int ste_colsum(const void* x, int is_bf16, int64_t rows, int cols, int64_t ld, float* out, void* stream);
 /* y[r, c] = x[r, c] * scale[r]  (fp32, row stride ld) */
 int ste_scale_rows(float* x, const float* scale, int64_t rows, int cols, int64_t ld, void* stream);
 int ste_mask_i64_to_f32(const int64_t* m, float* f, int32_t* i32, int64_t n, void* stream);

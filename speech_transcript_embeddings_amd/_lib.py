@@ -76,6 +76,8 @@ class LnBwdArgs(C.Structure):
         ("dgamma", c_void_p), ("dbeta", c_void_p),
         ("drop_p", c_float), ("seed", c_uint64), ("out_scale", c_float),
         ("in_drop_p", c_float), ("in_seed", c_uint64),
+        ("out_row_scale", c_void_p),
+        ("dsum", c_void_p),
     ]
 
 
@@ -97,6 +99,7 @@ class AttnArgs(C.Structure):
         ("dv", c_void_p), ("lddv", c_int64),
         ("delta", c_void_p),
         ("dE", c_void_p),
+        ("gwork", c_void_p),
     ]
 
 
@@ -127,6 +130,8 @@ _SIGS = {
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     "ste_pair_loss_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ste_pair_sim_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                 c_void_p, c_void_p]),
     "ste_text_embed_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
     "ste_text_embed_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
@@ -135,6 +140,7 @@ _SIGS = {
     "ste_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                           c_float, c_float, c_int, c_void_p, c_float, c_void_p]),
     "ste_cast_f32_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "ste_colsum": (c_int, [c_void_p, c_int, c_int64, c_int, c_int64, c_void_p, c_void_p]),
     "ste_scale_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int64, c_void_p]),
     "ste_mask_i64_to_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "ste_version": (C.c_char_p, []),

@@ -1,0 +1,177 @@
+// XLM-R embedding gather / scatter-add and the fused optimizer tail.
+//   embeddings: tf:models/xlm_roberta/modeling_xlm_roberta.py:75-121 (+ position ids :142-155)
+//   clip_grad_norm_ + AdamW: ref:training/trainer_unfreeze.py:1108-1110 with the param
+//   groups of :1487-1511 (torch.optim.AdamW decoupled weight decay, amsgrad=False).
+#include "common.h"
+#include "../../include/ste.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+// one block per sequence: position ids = cumsum(ids != pad) * (ids != pad) + pad
+__global__ __launch_bounds__(NT) void embed_fwd_kernel(const int64_t* ids, int L, int D, int pad, const float* word,
+                                                     const float* pos, const float* type0, float* out,
+                                                     int32_t* pos_ids) {
+  __shared__ int spos[2048];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) {
+    int c = 0;
+    for (int l = 0; l < L; ++l) {
+      const int nz = ids[(int64_t)b * L + l] != pad;
+      c += nz;
+      spos[l] = nz ? c + pad : pad;
+    }
+  }
+  __syncthreads();
+  for (int l = tid; l < L; l += NT) pos_ids[(int64_t)b * L + l] = spos[l];
+  for (int i = tid * 4; i < L * D; i += NT * 4) {
+    const int l = i / D, c = i % D;
+    const int64_t id = ids[(int64_t)b * L + l];
+    f32x4 v = *reinterpret_cast<const f32x4*>(word + id * D + c);
+    v += *reinterpret_cast<const f32x4*>(pos + (int64_t)spos[l] * D + c);
+    v += *reinterpret_cast<const f32x4*>(type0 + c);
+    *reinterpret_cast<f32x4*>(out + ((int64_t)b * L + l) * D + c) = v;
+  }
+}
+
+// rows per block reduce the token-type gradient locally; word/position rows scatter with atomics
+__global__ __launch_bounds__(NT) void embed_bwd_kernel(const int64_t* ids, const int32_t* pos_ids, const float* dout,
+                                                     int rows, int D, int pad, float* dword, float* dpos,
+                                                     float* dtype0, int rows_per_block) {
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  for (int c = threadIdx.x; c < D; c += NT) {
+    float tsum = 0.f;
+    for (int r = r0; r < r1; ++r) {
+      const float g = dout[(int64_t)r * D + c];
+      tsum += g;
+      const int64_t id = ids[r];
+      if (dword && id != pad) atomicAdd(dword + id * D + c, g);
+      const int p = pos_ids[r];
+      if (dpos && p != pad) atomicAdd(dpos + (int64_t)p * D + c, g);
+    }
+    if (dtype0) atomicAdd(dtype0 + c, tsum);
+  }
+}
+
+__global__ __launch_bounds__(NT) void sumsq_kernel(const float* g, int64_t n, double* acc) {
+  __shared__ double red[NT / 64];
+  double s = 0.0;
+  float sf = 0.f;
+  int cnt = 0;
+  for (int64_t i = ((int64_t)blockIdx.x * NT + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * NT * 4) {
+    if (i + 3 < n) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(g + i);
+      sf += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    } else {
+      for (int64_t j = i; j < n; ++j) sf += g[j] * g[j];
+    }
+    if (++cnt == 64) { s += sf; sf = 0.f; cnt = 0; }
+  }
+  s += sf;
+  s = wave_sum_d(s);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < NT / 64; ++i) t += red[i];
+    atomicAdd(acc, t);
+  }
+}
+
+__global__ __launch_bounds__(NT) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                 float* __restrict__ m, float* __restrict__ v, bf16* __restrict__ pb,
+                                                 int64_t n, float lr, float b1, float b2, float eps, float wd,
+                                                 float bc1, float bc2_sqrt, const double* sumsq, float max_norm) {
+  float coef = 1.f;
+  if (sumsq) {
+    const float tn = (float)sqrt(*sumsq);
+    coef = fminf(1.f, max_norm / (tn + 1e-6f));
+  }
+  const float step = lr / bc1;
+  const float decay = 1.f - lr * wd;
+  for (int64_t i = ((int64_t)blockIdx.x * NT + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * NT * 4) {
+    if (i + 3 < n) {
+      f32x4 pv = *reinterpret_cast<f32x4*>(p + i);
+      const f32x4 gv = *reinterpret_cast<const f32x4*>(g + i) * coef;
+      f32x4 mv = *reinterpret_cast<f32x4*>(m + i);
+      f32x4 vv = *reinterpret_cast<f32x4*>(v + i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pv[e] *= decay;
+        mv[e] = b1 * mv[e] + (1.f - b1) * gv[e];
+        vv[e] = b2 * vv[e] + (1.f - b2) * gv[e] * gv[e];
+        pv[e] -= step * mv[e] / (sqrtf(vv[e]) / bc2_sqrt + eps);
+      }
+      *reinterpret_cast<f32x4*>(p + i) = pv;
+      *reinterpret_cast<f32x4*>(m + i) = mv;
+      *reinterpret_cast<f32x4*>(v + i) = vv;
+      if (pb) store_bf16x4(pb + i, pv);
+    } else {
+      for (int64_t j = i; j < n; ++j) {
+        const float gv = g[j] * coef;
+        float pv = p[j] * decay;
+        m[j] = b1 * m[j] + (1.f - b1) * gv;
+        v[j] = b2 * v[j] + (1.f - b2) * gv * gv;
+        pv -= step * m[j] / (sqrtf(v[j]) / bc2_sqrt + eps);
+        p[j] = pv;
+        if (pb) pb[j] = (bf16)pv;
+      }
+    }
+  }
+}
+
+inline unsigned grid_for(int64_t n) {
+  int64_t b = (n / 4 + NT - 1) / NT;
+  if (b > 8192) b = 8192;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+extern "C" int ste_text_embed_fwd(const int64_t* ids, int B, int L, int D, int pad_idx, const float* word,
+                                  const float* pos, const float* type0, float* out, int32_t* pos_ids, void* stream) {
+  if (B <= 0 || L <= 0 || L > 2048 || (D & 3)) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(B), dim3(NT), 0, (hipStream_t)stream, ids, L, D, pad_idx, word, pos, type0,
+                     out, pos_ids);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_text_embed_bwd(const int64_t* ids, const int32_t* pos_ids, const float* dout, int B, int L, int D,
+                                  int pad_idx, float* dword, float* dpos, float* dtype0, void* stream) {
+  const int rows = B * L;
+  if (rows <= 0) return STE_ERR_SHAPE;
+  const int rpb = 32;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3((rows + rpb - 1) / rpb), dim3(NT), 0, (hipStream_t)stream, ids, pos_ids,
+                     dout, rows, D, pad_idx, dword, dpos, dtype0, rpb);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_sumsq(const float* g, int64_t n, double* acc, void* stream) {
+  if (n <= 0) return 0;
+  if (((uintptr_t)g) & 15) return STE_ERR_ARG;
+  unsigned gr = grid_for(n);
+  if (gr > 2048) gr = 2048;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(gr), dim3(NT), 0, (hipStream_t)stream, g, n, acc);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
+                         float beta2, float eps, float wd, int step, const double* sumsq, float max_norm,
+                         void* stream) {
+  if (n <= 0) return 0;
+  if (step < 1) return STE_ERR_ARG;
+  if ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) return STE_ERR_ARG;
+  if (p_bf16 && (((uintptr_t)p_bf16) & 7)) return STE_ERR_ARG;
+  const float bc1 = 1.f - powf(beta1, (float)step);
+  const float bc2s = sqrtf(1.f - powf(beta2, (float)step));
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, p, g, m, v, (bf16*)p_bf16, n,
+                     lr, beta1, beta2, eps, wd, bc1, bc2s, sumsq, max_norm);
+  STE_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,220 @@
+// Batched GPU fbank: the arithmetic of SeamlessM4TFeatureExtractor (w2v-bert-2.0's
+// extractor) that the reference runs per clip on CPU DataLoader workers
+// (ref:training/trainer_unfreeze.py:856-866 -> tf:models/seamless_m4t/
+// feature_extraction_seamless_m4t.py:112-138,240-301, tf:audio_utils.py:809-1017),
+// plus the collate padding of ref:training/trainer_unfreeze.py:880-921.
+//
+// Kernel 1 (one wavefront per 400-sample frame, 4 frames per block):
+//   x*2^15 -> remove frame mean -> pre-emphasis 0.97 (y0 *= 0.03) -> povey window
+//   -> 512-point radix-2 FFT in LDS (fp32, twiddles from double sincos) -> |X|^2
+//   -> 80 kaldi-scale triangular mel filters built in mel space (sparse, per-block
+//   table) -> max(1.1920929e-7, .) -> natural log.
+// Kernel 2 (one block per clip): per-mel-bin mean / unbiased variance over the clip's
+// frames in fp64, (x-mean)/sqrt(var+1e-7), pad odd frame counts with padding_value,
+// stack frame pairs into 160-d rows, zero rows beyond the clip, write the mask.
+// HBM-bound: 4 B/sample in, 640 B per stacked frame + mask out.
+#include "common.h"
+#include "../../include/ste.h"
+
+namespace {
+
+constexpr int FRAME = 400, HOP = 160, NFFT = 512, NBIN = 257, NMEL = 80;
+constexpr int MAXNZ = 640;  // non-zero filter taps (501 for these parameters)
+
+__device__ double hz_to_mel(double f) { return 1127.0 * log(1.0 + f / 700.0); }
+
+__global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restrict__ wav, int64_t ld_wav,
+                                                         const int32_t* __restrict__ lengths, int Fmax,
+                                                         float* __restrict__ work) {
+  __shared__ float2 sbuf[4][NFFT];
+  __shared__ float2 stw[NFFT / 2];
+  __shared__ float swin[FRAME];
+  __shared__ int sm_start[NMEL], sm_len[NMEL], sm_off[NMEL];
+  __shared__ float sm_w[MAXNZ];
+  __shared__ float spow[4][NBIN + 3];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.y;
+  // ---- constant tables (per block; cheap next to the streaming work)
+  for (int k = tid; k < NFFT / 2; k += 256) {
+    double s, c;
+    sincos(-2.0 * M_PI * (double)k / (double)NFFT, &s, &c);
+    stw[k] = make_float2((float)c, (float)s);
+  }
+  for (int n = tid; n < FRAME; n += 256) {
+    const double hann = 0.5 - 0.5 * cos(2.0 * M_PI * (double)n / (double)(FRAME - 1));
+    swin[n] = (float)pow(hann, 0.85);
+  }
+  if (tid == 0) {
+    const double mel_lo = hz_to_mel(20.0), mel_hi = hz_to_mel(8000.0);
+    int off = 0;
+    for (int m = 0; m < NMEL; ++m) {
+      const double f0 = mel_lo + (mel_hi - mel_lo) * m / (NMEL + 1);
+      const double f1 = mel_lo + (mel_hi - mel_lo) * (m + 1) / (NMEL + 1);
+      const double f2 = mel_lo + (mel_hi - mel_lo) * (m + 2) / (NMEL + 1);
+      int start = -1, len = 0;
+      for (int k = 0; k < NBIN; ++k) {
+        const double fk = hz_to_mel(31.25 * k);
+        const double down = (fk - f0) / (f1 - f0), up = (f2 - fk) / (f2 - f1);
+        const double wv = fmax(0.0, fmin(down, up));
+        if (wv > 0.0) {
+          if (start < 0) start = k;
+          if (off + len < MAXNZ) sm_w[off + len] = (float)wv;
+          ++len;
+        }
+      }
+      sm_start[m] = start < 0 ? 0 : start;
+      sm_len[m] = len;
+      sm_off[m] = off;
+      off += len;
+    }
+  }
+  __syncthreads();
+
+  const int f = blockIdx.x * 4 + w;
+  const int len = lengths[b];
+  const int F = len >= FRAME ? 1 + (len - FRAME) / HOP : 0;
+  if (f >= F || f >= Fmax) return;  // whole wave exits; no block barrier follows
+  const float* x = wav + (int64_t)b * ld_wav + (int64_t)f * HOP;
+  float v[7];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int n = lane + 64 * i;
+    v[i] = n < FRAME ? x[n] * 32768.0f : 0.f;
+    s += v[i];
+  }
+  const float mean = wave_sum(s) * (1.0f / FRAME);
+  float2* buf = sbuf[w];
+  // write (x - mean) to LDS, then pre-emphasis + window into bit-reversed complex slots
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int n = lane + 64 * i;
+    if (n < FRAME) buf[n].x = v[i] - mean;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  float y[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int n = lane + 64 * i;
+    float val = 0.f;
+    if (n < FRAME) {
+      const float cur = buf[n].x;
+      val = (n == 0) ? cur * (1.0f - 0.97f) : cur - 0.97f * buf[n - 1].x;
+      val *= swin[n];
+    }
+    y[i] = val;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int n = lane + 64 * i;
+    const int rev = __builtin_bitreverse32((unsigned)n) >> (32 - 9);
+    buf[rev] = make_float2(y[i], 0.f);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  // iterative radix-2 DIT, 256 butterflies per stage, 4 per lane
+#pragma unroll
+  for (int half = 1; half < NFFT; half <<= 1) {
+    const int tstride = (NFFT / 2) / half;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = lane + 64 * i;            // butterfly id 0..255
+      const int grp = j / half, pos = j % half;
+      const int i0 = grp * 2 * half + pos, i1 = i0 + half;
+      const float2 tw = stw[pos * tstride];
+      const float2 a = buf[i0], bb = buf[i1];
+      const float2 t = make_float2(bb.x * tw.x - bb.y * tw.y, bb.x * tw.y + bb.y * tw.x);
+      buf[i0] = make_float2(a.x + t.x, a.y + t.y);
+      buf[i1] = make_float2(a.x - t.x, a.y - t.y);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  }
+  float* pw = spow[w];
+  for (int k = lane; k < NBIN; k += 64) {
+    const float2 z = buf[k];
+    pw[k] = z.x * z.x + z.y * z.y;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  float* out = work + ((int64_t)b * Fmax + f) * NMEL;
+  for (int m = lane; m < NMEL; m += 64) {
+    const int st = sm_start[m], ln = sm_len[m], of = sm_off[m];
+    float acc = 0.f;
+    for (int i = 0; i < ln; ++i) acc += sm_w[of + i] * pw[st + i];
+    out[m] = logf(fmaxf(acc, 1.192092955078125e-07f));
+  }
+}
+
+__global__ __launch_bounds__(256) void fbank_cmvn_kernel(const int32_t* __restrict__ lengths, int Fmax, int Tmax,
+                                                       const float* __restrict__ work, float pad_value,
+                                                       float* __restrict__ feats, int64_t* __restrict__ mask,
+                                                       int mask_mode) {
+  __shared__ double ssum[3][NMEL], ssq[3][NMEL];
+  __shared__ float smean[NMEL], sinv[NMEL];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int len = lengths[b];
+  const int F = len >= FRAME ? 1 + (len - FRAME) / HOP : 0;
+  const int Tb = (F + 1) / 2;
+  const float* x = work + (int64_t)b * Fmax * NMEL;
+  const int m = tid % NMEL, part = tid / NMEL;  // 3 partitions of frames (tid < 240)
+  if (part < 3) {
+    double s = 0.0;
+    for (int f = part; f < F; f += 3) s += x[(int64_t)f * NMEL + m];
+    ssum[part][m] = s;
+  }
+  __syncthreads();
+  if (tid < NMEL) {
+    const double mean = (ssum[0][tid] + ssum[1][tid] + ssum[2][tid]) / (double)(F > 0 ? F : 1);
+    smean[tid] = (float)mean;
+  }
+  __syncthreads();
+  if (part < 3) {
+    const double mu = smean[m];
+    double q = 0.0;
+    for (int f = part; f < F; f += 3) {
+      const double d = x[(int64_t)f * NMEL + m] - mu;
+      q += d * d;
+    }
+    ssq[part][m] = q;
+  }
+  __syncthreads();
+  if (tid < NMEL) {
+    const double var = (ssq[0][tid] + ssq[1][tid] + ssq[2][tid]) / (double)(F > 1 ? F - 1 : 1);
+    sinv[tid] = (float)(1.0 / sqrt(var + 1e-7));
+  }
+  __syncthreads();
+  float* o = feats + (int64_t)b * Tmax * (2 * NMEL);
+  for (int i = tid; i < Tmax * 2 * NMEL; i += 256) {
+    const int t = i / (2 * NMEL), c = i % (2 * NMEL);
+    const int f = 2 * t + (c >= NMEL), mm = c % NMEL;
+    float val = 0.f;
+    if (t < Tb) val = f < F ? (x[(int64_t)f * NMEL + mm] - smean[mm]) * sinv[mm] : pad_value;
+    o[i] = val;
+  }
+  for (int t = tid; t < Tmax; t += 256) {
+    int64_t mv;
+    if (mask_mode == 0) mv = t < Tb ? 1 : 0;
+    else mv = (t < Tb && 2 * t + 1 < F) ? 1 : 0;
+    mask[(int64_t)b * Tmax + t] = mv;
+  }
+}
+
+}  // namespace
+
+extern "C" int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* lengths, int B, int Tmax, float pad_value,
+                         float* feats, int64_t* mask, int mask_mode, float* work, void* stream) {
+  if (B <= 0 || Tmax <= 0 || !wav || !lengths || !feats || !mask || !work) return STE_ERR_ARG;
+  const int Fmax = 2 * Tmax;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(fbank_logmel_kernel, dim3((Fmax + 3) / 4, B), dim3(256), 0, s, wav, ld_wav, lengths, Fmax, work);
+  STE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(fbank_cmvn_kernel, dim3(B), dim3(256), 0, s, lengths, Fmax, Tmax, work, pad_value, feats, mask,
+                     mask_mode);
+  STE_CHECK_LAUNCH();
+  return 0;
+}

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(ste_gemm_args p) {
     const int row = m0 + wm * 64 + lr;
     if (row >= p.M || !col_ok) continue;
     f32x4 v = *reinterpret_cast<const f32x4*>(epi + lr * EPI_LD + (lane & 15) * 4);
-    v = v * p.alpha + bias;
+    v = (v + bias) * p.alpha;
     if (p.act >= STE_ACT_SWISH && p.act <= STE_ACT_RELU) {
       if (p.C2) store_bf16x4((bf16*)p.C2 + offC + (int64_t)row * p.ldc2 + col, v);
 #pragma unroll

@@ -1,0 +1,439 @@
+// Head-side kernels of EnhancedAudioTextModel (ref = /root/reference/training/trainer_unfreeze.py):
+//   AttentivePooling core (ref:171-211) fwd/bwd
+//   single-query CrossModalAttention core (ref:125-168, called with x.unsqueeze(1) at :653-667)
+//   F.normalize (ref:561-563), batch similarity matrix on the fp32 MFMA (ref:1073-1074),
+//   AlignmentAwareInfoNCE (ref:702-742) fwd/bwd.
+// These are small (rows = batch), latency-bound kernels; the big sequence-length
+// projections around them run through ste_gemm.
+#include "common.h"
+#include "../../include/ste.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+STE_DEV float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+  return s;
+}
+STE_DEV float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float s = -INFINITY;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s = fmaxf(s, red[i]);
+  return s;
+}
+
+STE_DEV float dot_bf16_f32(const bf16* a, const float* b, int n, int lane) {
+  float acc = 0.f;
+  for (int c = lane * 4; c < n; c += 256) {
+    f32x4 x = load_bf16x4(a + c);
+    f32x4 y = *reinterpret_cast<const f32x4*>(b + c);
+    acc += x[0] * y[0] + x[1] * y[1] + x[2] * y[2] + x[3] * y[3];
+  }
+  return wave_sum(acc);
+}
+
+// ------------------------------------------------------------ attentive pooling
+__global__ __launch_bounds__(NT) void pool_fwd_kernel(const bf16* t, const float* w2, const float* b2, const bf16* h,
+                                                    const int32_t* mask, int L, int Hh, int H, float* weights,
+                                                    float* pooled, bf16* pooled_bf16) {
+  extern __shared__ float sc[];  // L scores
+  __shared__ float red[8];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int l = w; l < L; l += NT / 64) {
+    float s = dot_bf16_f32(t + (int64_t)(b * L + l) * Hh, w2, Hh, lane) + b2[0];
+    if (mask && mask[b * L + l] == 0) s = -1e9f;
+    if (lane == 0) sc[l] = s;
+  }
+  __syncthreads();
+  float mx = -INFINITY;
+  for (int l = tid; l < L; l += NT) mx = fmaxf(mx, sc[l]);
+  mx = block_max(mx, red);
+  float sum = 0.f;
+  for (int l = tid; l < L; l += NT) { float e = __expf(sc[l] - mx); sc[l] = e; sum += e; }
+  sum = block_sum(sum, red);
+  const float inv = 1.0f / sum;
+  for (int l = tid; l < L; l += NT) { sc[l] *= inv; weights[b * L + l] = sc[l]; }
+  __syncthreads();
+  for (int c = tid * 4; c < H; c += NT * 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int l = 0; l < L; ++l) acc += load_bf16x4(h + (int64_t)(b * L + l) * H + c) * sc[l];
+    *reinterpret_cast<f32x4*>(pooled + (int64_t)b * H + c) = acc;
+    if (pooled_bf16) store_bf16x4(pooled_bf16 + (int64_t)b * H + c, acc);
+  }
+}
+
+// dz (pre-tanh gradient of the scorer's first Linear) = dscore * w2 * (1 - t^2)
+__global__ __launch_bounds__(NT) void pool_bwd_kernel(const bf16* t, const float* w2, const bf16* h,
+                                                    const float* weights, const float* dpooled, int L, int Hh, int H,
+                                                    float* dh, bf16* dz, float* dw2, float* db2) {
+  extern __shared__ float sdw[];  // L
+  __shared__ float red[8];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* dp = dpooled + (int64_t)b * H;
+  for (int l = w; l < L; l += NT / 64) {
+    float s = dot_bf16_f32(h + (int64_t)(b * L + l) * H, dp, H, lane);
+    if (lane == 0) sdw[l] = s;
+  }
+  __syncthreads();
+  float acc = 0.f;
+  for (int l = tid; l < L; l += NT) acc += weights[b * L + l] * sdw[l];
+  const float tot = block_sum(acc, red);
+  float dbs = 0.f;
+  for (int l = tid; l < L; l += NT) {
+    const float ds = weights[b * L + l] * (sdw[l] - tot);
+    sdw[l] = ds;
+    dbs += ds;
+  }
+  dbs = block_sum(dbs, red);  // contains a barrier: sdw now holds dscore
+  if (tid == 0 && db2) atomicAdd(db2, dbs);
+  // dh[l][c] += w[l] * dpooled[c]
+  for (int c = tid * 4; c < H; c += NT * 4) {
+    const f32x4 d = *reinterpret_cast<const f32x4*>(dp + c);
+    for (int l = 0; l < L; ++l) {
+      f32x4* o = reinterpret_cast<f32x4*>(dh + (int64_t)(b * L + l) * H + c);
+      *o = *o + d * weights[b * L + l];
+    }
+  }
+  // dz and dw2 partials
+  for (int k = tid * 4; k < Hh; k += NT * 4) {
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(w2 + k);
+    f32x4 g2 = {0.f, 0.f, 0.f, 0.f};
+    for (int l = 0; l < L; ++l) {
+      const f32x4 tv = load_bf16x4(t + (int64_t)(b * L + l) * Hh + k);
+      const float ds = sdw[l];
+      g2 += tv * ds;
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = ds * wv[e] * (1.f - tv[e] * tv[e]);
+      store_bf16x4(dz + (int64_t)(b * L + l) * Hh + k, o);
+    }
+    if (dw2) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomicAdd(dw2 + k + e, g2[e]);
+    }
+  }
+}
+
+// ---------------------------------------------------- single-query cross attention
+// scores/probs layout: [B][nh][S]
+__global__ __launch_bounds__(NT) void xattn1_fwd_kernel(const float* q, const bf16* k, const bf16* v, int64_t ldkv,
+                                                      const int32_t* mask, int S, int P, int nh, float scale,
+                                                      float drop_p, uint64_t seed, float* probs, float* out) {
+  extern __shared__ float sp[];  // nh * S
+  __shared__ float sq[1024];
+  __shared__ float red[8];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int dh = P / nh;
+  for (int c = tid; c < P; c += NT) sq[c] = q[(int64_t)b * P + c];
+  __syncthreads();
+  for (int i = tid; i < nh * S; i += NT) {
+    const int hh = i / S, s = i % S;
+    const bf16* kr = k + (int64_t)(b * S + s) * ldkv + hh * dh;
+    float acc = 0.f;
+    for (int d = 0; d < dh; d += 4) {
+      f32x4 x = load_bf16x4(kr + d);
+      acc += x[0] * sq[hh * dh + d] + x[1] * sq[hh * dh + d + 1] + x[2] * sq[hh * dh + d + 2] + x[3] * sq[hh * dh + d + 3];
+    }
+    acc *= scale;
+    if (mask && mask[b * S + s] == 0) acc = -1e9f;
+    sp[i] = acc;
+  }
+  __syncthreads();
+  // softmax per head: wave w handles heads w, w+4, ...
+  const uint32_t thresh = (uint32_t)(drop_p * 4294967296.0);
+  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  for (int hh = w; hh < nh; hh += NT / 64) {
+    float* row = sp + hh * S;
+    float mx = -INFINITY;
+    for (int s = lane; s < S; s += 64) mx = fmaxf(mx, row[s]);
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int s = lane; s < S; s += 64) { float e = __expf(row[s] - mx); row[s] = e; sum += e; }
+    sum = wave_sum(sum);
+    const float inv = 1.f / sum;
+    for (int s = lane; s < S; s += 64) {
+      float p = row[s] * inv;
+      probs[((int64_t)b * nh + hh) * S + s] = p;
+      if (drop_p > 0.f) p *= drop_scale(seed, ((uint64_t)b * nh + hh) * S + s, thresh, inv_keep);
+      row[s] = p;
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < P; c += NT) {
+    const int hh = c / dh;
+    float acc = 0.f;
+    for (int s = 0; s < S; ++s) acc += sp[hh * S + s] * (float)v[(int64_t)(b * S + s) * ldkv + c];
+    out[(int64_t)b * P + c] = acc;
+  }
+}
+
+// dk, dv are fp32 and ACCUMULATED (+=); dq is written.
+__global__ __launch_bounds__(NT) void xattn1_bwd_kernel(const float* q, const bf16* k, const bf16* v, int64_t ldkv,
+                                                      const float* probs, const float* dout, int S, int P, int nh,
+                                                      float scale, float drop_p, uint64_t seed, float* dq, float* dk,
+                                                      float* dv) {
+  extern __shared__ float sds[];  // nh * S : dp then ds
+  __shared__ float sq[1024], sdo[1024];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int dh = P / nh;
+  const uint32_t thresh = (uint32_t)(drop_p * 4294967296.0);
+  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  for (int c = tid; c < P; c += NT) { sq[c] = q[(int64_t)b * P + c]; sdo[c] = dout[(int64_t)b * P + c]; }
+  __syncthreads();
+  for (int i = tid; i < nh * S; i += NT) {
+    const int hh = i / S, s = i % S;
+    const bf16* vr = v + (int64_t)(b * S + s) * ldkv + hh * dh;
+    float acc = 0.f;
+    for (int d = 0; d < dh; d += 4) {
+      f32x4 x = load_bf16x4(vr + d);
+      acc += x[0] * sdo[hh * dh + d] + x[1] * sdo[hh * dh + d + 1] + x[2] * sdo[hh * dh + d + 2] + x[3] * sdo[hh * dh + d + 3];
+    }
+    if (drop_p > 0.f) acc *= drop_scale(seed, ((uint64_t)b * nh + hh) * S + s, thresh, inv_keep);
+    sds[i] = acc;  // dp (gradient wrt pre-dropout probability)
+  }
+  __syncthreads();
+  for (int hh = w; hh < nh; hh += NT / 64) {
+    const float* pr = probs + ((int64_t)b * nh + hh) * S;
+    float* row = sds + hh * S;
+    float acc = 0.f;
+    for (int s = lane; s < S; s += 64) acc += pr[s] * row[s];
+    acc = wave_sum(acc);
+    for (int s = lane; s < S; s += 64) row[s] = pr[s] * (row[s] - acc) * scale;
+  }
+  __syncthreads();
+  // dq[c] = Σ_s ds[h][s] k[s][c]
+  for (int c = tid; c < P; c += NT) {
+    const int hh = c / dh;
+    float acc = 0.f;
+    for (int s = 0; s < S; ++s) acc += sds[hh * S + s] * (float)k[(int64_t)(b * S + s) * ldkv + c];
+    dq[(int64_t)b * P + c] = acc;
+  }
+  // dk[s][c] += ds[h][s] q[c];  dv[s][c] += p'[h][s] dout[c]
+  for (int i = tid; i < S * P; i += NT) {
+    const int s = i / P, c = i % P, hh = c / dh;
+    const int64_t o = (int64_t)(b * S + s) * P + c;
+    dk[o] += sds[hh * S + s] * sq[c];
+    float p = probs[((int64_t)b * nh + hh) * S + s];
+    if (drop_p > 0.f) p *= drop_scale(seed, ((uint64_t)b * nh + hh) * S + s, thresh, inv_keep);
+    dv[o] += p * sdo[c];
+  }
+}
+
+// ---------------------------------------------------------------- L2 normalize
+__global__ __launch_bounds__(NT) void l2norm_fwd_kernel(const float* x, int cols, float* y, float* norms) {
+  __shared__ float red[8];
+  const int r = blockIdx.x;
+  float s = 0.f;
+  for (int c = threadIdx.x; c < cols; c += NT) { float v = x[(int64_t)r * cols + c]; s += v * v; }
+  s = block_sum(s, red);
+  const float n = fmaxf(sqrtf(s), 1e-12f);
+  if (threadIdx.x == 0) norms[r] = sqrtf(s);
+  for (int c = threadIdx.x; c < cols; c += NT) y[(int64_t)r * cols + c] = x[(int64_t)r * cols + c] / n;
+}
+__global__ __launch_bounds__(NT) void l2norm_bwd_kernel(const float* y, const float* norms, const float* dy, int cols,
+                                                      float* dx) {
+  __shared__ float red[8];
+  const int r = blockIdx.x;
+  const float nr = norms[r];
+  float s = 0.f;
+  for (int c = threadIdx.x; c < cols; c += NT) s += y[(int64_t)r * cols + c] * dy[(int64_t)r * cols + c];
+  s = block_sum(s, red);
+  const float inv = 1.f / fmaxf(nr, 1e-12f);
+  const bool clamped = nr < 1e-12f;
+  for (int c = threadIdx.x; c < cols; c += NT) {
+    const int64_t i = (int64_t)r * cols + c;
+    dx[i] = clamped ? dy[i] * inv : (dy[i] - y[i] * s) * inv;
+  }
+}
+
+// ------------------------------------------- batch similarity on the fp32 MFMA
+// S[i][j] = Σ_k A[i][k] T[j][k]; one wave per 16x16 output tile (v_mfma_f32_16x16x4_f32).
+__global__ __launch_bounds__(64) void similarity_kernel(const float* A, const float* Tm, int B, int NTt, int P,
+                                                      float* S) {
+  const int lane = threadIdx.x;
+  const int i0 = blockIdx.x * 16, j0 = blockIdx.y * 16;
+  const int ia = i0 + (lane & 15), jb = j0 + (lane & 15), kk = lane >> 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < P; k += 4) {
+    const float a = (ia < B && k + kk < P) ? A[(int64_t)ia * P + k + kk] : 0.f;
+    const float bv = (jb < NTt && k + kk < P) ? Tm[(int64_t)jb * P + k + kk] : 0.f;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + (lane >> 4) * 4 + r, j = j0 + (lane & 15);
+    if (i < B && j < NTt) S[(int64_t)i * NTt + j] = acc[r];
+  }
+}
+
+// ------------------------------------------------------------------- pair loss
+__global__ __launch_bounds__(NT) void pair_loss_fwd_kernel(const float* S, int64_t ldS, int off_neg, const float* align,
+                                                         int B, int L, float tau, float aw, float gamma, float* s_pos,
+                                                         float* s_neg, float* loss) {
+  __shared__ float red[8];
+  float acc = 0.f, pen = 0.f;
+  for (int i = threadIdx.x; i < B; i += NT) {
+    const float sp = S[(int64_t)i * ldS + i], sn = S[(int64_t)i * ldS + off_neg + i];
+    s_pos[i] = sp;
+    s_neg[i] = sn;
+    const float x = (sn - sp) / tau;
+    float ce = fmaxf(x, 0.f) + log1pf(__expf(-fabsf(x)));
+    if (align) {
+      float m = 0.f;
+      for (int l = 0; l < L; ++l) m += align[(int64_t)i * L + l];
+      m /= (float)L;
+      ce *= 1.f - sigmoidf_(m) * aw;
+    }
+    acc += ce;
+    pen += fmaxf(sn, 0.f);
+  }
+  acc = block_sum(acc, red);
+  pen = block_sum(pen, red);
+  if (threadIdx.x == 0) loss[0] = acc / (float)B + (gamma > 0.f ? gamma * pen / (float)B : 0.f);
+}
+
+__global__ __launch_bounds__(NT) void pair_loss_bwd_kernel(const float* s_pos, const float* s_neg, const float* align,
+                                                         int B, int L, float tau, float aw, float gamma,
+                                                         const float* gscale, float* ds_pos, float* ds_neg,
+                                                         float* dalign) {
+  const float gs = gscale ? gscale[0] : 1.f;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < B; i += gridDim.x * NT) {
+    const float sp = s_pos[i], sn = s_neg[i];
+    const float x = (sn - sp) / tau;
+    const float ce = fmaxf(x, 0.f) + log1pf(__expf(-fabsf(x)));
+    float factor = 1.f, sg = 0.f;
+    if (align) {
+      float m = 0.f;
+      for (int l = 0; l < L; ++l) m += align[(int64_t)i * L + l];
+      m /= (float)L;
+      sg = sigmoidf_(m);
+      factor = 1.f - sg * aw;
+    }
+    const float dce = gs * factor / (float)B;
+    const float dx = sigmoidf_(x) * dce / tau;
+    ds_pos[i] = -dx;
+    ds_neg[i] = dx + ((gamma > 0.f && sn > 0.f) ? gs * gamma / (float)B : 0.f);
+    if (align && dalign) {
+      const float da = gs * ce / (float)B * (-aw) * sg * (1.f - sg) / (float)L;
+      for (int l = 0; l < L; ++l) dalign[(int64_t)i * L + l] = da;
+    }
+  }
+}
+
+// d(aud), d(txt_pos), d(txt_neg) from ds_pos/ds_neg through s = <aud, txt>
+__global__ __launch_bounds__(NT) void pair_sim_bwd_kernel(const float* a, const float* tp, const float* tn,
+                                                        const float* ds_pos, const float* ds_neg, int P, float* da,
+                                                        float* dtp, float* dtn) {
+  const int i = blockIdx.x;
+  const float gp = ds_pos[i], gn = ds_neg[i];
+  for (int c = threadIdx.x; c < P; c += NT) {
+    const int64_t o = (int64_t)i * P + c;
+    da[o] = gp * tp[o] + gn * tn[o];
+    dtp[o] = gp * a[o];
+    dtn[o] = gn * a[o];
+  }
+}
+
+}  // namespace
+
+extern "C" int ste_attn_pool_fwd(const void* t, const float* w2, const float* b2, const void* h, const int32_t* mask,
+                                 int B, int L, int Hh, int H, float* weights, float* pooled, void* pooled_bf16,
+                                 void* stream) {
+  if (B <= 0 || L <= 0 || (Hh & 3) || (H & 3) || L > 8192) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(pool_fwd_kernel, dim3(B), dim3(NT), L * sizeof(float), (hipStream_t)stream, (const bf16*)t, w2,
+                     b2, (const bf16*)h, mask, L, Hh, H, weights, pooled, (bf16*)pooled_bf16);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float* weights,
+                                 const float* dpooled, int B, int L, int Hh, int H, float* dh, void* dt, float* dw2,
+                                 float* db2, void* stream) {
+  if (B <= 0 || L <= 0 || (Hh & 3) || (H & 3) || L > 8192) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3(B), dim3(NT), L * sizeof(float), (hipStream_t)stream, (const bf16*)t, w2,
+                     (const bf16*)h, weights, dpooled, L, Hh, H, dh, (bf16*)dt, dw2, db2);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_xattn1_fwd(const float* q, const void* k, const void* v, int64_t ldkv, const int32_t* mask, int B,
+                              int S, int P, int nh, float scale, float drop_p, uint64_t seed, float* probs, float* out,
+                              void* stream) {
+  if (B <= 0 || S <= 0 || P > 1024 || P % nh || (P / nh) % 4 || nh * S > 16384) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(xattn1_fwd_kernel, dim3(B), dim3(NT), nh * S * sizeof(float), (hipStream_t)stream, q,
+                     (const bf16*)k, (const bf16*)v, ldkv, mask, S, P, nh, scale, drop_p, seed, probs, out);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_xattn1_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
+                              const float* dout, int B, int S, int P, int nh, float scale, float drop_p, uint64_t seed,
+                              float* dq, float* dk, float* dv, void* stream) {
+  if (B <= 0 || S <= 0 || P > 1024 || P % nh || (P / nh) % 4 || nh * S > 16384) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(xattn1_bwd_kernel, dim3(B), dim3(NT), nh * S * sizeof(float), (hipStream_t)stream, q,
+                     (const bf16*)k, (const bf16*)v, ldkv, probs, dout, S, P, nh, scale, drop_p, seed, dq, dk, dv);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_l2norm_fwd(const float* x, int rows, int cols, float* y, float* norms, void* stream) {
+  if (rows <= 0 || cols <= 0) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(l2norm_fwd_kernel, dim3(rows), dim3(NT), 0, (hipStream_t)stream, x, cols, y, norms);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_l2norm_bwd(const float* y, const float* norms, const float* dy, int rows, int cols, float* dx,
+                              void* stream) {
+  if (rows <= 0 || cols <= 0) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(l2norm_bwd_kernel, dim3(rows), dim3(NT), 0, (hipStream_t)stream, y, norms, dy, cols, dx);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_similarity(const float* a, const float* t, int B, int NTt, int P, float* S, void* stream) {
+  if (B <= 0 || NTt <= 0 || P <= 0) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(similarity_kernel, dim3((B + 15) / 16, (NTt + 15) / 16), dim3(64), 0, (hipStream_t)stream, a, t,
+                     B, NTt, P, S);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_pair_loss_fwd(const float* S, int64_t ldS, int off_neg, const float* align, int B, int L, float tau,
+                                 float aw, float gamma, float* s_pos, float* s_neg, float* loss, void* stream) {
+  if (B <= 0) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(pair_loss_fwd_kernel, dim3(1), dim3(NT), 0, (hipStream_t)stream, S, ldS, off_neg, align, B, L,
+                     tau, aw, gamma, s_pos, s_neg, loss);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_pair_loss_bwd(const float* s_pos, const float* s_neg, const float* align, int B, int L, float tau,
+                                 float aw, float gamma, const float* gscale, float* ds_pos, float* ds_neg,
+                                 float* dalign, void* stream) {
+  if (B <= 0) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(pair_loss_bwd_kernel, dim3((B + NT - 1) / NT), dim3(NT), 0, (hipStream_t)stream, s_pos, s_neg,
+                     align, B, L, tau, aw, gamma, gscale, ds_pos, ds_neg, dalign);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_pair_sim_bwd(const float* a, const float* tp, const float* tn, const float* ds_pos,
+                                const float* ds_neg, int B, int P, float* da, float* dtp, float* dtn, void* stream) {
+  if (B <= 0 || P <= 0) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(pair_sim_bwd_kernel, dim3(B), dim3(NT), 0, (hipStream_t)stream, a, tp, tn, ds_pos, ds_neg, P,
+                     da, dtp, dtn);
+  STE_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,7 +1,7 @@
 // LayerNorm forward/backward, one wavefront per row, fp32 statistics.
 // Replaces nn.LayerNorm in both encoders and the heads (see include/ste.h).
 // HBM-bound: forward reads x once and writes y once; backward reads dy, x once.
-// Rows are processed grid-stride so the dgamma/dbeta partials of a whole block
+// Rows are processed grid-stride so the dgamma/dbeta/dsum partials of a whole block
 // are reduced in LDS and flushed with one atomic per column per block.
 #include "common.h"
 #include "../../include/ste.h"
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(ste_ln_fwd_args a) {
 
 template <int MAXC>
 __global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
-  __shared__ float red[2][NT / 64][MAXC * 4 * 64];
+  __shared__ float red[3][NT / 64][MAXC * 4 * 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wave = blockIdx.x * (NT / 64) + wid;
   const int nwaves = gridDim.x * (NT / 64);
@@ -83,9 +83,9 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
   const float inv_keep = a.drop_p > 0.f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
   const uint32_t in_thresh = (uint32_t)(a.in_drop_p * 4294967296.0);
   const float in_inv_keep = a.in_drop_p > 0.f ? 1.0f / (1.0f - a.in_drop_p) : 1.0f;
-  float dg[MAXC * 4], db[MAXC * 4];
+  float dg[MAXC * 4], db[MAXC * 4], dsm[MAXC * 4];
 #pragma unroll
-  for (int i = 0; i < MAXC * 4; ++i) { dg[i] = 0.f; db[i] = 0.f; }
+  for (int i = 0; i < MAXC * 4; ++i) { dg[i] = 0.f; db[i] = 0.f; dsm[i] = 0.f; }
 
   for (int row = wave; row < a.rows; row += nwaves) {
     float x[MAXC * 4], g[MAXC * 4];
@@ -120,6 +120,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
     }
     s1 = wave_sum(s1) * inv_n;
     s2 = wave_sum(s2) * inv_n;
+    const float ors = a.out_row_scale ? a.out_row_scale[row] : 1.0f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       int col = (lane + c * 64) * 4;
@@ -132,21 +133,25 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
       }
       if (a.dres) d += *reinterpret_cast<const f32x4*>(a.dres + (int64_t)row * a.lddres + col);
       if (a.dx) *reinterpret_cast<f32x4*>(a.dx + (int64_t)row * a.lddx + col) = d;
-      if (a.dxb) {
-        f32x4 o = d * a.out_scale;
+      if (a.dxb || a.dsum) {
+        f32x4 o = d * (a.out_scale * ors);
         if (a.drop_p > 0.f) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] *= drop_scale(a.seed, (uint64_t)row * a.cols + col + e, thresh, inv_keep);
         }
-        store_bf16x4((bf16*)a.dxb + (int64_t)row * a.lddxb + col, o);
+        if (a.dxb) store_bf16x4((bf16*)a.dxb + (int64_t)row * a.lddxb + col, o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dsm[c * 4 + e] += o[e];
       }
     }
   }
-  if (!a.dgamma) return;
+  if (!a.dgamma && !a.dbeta && !a.dsum) return;
 #pragma unroll
   for (int i = 0; i < MAXC * 4; ++i) {
-    red[0][wid][(i >> 2) * 256 + lane * 4 + (i & 3)] = dg[i];
-    red[1][wid][(i >> 2) * 256 + lane * 4 + (i & 3)] = db[i];
+    const int j = (i >> 2) * 256 + lane * 4 + (i & 3);
+    red[0][wid][j] = dg[i];
+    red[1][wid][j] = db[i];
+    red[2][wid][j] = dsm[i];
   }
   __syncthreads();
   for (int j = threadIdx.x; j < MAXC * 256; j += NT) {
@@ -154,11 +159,12 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
     const int c = j >> 8, rem = j & 255;
     const int col = (c * 64 + (rem >> 2)) * 4 + (rem & 3);
     if (col >= a.cols) continue;
-    float sg = 0.f, sb = 0.f;
+    float sg = 0.f, sb = 0.f, ss = 0.f;
 #pragma unroll
-    for (int w = 0; w < NT / 64; ++w) { sg += red[0][w][j]; sb += red[1][w][j]; }
-    atomicAdd(a.dgamma + col, sg);
+    for (int w = 0; w < NT / 64; ++w) { sg += red[0][w][j]; sb += red[1][w][j]; ss += red[2][w][j]; }
+    if (a.dgamma) atomicAdd(a.dgamma + col, sg);
     if (a.dbeta) atomicAdd(a.dbeta + col, sb);
+    if (a.dsum) atomicAdd(a.dsum + col, ss);
   }
 }
 

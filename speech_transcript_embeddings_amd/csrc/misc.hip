@@ -25,7 +25,43 @@ __global__ void mask_cvt_kernel(const int64_t* m, float* f, int32_t* i32, int64_
     if (i32) i32[i] = v != 0 ? 1 : 0;
   }
 }
+// out[c] += Σ_r x[r, c]; block = 64-column stripe x row chunk, 256 threads = 16 cols x 16 row lanes (x4 vector)
+__global__ void colsum_kernel(const void* x, int is_bf16, int64_t rows, int cols, int64_t ld, float* out,
+                              int64_t rows_per_block) {
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + tx * 4;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    for (int64_t r = r0 + ty; r < r1; r += 16) {
+      if (is_bf16) acc += load_bf16x4((const bf16*)x + r * ld + c);
+      else acc += *reinterpret_cast<const f32x4*>((const float*)x + r * ld + c);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[ty][tx * 4 + e] = acc[e];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int cc = blockIdx.x * 64 + threadIdx.x;
+    float s = 0.f;
+#pragma unroll
+    for (int y = 0; y < 16; ++y) s += red[y][threadIdx.x];
+    if (cc < cols) atomicAdd(out + cc, s);
+  }
+}
 }  // namespace
+
+extern "C" int ste_colsum(const void* x, int is_bf16, int64_t rows, int cols, int64_t ld, float* out, void* stream) {
+  if (rows <= 0) return 0;
+  if ((cols & 3) || (ld & 3)) return STE_ERR_SHAPE;
+  const int64_t rpb = 512;
+  dim3 grid((cols + 63) / 64, (unsigned)((rows + rpb - 1) / rpb));
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, is_bf16, rows, cols, ld, out, rpb);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int ste_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream) {
   if (n <= 0) return 0;

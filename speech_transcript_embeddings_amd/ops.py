@@ -112,7 +112,8 @@ def layernorm_fwd(x, gamma, beta, eps, *, y=None, yb=None, mean=None, rstd=None,
 
 
 def layernorm_bwd(dy, x, mean, rstd, gamma, *, beta=None, dx=None, dxb=None, dres=None, dgamma=None, dbeta=None,
-                  row_scale=None, act=_lib.ACT_NONE, drop_p=0.0, seed=0, out_scale=1.0, in_drop_p=0.0, in_seed=0):
+                  row_scale=None, act=_lib.ACT_NONE, drop_p=0.0, seed=0, out_scale=1.0, in_drop_p=0.0, in_seed=0,
+                  out_row_scale=None, dsum=None):
     rows, cols = x.shape
     a = LnBwdArgs()
     a.rows, a.cols = rows, cols
@@ -129,5 +130,157 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, *, beta=None, dx=None, dxb=None, dre
     a.dgamma, a.dbeta = ptr(dgamma), ptr(dbeta)
     a.drop_p, a.seed, a.out_scale = float(drop_p), int(seed) & (2**64 - 1), float(out_scale)
     a.in_drop_p, a.in_seed = float(in_drop_p), int(in_seed) & (2**64 - 1)
+    a.out_row_scale, a.dsum = ptr(out_row_scale), ptr(dsum)
     call("ste_layernorm_bwd", C.byref(a), _s())
     return dx, dxb
+
+
+# -------------------------------------------------------------- attention
+def attention_fwd(q, k, v, *, B, T, H, o, lse, key_mask=None, rel_E=None, rel_left=64, rel_right=8,
+                  scale=0.125, drop_p=0.0, seed=0):
+    """q/k/v/o: bf16 [B*T, *] views (row-major, head h at columns h*64..), lse fp32 [B*H*T]."""
+    a = AttnArgs()
+    a.B, a.T, a.H = B, T, H
+    a.q, a.ldq = ptr(q), _ld(q)
+    a.k, a.ldk = ptr(k), _ld(k)
+    a.v, a.ldv = ptr(v), _ld(v)
+    a.o, a.ldo = ptr(o), _ld(o)
+    a.lse = ptr(lse)
+    a.key_mask = ptr(key_mask)
+    a.rel_E, a.rel_left, a.rel_right = ptr(rel_E), rel_left, rel_right
+    a.scale, a.drop_p, a.seed = float(scale), float(drop_p), int(seed) & (2**64 - 1)
+    call("ste_attention_fwd", C.byref(a), _s())
+    return a
+
+
+def attention_bwd(q, k, v, o, lse, dout, dq, dk, dv, *, B, T, H, delta, key_mask=None, rel_E=None, rel_left=64,
+                  rel_right=8, scale=0.125, drop_p=0.0, seed=0, dE=None, gwork=None):
+    a = AttnArgs()
+    a.B, a.T, a.H = B, T, H
+    a.q, a.ldq = ptr(q), _ld(q)
+    a.k, a.ldk = ptr(k), _ld(k)
+    a.v, a.ldv = ptr(v), _ld(v)
+    a.o, a.ldo = ptr(o), _ld(o)
+    a.lse = ptr(lse)
+    a.key_mask = ptr(key_mask)
+    a.rel_E, a.rel_left, a.rel_right = ptr(rel_E), rel_left, rel_right
+    a.scale, a.drop_p, a.seed = float(scale), float(drop_p), int(seed) & (2**64 - 1)
+    a.dout, a.lddo = ptr(dout), _ld(dout)
+    a.dq, a.lddq = ptr(dq), _ld(dq)
+    a.dk, a.lddk = ptr(dk), _ld(dk)
+    a.dv, a.lddv = ptr(dv), _ld(dv)
+    a.delta, a.dE, a.gwork = ptr(delta), ptr(dE), ptr(gwork)
+    call("ste_attention_bwd", C.byref(a), _s())
+
+
+# ------------------------------------------------------------ conv module
+def glu_dwconv_fwd(pre, w, out, B, T):
+    C_ = w.shape[0]
+    call("ste_glu_dwconv_fwd", ptr(pre), ptr(w), ptr(out), B, T, C_, w.shape[-1], _s())
+    return out
+
+
+def glu_dwconv_bwd(pre, w, dout, dpre, dw, B, T):
+    C_ = w.shape[0]
+    call("ste_glu_dwconv_bwd", ptr(pre), ptr(w), ptr(dout), ptr(dpre), ptr(dw), B, T, C_, w.shape[-1], _s())
+    return dpre
+
+
+# ------------------------------------------------------------------ fbank
+def fbank(wav, lengths, Tmax, *, pad_value=1.0, mask_mode=0, feats=None, mask=None, work=None):
+    """wav fp32 [B, N] (rows padded), lengths int32 [B] -> feats fp32 [B,Tmax,160], mask int64 [B,Tmax]."""
+    B = wav.shape[0]
+    dev = wav.device
+    if feats is None:
+        feats = torch.empty((B, Tmax, 160), device=dev, dtype=F32)
+    if mask is None:
+        mask = torch.empty((B, Tmax), device=dev, dtype=torch.int64)
+    if work is None:
+        work = torch.empty((B, 2 * Tmax, 80), device=dev, dtype=F32)
+    call("ste_fbank", ptr(wav), wav.stride(0), ptr(lengths), B, Tmax, float(pad_value), ptr(feats), ptr(mask),
+         int(mask_mode), ptr(work), _s())
+    return feats, mask
+
+
+# ------------------------------------------------------------------ heads
+def attn_pool_fwd(t, w2, b2, h, mask, B, L, weights, pooled, pooled_bf16=None):
+    call("ste_attn_pool_fwd", ptr(t), ptr(w2), ptr(b2), ptr(h), ptr(mask), B, L, t.shape[-1], h.shape[-1],
+         ptr(weights), ptr(pooled), ptr(pooled_bf16), _s())
+
+
+def attn_pool_bwd(t, w2, h, weights, dpooled, B, L, dh, dz, dw2=None, db2=None):
+    call("ste_attn_pool_bwd", ptr(t), ptr(w2), ptr(h), ptr(weights), ptr(dpooled), B, L, t.shape[-1], h.shape[-1],
+         ptr(dh), ptr(dz), ptr(dw2), ptr(db2), _s())
+
+
+def xattn1_fwd(q, k, v, mask, B, S, nh, probs, out, drop_p=0.0, seed=0):
+    P = q.shape[-1]
+    call("ste_xattn1_fwd", ptr(q), ptr(k), ptr(v), _ld(k), ptr(mask), B, S, P, nh, float((P // nh) ** -0.5),
+         float(drop_p), int(seed) & (2**64 - 1), ptr(probs), ptr(out), _s())
+
+
+def xattn1_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, drop_p=0.0, seed=0):
+    P = q.shape[-1]
+    call("ste_xattn1_bwd", ptr(q), ptr(k), ptr(v), _ld(k), ptr(probs), ptr(dout), B, S, P, nh,
+         float((P // nh) ** -0.5), float(drop_p), int(seed) & (2**64 - 1), ptr(dq), ptr(dk), ptr(dv), _s())
+
+
+def l2norm_fwd(x, y, norms):
+    call("ste_l2norm_fwd", ptr(x), x.shape[0], x.shape[1], ptr(y), ptr(norms), _s())
+
+
+def l2norm_bwd(y, norms, dy, dx):
+    call("ste_l2norm_bwd", ptr(y), ptr(norms), ptr(dy), y.shape[0], y.shape[1], ptr(dx), _s())
+
+
+def similarity(a, t, S):
+    call("ste_similarity", ptr(a), ptr(t), a.shape[0], t.shape[0], a.shape[1], ptr(S), _s())
+
+
+def pair_loss_fwd(S, off_neg, align, B, L, tau, aw, gamma, s_pos, s_neg, loss):
+    call("ste_pair_loss_fwd", ptr(S), _ld(S), off_neg, ptr(align), B, L, float(tau), float(aw), float(gamma),
+         ptr(s_pos), ptr(s_neg), ptr(loss), _s())
+
+
+def pair_loss_bwd(s_pos, s_neg, align, B, L, tau, aw, gamma, gscale, ds_pos, ds_neg, dalign=None):
+    call("ste_pair_loss_bwd", ptr(s_pos), ptr(s_neg), ptr(align), B, L, float(tau), float(aw), float(gamma),
+         ptr(gscale), ptr(ds_pos), ptr(ds_neg), ptr(dalign), _s())
+
+
+def pair_sim_bwd(a, tp, tn, ds_pos, ds_neg, da, dtp, dtn):
+    call("ste_pair_sim_bwd", ptr(a), ptr(tp), ptr(tn), ptr(ds_pos), ptr(ds_neg), a.shape[0], a.shape[1], ptr(da),
+         ptr(dtp), ptr(dtn), _s())
+
+
+# -------------------------------------------------------------- embedding
+def text_embed_fwd(ids, pad_idx, word, pos, type0, out, pos_ids):
+    B, L = ids.shape
+    call("ste_text_embed_fwd", ptr(ids), B, L, word.shape[1], pad_idx, ptr(word), ptr(pos), ptr(type0), ptr(out),
+         ptr(pos_ids), _s())
+
+
+def text_embed_bwd(ids, pos_ids, dout, pad_idx, dword, dpos, dtype0):
+    B, L = ids.shape
+    call("ste_text_embed_bwd", ptr(ids), ptr(pos_ids), ptr(dout), B, L, dout.shape[-1], pad_idx, ptr(dword),
+         ptr(dpos), ptr(dtype0), _s())
+
+
+# -------------------------------------------------------------- optimizer
+def sumsq(g, acc):
+    call("ste_sumsq", ptr(g), g.numel(), ptr(acc), _s())
+
+
+def adamw(p, g, m, v, p_bf16, *, lr, beta1, beta2, eps, wd, step, sumsq_acc=None, max_norm=1.0):
+    call("ste_adamw", ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), p.numel(), float(lr), float(beta1), float(beta2),
+         float(eps), float(wd), int(step), ptr(sumsq_acc), float(max_norm), _s())
+
+
+def cast_bf16(x, y):
+    call("ste_cast_f32_bf16", ptr(x), ptr(y), x.numel(), _s())
+    return y
+
+
+def colsum(x, out):
+    """out[c] += Σ_r x[r, c]."""
+    call("ste_colsum", ptr(x), int(x.dtype == BF16), x.shape[0], x.shape[1], _ld(x), ptr(out), _s())
+    return out

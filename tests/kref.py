@@ -1,0 +1,59 @@
+"""Test-side fp32 torch references for individual kernels (the "plain PyTorch fp32
+reference of the same op" for each HIP kernel) and a numpy copy of the kernels'
+counter-based dropout hash, so dropout masks can be reproduced exactly."""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+M64 = (1 << 64) - 1
+
+
+def ste_hash(seed: int, idx: np.ndarray) -> np.ndarray:
+    idx = idx.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        x = np.uint64(seed & M64) ^ (idx * np.uint64(0x9E3779B97F4A7C15))
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xFF51AFD7ED558CCD)
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xC4CEB9FE1A85EC53)
+        x ^= x >> np.uint64(33)
+    return (x & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
+def drop_scale(seed: int, idx: np.ndarray, p: float) -> np.ndarray:
+    thresh = np.uint32(min(int(p * 4294967296.0), 0xFFFFFFFF))
+    keep = ste_hash(seed, idx) >= thresh
+    return keep.astype(np.float32) / (1.0 - p)
+
+
+def attention_ref(q, k, v, mask, E=None, left=64, right=8, drop_p=0.0, seed=0):
+    """q,k,v [B,T,H,64] fp32; mask [B,T] (1 valid) or None; returns o [B,T,H,64]."""
+    B, T, H, D = q.shape
+    qh, kh, vh = (x.permute(0, 2, 1, 3) for x in (q, k, v))
+    s = qh @ kh.transpose(-1, -2)
+    if E is not None:
+        pos = torch.arange(T, device=q.device)
+        dist = (pos.view(1, -1) - pos.view(-1, 1)).clamp(-left, right) + left
+        qe = qh @ E.t()
+        s = s + torch.gather(qe, 3, dist.view(1, 1, T, T).expand(B, H, T, T))
+    s = s / math.sqrt(D)
+    if mask is not None:
+        s = s + (1.0 - mask[:, None, None, :].float()) * torch.finfo(torch.float32).min
+    p = torch.softmax(s, -1)
+    if drop_p > 0:
+        bb, hh, ll, rr = np.meshgrid(np.arange(B), np.arange(H), np.arange(T), np.arange(T), indexing="ij")
+        idx = ((bb * H + hh) * T + ll).astype(np.uint64) * np.uint64(T) + rr.astype(np.uint64)
+        p = p * torch.from_numpy(drop_scale(seed, idx, drop_p)).to(p.device)
+    return (p @ vh).permute(0, 2, 1, 3)
+
+
+def glu_dwconv_ref(pre, w, B, T):
+    """pre [B*T, 2C] fp32, w [C, K] -> [B*T, C]."""
+    C = w.shape[0]
+    x = pre.view(B, T, 2 * C).transpose(1, 2)
+    x = F.glu(x, dim=1)
+    x = F.pad(x, (w.shape[1] - 1, 0))
+    y = F.conv1d(x, w.unsqueeze(1), groups=C)
+    return y.transpose(1, 2).reshape(B * T, C)

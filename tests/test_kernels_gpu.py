@@ -1,0 +1,358 @@
+"""Per-kernel parity: every libste.so kernel vs a plain PyTorch fp32 reference of the same op
+(tests/kref.py), through the C ABI (speech_transcript_embeddings_amd.ops -> ctypes)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from kref import attention_ref, drop_scale, glu_dwconv_ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from speech_transcript_embeddings_amd import ops as _ops
+    return _ops
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+# ------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("M,N,K", [(64, 128, 64), (300, 384, 200), (1000, 1024, 160), (130, 776, 96)])
+def test_gemm_layouts(ops, M, N, K):
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = torch.randn(N, K, device=DEV).bfloat16()
+    b = torch.randn(N, device=DEV)
+    y = ops.linear(x, w, b)
+    assert rel_err(y, x.float() @ w.float().t() + b) < 1e-5
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    assert rel_err(ops.linear_dx(dy, w), dy.float() @ w.float()) < 1e-5
+    assert rel_err(ops.linear_dw(dy, x), dy.float().t() @ x.float()) < 1e-5
+
+
+def test_gemm_epilogues(ops):
+    from speech_transcript_embeddings_amd import _lib
+    torch.manual_seed(1)
+    M, N, K = 257, 256, 128
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = torch.randn(N, K, device=DEV).bfloat16() * 0.1
+    b = torch.randn(N, device=DEV)
+    ref = x.float() @ w.float().t() + b
+    for act, fn in [(_lib.ACT_SWISH, F.silu), (_lib.ACT_GELU, F.gelu), (_lib.ACT_TANH, torch.tanh),
+                    (_lib.ACT_RELU, F.relu)]:
+        pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        out = ops.linear(x, w, b, act=act, pre_out=pre)
+        assert rel_err(out, fn(ref)) < 1e-5
+        assert rel_err(pre, ref) < 5e-3
+    # activation backward with Z, dropout, row scale, colsum, residual, beta
+    z = torch.randn(M, N, device=DEV).bfloat16()
+    rs = (torch.rand(M, device=DEV) > 0.3).float()
+    r = torch.randn(M, N, device=DEV)
+    cs = torch.zeros(N, device=DEV)
+    c = torch.randn(M, N, device=DEV)
+    c0 = c.clone()
+    seed, p = 1234, 0.25
+    ops.linear(x, w, None, act=_lib.ACT_GELU_BWD, z=z, drop_p=p, seed=seed, row_scale=rs, colsum=cs, residual=r,
+               beta=1.0, out=c, alpha=0.5)
+    idx = (np.arange(M)[:, None] * N + np.arange(N)[None, :]).astype(np.uint64)
+    dmask = torch.from_numpy(drop_scale(seed, idx, p)).to(DEV)
+    zf = z.float()
+    gd = torch.special.ndtr(zf) + zf * torch.exp(-0.5 * zf * zf) / math.sqrt(2 * math.pi)
+    v = 0.5 * (x.float() @ w.float().t()) * gd * dmask * rs[:, None]
+    assert rel_err(cs, v.sum(0)) < 1e-4
+    assert rel_err(c, v + r + c0) < 1e-5
+
+
+# -------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("cols", [160, 768, 1024])
+def test_layernorm_fwd_bwd(ops, cols):
+    from speech_transcript_embeddings_amd import _lib
+    torch.manual_seed(cols)
+    rows = 333
+    x = torch.randn(rows, cols, device=DEV) * 2 + 0.5
+    g = torch.randn(cols, device=DEV)
+    b = torch.randn(cols, device=DEV)
+    rs = (torch.rand(rows, device=DEV) > 0.2).float()
+    for act in (_lib.ACT_NONE, _lib.ACT_SWISH):
+        y = torch.empty_like(x)
+        yb = torch.empty(rows, cols, device=DEV, dtype=torch.bfloat16)
+        mean, rstd = ops.layernorm_fwd(x, g, b, 1e-5, y=y, yb=yb, row_scale=rs, act=act)
+        xr, gr, br = (t.clone().requires_grad_() for t in (x, g, b))
+        ref = F.layer_norm(xr, (cols,), gr, br, 1e-5) * rs[:, None]
+        if act == _lib.ACT_SWISH:
+            ref = F.silu(ref)
+        assert rel_err(y, ref) < 1e-5
+        assert rel_err(yb, ref) < 5e-3
+        dy = torch.randn_like(x)
+        ref.backward(dy)
+        dres = torch.randn_like(x)
+        dx = torch.empty_like(x)
+        dxb = torch.empty(rows, cols, device=DEV, dtype=torch.bfloat16)
+        dg = torch.zeros(cols, device=DEV)
+        db = torch.zeros(cols, device=DEV)
+        ops.layernorm_bwd(dy, x, mean, rstd, g, beta=b, dx=dx, dxb=dxb, dres=dres, dgamma=dg, dbeta=db, row_scale=rs,
+                          act=act, out_scale=0.5)
+        assert rel_err(dx, xr.grad + dres) < 1e-5
+        assert rel_err(dxb, 0.5 * (xr.grad + dres)) < 5e-3
+        assert rel_err(dg, gr.grad) < 1e-5
+        assert rel_err(db, br.grad) < 1e-5
+
+
+# -------------------------------------------------------------- attention
+def _attn_case(ops, B, T, H, rel, masked, drop_p, seed=7):
+    torch.manual_seed(T * 7 + H)
+    D = 64
+    W = H * D
+    qkv = (torch.randn(B * T, 3 * W, device=DEV) * 0.7).bfloat16()
+    q, k, v = qkv[:, :W], qkv[:, W:2 * W], qkv[:, 2 * W:]
+    mask = None
+    if masked:
+        m = torch.ones(B, T, dtype=torch.int32, device=DEV)
+        m[0, T - T // 3:] = 0
+        if B > 1:
+            m[1, :5] = 0
+        mask = m.reshape(-1).contiguous()
+    E = (torch.randn(73, D, device=DEV) * 0.5).bfloat16() if rel else None
+    o = torch.empty(B * T, W, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * T, device=DEV)
+    ops.attention_fwd(q, k, v, B=B, T=T, H=H, o=o, lse=lse, key_mask=mask, rel_E=E, drop_p=drop_p, seed=seed)
+    qf, kf, vf = (t.float().view(B, T, H, D).clone().requires_grad_() for t in (q, k, v))
+    Ef = E.float().clone().requires_grad_() if rel else None
+    ref = attention_ref(qf, kf, vf, mask.view(B, T) if masked else None, Ef, drop_p=drop_p, seed=seed)
+    assert rel_err(o.view(B, T, H, D), ref) < 1e-2
+    do = torch.randn(B * T, W, device=DEV).bfloat16()
+    ref.backward(do.float().view(B, T, H, D))
+    dqkv = torch.zeros(B * T, 3 * W, device=DEV, dtype=torch.bfloat16)
+    delta = torch.empty(B * H * T, device=DEV)
+    dE = torch.zeros(73, D, device=DEV) if rel else None
+    gw = torch.empty(B * H * T * 80, device=DEV) if rel else None
+    ops.attention_bwd(q, k, v, o, lse, do, dqkv[:, :W], dqkv[:, W:2 * W], dqkv[:, 2 * W:], B=B, T=T, H=H, delta=delta,
+                      key_mask=mask, rel_E=E, drop_p=drop_p, seed=seed, dE=dE, gwork=gw)
+    assert rel_err(dqkv[:, :W].view(B, T, H, D), qf.grad) < 2e-2
+    assert rel_err(dqkv[:, W:2 * W].view(B, T, H, D), kf.grad) < 2e-2
+    assert rel_err(dqkv[:, 2 * W:].view(B, T, H, D), vf.grad) < 2e-2
+    if rel:
+        assert rel_err(dE, Ef.grad) < 2e-2
+
+
+@pytest.mark.parametrize("T", [99, 150, 499])
+def test_attention_relkey(ops, T):
+    _attn_case(ops, B=2, T=T, H=2, rel=True, masked=True, drop_p=0.0)
+
+
+def test_attention_relkey_unmasked_long(ops):
+    _attn_case(ops, B=1, T=700, H=1, rel=True, masked=False, drop_p=0.0)
+
+
+@pytest.mark.parametrize("drop_p", [0.0, 0.1])
+def test_attention_text(ops, drop_p):
+    _attn_case(ops, B=3, T=64, H=3, rel=False, masked=True, drop_p=drop_p)
+
+
+# ---------------------------------------------------------------- conv
+@pytest.mark.parametrize("T", [37, 150])
+def test_glu_dwconv(ops, T):
+    torch.manual_seed(T)
+    B, Cc = 2, 128
+    pre = torch.randn(B * T, 2 * Cc, device=DEV).bfloat16()
+    w = torch.randn(Cc, 31, device=DEV) * 0.2
+    out = torch.empty(B * T, Cc, device=DEV, dtype=torch.bfloat16)
+    ops.glu_dwconv_fwd(pre, w, out, B, T)
+    pr = pre.float().clone().requires_grad_()
+    wr = w.clone().requires_grad_()
+    ref = glu_dwconv_ref(pr, wr, B, T)
+    assert rel_err(out, ref) < 5e-3
+    do = torch.randn(B * T, Cc, device=DEV).bfloat16()
+    ref.backward(do.float())
+    dpre = torch.empty_like(pre)
+    dw = torch.zeros_like(w)
+    ops.glu_dwconv_bwd(pre, w, do, dpre, dw, B, T)
+    assert rel_err(dpre, pr.grad) < 5e-3
+    assert rel_err(dw, wr.grad) < 1e-4
+
+
+# ---------------------------------------------------------------- fbank
+def test_fbank_matches_golden(ops):
+    from conftest import GOLDEN
+    z = np.load(GOLDEN / "fbank_golden.npz")
+    cases = list(z["cases"])
+    waves = [z[f"{c}_wave"] for c in cases]
+    N = max(w.size for w in waves)
+    wav = torch.zeros(len(waves), N, device=DEV)
+    for i, w in enumerate(waves):
+        wav[i, : w.size] = torch.from_numpy(w)
+    lens = torch.tensor([w.size for w in waves], dtype=torch.int32, device=DEV)
+    Tmax = z["batch_feats"].shape[1]
+    feats, mask = ops.fbank(wav, lens, Tmax, pad_value=1.0, mask_mode=0)
+    np.testing.assert_array_equal(mask.cpu().numpy(), z["batch_mask"])
+    np.testing.assert_allclose(feats.cpu().numpy(), z["batch_feats"], atol=2e-3, rtol=0)
+    feats1, mask1 = ops.fbank(wav, lens, Tmax, pad_value=1.0, mask_mode=1)
+    for i, c in enumerate(cases):
+        T = z[f"{c}_feats"].shape[0]
+        np.testing.assert_array_equal(mask1[i, :T].cpu().numpy(), z[f"{c}_mask"])
+
+
+# ---------------------------------------------------------------- heads
+def test_attn_pool(ops):
+    torch.manual_seed(3)
+    B, L, H, Hh = 3, 50, 256, 128
+    h = torch.randn(B * L, H, device=DEV).bfloat16()
+    t = torch.tanh(torch.randn(B * L, Hh, device=DEV)).bfloat16()
+    w2 = torch.randn(Hh, device=DEV) * 0.3
+    b2 = torch.randn(1, device=DEV)
+    mask = torch.ones(B * L, dtype=torch.int32, device=DEV)
+    mask[L - 7:L] = 0
+    weights = torch.empty(B * L, device=DEV)
+    pooled = torch.empty(B, H, device=DEV)
+    ops.attn_pool_fwd(t, w2, b2, h, mask, B, L, weights, pooled)
+    tr = t.float().clone().requires_grad_()
+    hr = h.float().clone().requires_grad_()
+    w2r = w2.clone().requires_grad_()
+    b2r = b2.clone().requires_grad_()
+    s = (tr @ w2r + b2r).view(B, L).masked_fill(mask.view(B, L) == 0, -1e9)
+    wref = torch.softmax(s, 1)
+    pref = torch.bmm(wref.unsqueeze(1), hr.view(B, L, H)).squeeze(1)
+    assert rel_err(pooled, pref) < 1e-5
+    dp = torch.randn(B, H, device=DEV)
+    pref.backward(dp)
+    dh = torch.zeros(B * L, H, device=DEV)
+    dz = torch.empty(B * L, Hh, device=DEV, dtype=torch.bfloat16)
+    dw2 = torch.zeros(Hh, device=DEV)
+    db2 = torch.zeros(1, device=DEV)
+    ops.attn_pool_bwd(t, w2, h, weights, dp, B, L, dh, dz, dw2, db2)
+    assert rel_err(dh, hr.grad) < 1e-5
+    assert rel_err(dz, tr.grad * (1 - t.float() ** 2)) < 5e-3
+    assert rel_err(dw2, w2r.grad) < 1e-4
+    assert abs(db2.item() - b2r.grad.item()) < 1e-4
+
+
+@pytest.mark.parametrize("drop_p", [0.0, 0.1])
+def test_xattn1(ops, drop_p):
+    torch.manual_seed(4)
+    B, S, P, nh = 3, 40, 256, 8
+    q = torch.randn(B, P, device=DEV)
+    kv = torch.randn(B * S, 2 * P, device=DEV).bfloat16()
+    k, v = kv[:, :P], kv[:, P:]
+    mask = torch.ones(B * S, dtype=torch.int32, device=DEV)
+    mask[S - 9:S] = 0
+    probs = torch.empty(B * nh * S, device=DEV)
+    out = torch.empty(B, P, device=DEV)
+    seed = 99
+    ops.xattn1_fwd(q, k, v, mask, B, S, nh, probs, out, drop_p=drop_p, seed=seed)
+    d = P // nh
+    qr = q.clone().requires_grad_()
+    kr = k.float().clone().requires_grad_()
+    vr = v.float().clone().requires_grad_()
+    qh = qr.view(B, 1, nh, d).transpose(1, 2)
+    kh = kr.view(B, S, nh, d).transpose(1, 2)
+    vh = vr.view(B, S, nh, d).transpose(1, 2)
+    a = (qh @ kh.transpose(-2, -1)) * d ** -0.5
+    a = a.masked_fill(mask.view(B, 1, 1, S) == 0, -1e9).softmax(-1)
+    if drop_p > 0:
+        idx = np.arange(B * nh * S).astype(np.uint64)
+        a = a * torch.from_numpy(drop_scale(seed, idx, drop_p)).to(DEV).view(B, nh, 1, S)
+    ref = (a @ vh).transpose(1, 2).reshape(B, P)
+    assert rel_err(out, ref) < 1e-5
+    do = torch.randn(B, P, device=DEV)
+    ref.backward(do)
+    dq = torch.empty(B, P, device=DEV)
+    dk = torch.zeros(B * S, P, device=DEV)
+    dv = torch.zeros(B * S, P, device=DEV)
+    ops.xattn1_bwd(q, k, v, probs, do, B, S, nh, dq, dk, dv, drop_p=drop_p, seed=seed)
+    assert rel_err(dq, qr.grad) < 1e-5
+    assert rel_err(dk, kr.grad) < 1e-5
+    assert rel_err(dv, vr.grad) < 1e-5
+
+
+def test_loss_chain(ops):
+    """normalize -> fp32-MFMA similarity -> AlignmentAwareInfoNCE, fwd + bwd vs torch."""
+    torch.manual_seed(5)
+    B, P, L = 20, 96, 9
+    xa, xp, xn = (torch.randn(B, P, device=DEV) for _ in range(3))
+    align = torch.randn(B, L, device=DEV)
+    ya, yp, yn = (torch.empty(B, P, device=DEV) for _ in range(3))
+    na, np_, nn_ = (torch.empty(B, device=DEV) for _ in range(3))
+    for x, y, n in ((xa, ya, na), (xp, yp, np_), (xn, yn, nn_)):
+        ops.l2norm_fwd(x, y, n)
+    S = torch.empty(B, 2 * B, device=DEV)
+    ops.similarity(ya, torch.cat([yp, yn]), S)
+    sp, sn, loss = torch.empty(B, device=DEV), torch.empty(B, device=DEV), torch.empty(1, device=DEV)
+    ops.pair_loss_fwd(S, B, align, B, L, 0.1, 0.5, 0.35, sp, sn, loss)
+    xr = [t.clone().requires_grad_() for t in (xa, xp, xn, align)]
+    a_, p_, n_ = (F.normalize(t, p=2, dim=1) for t in xr[:3])
+    Sref = a_ @ torch.cat([p_, n_]).t()
+    assert rel_err(S, Sref) < 1e-6
+    spr, snr = (a_ * p_).sum(1), (a_ * n_).sum(1)
+    logits = torch.stack([spr, snr], 1) / 0.1
+    per = F.cross_entropy(logits, torch.zeros(B, dtype=torch.long, device=DEV), reduction="none")
+    per = per * (1.0 - torch.sigmoid(xr[3].mean(1)) * 0.5)
+    lref = per.mean() + 0.35 * F.relu(snr).mean()
+    assert abs(loss.item() - lref.item()) < 1e-5 * max(1, abs(lref.item()))
+    lref.backward()
+    dsp, dsn = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    dalign = torch.empty(B, L, device=DEV)
+    ops.pair_loss_bwd(sp, sn, align, B, L, 0.1, 0.5, 0.35, None, dsp, dsn, dalign)
+    assert rel_err(dalign, xr[3].grad) < 1e-5
+    dya, dyp, dyn = (torch.empty(B, P, device=DEV) for _ in range(3))
+    ops.pair_sim_bwd(ya, yp, yn, dsp, dsn, dya, dyp, dyn)
+    for y, n, dy, ref in ((ya, na, dya, xr[0]), (yp, np_, dyp, xr[1]), (yn, nn_, dyn, xr[2])):
+        dx = torch.empty(B, P, device=DEV)
+        ops.l2norm_bwd(y, n, dy, dx)
+        assert rel_err(dx, ref.grad) < 1e-5
+
+
+def test_text_embedding(ops):
+    torch.manual_seed(6)
+    B, L, D, V, pad = 3, 17, 128, 500, 1
+    ids = torch.randint(5, V, (B, L), device=DEV)
+    ids[1, 12:] = pad
+    word = torch.randn(V, D, device=DEV)
+    pos = torch.randn(514, D, device=DEV)
+    typ = torch.randn(1, D, device=DEV)
+    out = torch.empty(B * L, D, device=DEV)
+    pid = torch.empty(B * L, dtype=torch.int32, device=DEV)
+    ops.text_embed_fwd(ids, pad, word, pos, typ, out, pid)
+    nz = (ids != pad).int()
+    pref = (torch.cumsum(nz, 1) * nz).long() + pad
+    assert torch.equal(pid.view(B, L).long(), pref)
+    wr, pr, tr = (t.clone().requires_grad_() for t in (word, pos, typ))
+    ref = F.embedding(ids, wr, padding_idx=pad) + tr[0] + F.embedding(pref, pr, padding_idx=pad)
+    assert rel_err(out, ref.view(B * L, D)) < 1e-6
+    do = torch.randn(B * L, D, device=DEV)
+    ref.backward(do.view(B, L, D))
+    dw, dp_, dt = torch.zeros_like(word), torch.zeros_like(pos), torch.zeros_like(typ)
+    ops.text_embed_bwd(ids, pid, do, pad, dw, dp_, dt)
+    assert rel_err(dw, wr.grad) < 1e-6
+    assert rel_err(dp_, pr.grad) < 1e-6
+    assert rel_err(dt, tr.grad) < 1e-6
+
+
+def test_adamw_clip(ops):
+    torch.manual_seed(8)
+    n = 100003
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV) * 0.01
+    m = torch.randn(n, device=DEV) * 1e-3
+    v = torch.rand(n, device=DEV) * 1e-5
+    acc = torch.zeros(1, device=DEV, dtype=torch.float64)
+    ops.sumsq(g, acc)
+    assert abs(acc.item() - (g.double() ** 2).sum().item()) < 1e-6 * acc.item()
+    pr = p.clone().requires_grad_()
+    opt = torch.optim.AdamW([pr], lr=1e-3, weight_decay=0.01)
+    opt.state[pr] = {"step": torch.tensor(4.0), "exp_avg": m.clone(), "exp_avg_sq": v.clone()}
+    total = acc.sqrt().item()
+    pr.grad = g * min(1.0, 0.05 / (total + 1e-6))
+    opt.step()
+    pb = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    ops.adamw(p, g, m, v, pb, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, wd=0.01, step=5, sumsq_acc=acc,
+              max_norm=0.05)
+    assert rel_err(p, pr.detach()) < 1e-6
+    assert torch.equal(pb, p.bfloat16())
