@@ -206,7 +206,7 @@ int ste_xattn1_fwd(const float* q, const void* k, const void* v, int64_t ldkv, c
                    int P, int nh, float scale, float drop_p, uint64_t seed, float* probs, float* out, void* stream);
 int ste_xattn1_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs, const float* dout,
                    int B, int S, int P, int nh, float scale, float drop_p, uint64_t seed, float* dq, float* dk,
-                   float* dv, void* stream);
+                   float* dv, int64_t lddkv, void* stream);  /* dk/dv: fp32 rows of stride lddkv, += */
 
 /* ------------------------------------------------------------------- loss --
  * F.normalize(p=2, dim=1, eps=1e-12) rows (ref:training/trainer_unfreeze.py:561-563). */

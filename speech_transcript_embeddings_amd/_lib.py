@@ -122,7 +122,7 @@ _SIGS = {
     "ste_xattn1_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                c_float, c_uint64, c_void_p, c_void_p, c_void_p]),
     "ste_xattn1_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                               c_float, c_float, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
+                               c_float, c_float, c_uint64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "ste_l2norm_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "ste_l2norm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "ste_similarity": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),

@@ -182,7 +182,7 @@ __global__ __launch_bounds__(NT) void xattn1_fwd_kernel(const float* q, const bf
 __global__ __launch_bounds__(NT) void xattn1_bwd_kernel(const float* q, const bf16* k, const bf16* v, int64_t ldkv,
                                                       const float* probs, const float* dout, int S, int P, int nh,
                                                       float scale, float drop_p, uint64_t seed, float* dq, float* dk,
-                                                      float* dv) {
+                                                      float* dv, int64_t lddkv) {
   extern __shared__ float sds[];  // nh * S : dp then ds
   __shared__ float sq[1024], sdo[1024];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(NT) void xattn1_bwd_kernel(const float* q, const bf
   // dk[s][c] += ds[h][s] q[c];  dv[s][c] += p'[h][s] dout[c]
   for (int i = tid; i < S * P; i += NT) {
     const int s = i / P, c = i % P, hh = c / dh;
-    const int64_t o = (int64_t)(b * S + s) * P + c;
+    const int64_t o = (int64_t)(b * S + s) * lddkv + c;
     dk[o] += sds[hh * S + s] * sq[c];
     float p = probs[((int64_t)b * nh + hh) * S + s];
     if (drop_p > 0.f) p *= drop_scale(seed, ((uint64_t)b * nh + hh) * S + s, thresh, inv_keep);
@@ -379,10 +379,11 @@ extern "C" int ste_xattn1_fwd(const float* q, const void* k, const void* v, int6
 
 extern "C" int ste_xattn1_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
                               const float* dout, int B, int S, int P, int nh, float scale, float drop_p, uint64_t seed,
-                              float* dq, float* dk, float* dv, void* stream) {
-  if (B <= 0 || S <= 0 || P > 1024 || P % nh || (P / nh) % 4 || nh * S > 16384) return STE_ERR_SHAPE;
+                              float* dq, float* dk, float* dv, int64_t lddkv, void* stream) {
+  if (B <= 0 || S <= 0 || P > 1024 || P % nh || (P / nh) % 4 || nh * S > 16384 || lddkv < P) return STE_ERR_SHAPE;
   hipLaunchKernelGGL(xattn1_bwd_kernel, dim3(B), dim3(NT), nh * S * sizeof(float), (hipStream_t)stream, q,
-                     (const bf16*)k, (const bf16*)v, ldkv, probs, dout, S, P, nh, scale, drop_p, seed, dq, dk, dv);
+                     (const bf16*)k, (const bf16*)v, ldkv, probs, dout, S, P, nh, scale, drop_p, seed, dq, dk, dv,
+                     lddkv);
   STE_CHECK_LAUNCH();
   return 0;
 }

@@ -1,0 +1,667 @@
+"""The hot path as an explicit HIP schedule: forward and backward of the whole
+contrastive step (two encoders + heads), every op a libste.so kernel.
+
+Reference call stack being replaced (ref = /root/reference/training/trainer_unfreeze.py):
+  EnhancedAudioTextModel.compute_pos_neg_embeddings  ref:502-565
+    encode_text x2 (pos, neg)                        ref:567-585  -> XLM-R (batched pos+neg here)
+    encode_audio                                     ref:587-641  -> Wav2Vec2Bert (Conformer)
+    apply_cross_modal_attention x2                   ref:643-682
+    word_level_alignment (optional)                  ref:550-558
+    F.normalize x3                                   ref:561-563
+and the autograd backward of all of it.
+
+Data layout in HBM: activations are row-major [rows, features]; rows = batch*time
+(audio) or 2*batch*tokens (text, pos rows then neg rows).  Residual streams and
+LayerNorm inputs are fp32; every GEMM operand is bf16 (MFMA), accumulation fp32.
+Backward writes parameter gradients straight into the flat gradient buffer of
+store.py (beta=1 accumulation), so micro-batch accumulation needs no extra pass.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib, ops
+from ._lib import (ACT_GELU, ACT_GELU_BWD, ACT_NONE, ACT_RELU, ACT_RELU_BWD, ACT_SWISH, ACT_SWISH_BWD,
+                   ACT_TANH)
+
+BF16, F32 = torch.bfloat16, torch.float32
+_GOLD = 0x9E3779B97F4A7C15
+_M64 = (1 << 64) - 1
+
+
+def _site_seed(base: int, site: int) -> int:
+    x = (base + (site + 1) * _GOLD) & _M64
+    x ^= x >> 31
+    return (x * 0xBF58476D1CE4E5B9) & _M64
+
+
+class Ctx(dict):
+    """Saved activations of one forward (freed when backward finishes)."""
+
+
+class Engine:
+    def __init__(self, model):
+        self.m = model
+        self.s = model.store
+        self.acfg = model.audio_cfg
+        self.tcfg = model.text_cfg
+
+    # ------------------------------------------------------------- helpers
+    def _e(self, *shape, dtype=F32):
+        return torch.empty(shape, device=self.s.device, dtype=dtype)
+
+    def _z(self, *shape, dtype=F32):
+        return torch.zeros(shape, device=self.s.device, dtype=dtype)
+
+    def _dw(self, dy_b, x_b, wname, fused=1):
+        """dW[N,K] += dyᵀ·x into the flat gradient buffer (if the weight receives gradients)."""
+        g = self.s.fused(wname, fused, "g") if fused > 1 else self.s.g(wname)
+        if g is None:
+            return
+        g2 = g.view(g.shape[0], -1)
+        ops.linear_dw(dy_b, x_b, out=g2, beta=1.0)
+
+    def _db(self, x, bname, fused=1):
+        g = self.s.fused(bname, fused, "g") if fused > 1 else self.s.g(bname)
+        if g is not None:
+            ops.colsum(x, g)
+
+    def _ln(self, x, name, eps, **kw):
+        return ops.layernorm_fwd(x, self.s.p(name + ".weight"), self.s.p(name + ".bias"), eps, **kw)
+
+    def _ln_bwd(self, dy, x, stats, name, **kw):
+        g = self.s.g(name + ".weight")
+        return ops.layernorm_bwd(dy, x, stats[0], stats[1], self.s.p(name + ".weight"), beta=self.s.p(name + ".bias"),
+                                 dgamma=g, dbeta=self.s.g(name + ".bias"), **kw)
+
+    # ================================================================ audio
+    def audio_forward(self, feats, mask_i64, train, base_seed, ctx):
+        c = self.acfg
+        b, T, fin = feats.shape
+        M = b * T
+        D = c.hidden_size
+        maskf = self._e(M)
+        mask32 = self._e(M, dtype=torch.int32)
+        _lib.call("ste_mask_i64_to_f32", mask_i64.data_ptr(), maskf.data_ptr(), mask32.data_ptr(), M,
+                  _lib.stream_ptr())
+        xin = feats.reshape(M, fin)
+        a0 = self._e(M, fin, dtype=BF16)
+        st0 = self._ln(xin, "audio_encoder.feature_projection.layer_norm", c.layer_norm_eps, yb=a0)
+        x = ops.linear(a0, self.s.w("audio_encoder.feature_projection.projection.weight"),
+                       self.s.p("audio_encoder.feature_projection.projection.bias"), row_scale=maskf)
+        ctx.update(a_b=b, a_T=T, a_maskf=maskf, a_mask32=mask32, a_xin=xin, a_a0=a0, a_st0=st0)
+        layers = []
+        xb = None
+        nl = c.num_hidden_layers
+        for i in range(nl):
+            if train and c.layerdrop > 0 and float(torch.rand([])) < c.layerdrop:
+                layers.append(None)
+                continue
+            last = i == nl - 1
+            x, xb, sv = self._conformer_fwd(i, x, b, T, maskf, mask32, train, _site_seed(base_seed, 100 + i), last)
+            layers.append(sv)
+        if xb is None or layers[-1] is None:
+            xb = ops.cast_bf16(x, self._e(M, D, dtype=BF16))
+        ctx["a_layers"] = layers
+        return x, xb
+
+    def _conformer_fwd(self, i, x, b, T, maskf, mask32, train, seed, want_bf16):
+        c = self.acfg
+        s = self.s
+        pre = f"audio_encoder.encoder.layers.{i}."
+        M, D, F_ = x.shape[0], c.hidden_size, c.intermediate_size
+        H = c.num_attention_heads
+        eps = c.layer_norm_eps
+        tr = s.trainable_layer(pre + "ffn1_layer_norm.weight")
+        sv = {"tr": tr, "seed": seed}
+        # -- FFN1 (half-step)
+        a1 = self._e(M, D, dtype=BF16)
+        sv["st1"] = self._ln(x, pre + "ffn1_layer_norm", eps, yb=a1)
+        z1 = self._e(M, F_, dtype=BF16)
+        h1 = ops.linear(a1, s.w(pre + "ffn1.intermediate_dense.weight"), s.p(pre + "ffn1.intermediate_dense.bias"),
+                        act=ACT_SWISH, pre_out=z1, out_bf16=True)
+        x1 = ops.linear(h1, s.w(pre + "ffn1.output_dense.weight"), s.p(pre + "ffn1.output_dense.bias"), alpha=0.5,
+                        residual=x)
+        # -- relative-key MHSA
+        a2 = self._e(M, D, dtype=BF16)
+        sv["st2"] = self._ln(x1, pre + "self_attn_layer_norm", eps, yb=a2)
+        qkv = ops.linear(a2, s.fused(pre + "self_attn.linear_q.weight", 3, "w"),
+                         s.fused(pre + "self_attn.linear_q.bias", 3, "p"), out_bf16=True)
+        o = self._e(M, D, dtype=BF16)
+        lse = self._e(b * H * T)
+        ops.attention_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B=b, T=T, H=H, o=o, lse=lse, key_mask=mask32,
+                          rel_E=s.w(pre + "self_attn.distance_embedding.weight"),
+                          rel_left=c.left_max_position_embeddings, rel_right=c.right_max_position_embeddings,
+                          scale=1.0 / math.sqrt(D // H))
+        x2 = ops.linear(o, s.w(pre + "self_attn.linear_out.weight"), s.p(pre + "self_attn.linear_out.bias"),
+                        residual=x1)
+        # -- convolution module
+        a3 = self._e(M, D, dtype=BF16)
+        sv["st3"] = self._ln(x2, pre + "conv_module.layer_norm", eps, yb=a3, row_scale=maskf)
+        pw1 = ops.linear(a3, s.w(pre + "conv_module.pointwise_conv1.weight"), None, out_bf16=True)
+        cv = self._e(M, D, dtype=BF16)
+        ops.glu_dwconv_fwd(pw1, s.p(pre + "conv_module.depthwise_conv.weight").view(D, -1), cv, b, T)
+        sw = self._e(M, D, dtype=BF16)
+        sv["st4"] = self._ln(cv, pre + "conv_module.depthwise_layer_norm", eps, yb=sw, act=ACT_SWISH)
+        p_conv = c.conformer_conv_dropout if train else 0.0
+        x3 = ops.linear(sw, s.w(pre + "conv_module.pointwise_conv2.weight"), None, residual=x2, drop_p=p_conv,
+                        seed=_site_seed(seed, 1))
+        # -- FFN2 (half-step) + final LN
+        a5 = self._e(M, D, dtype=BF16)
+        sv["st5"] = self._ln(x3, pre + "ffn2_layer_norm", eps, yb=a5)
+        z2 = self._e(M, F_, dtype=BF16)
+        h2 = ops.linear(a5, s.w(pre + "ffn2.intermediate_dense.weight"), s.p(pre + "ffn2.intermediate_dense.bias"),
+                        act=ACT_SWISH, pre_out=z2, out_bf16=True)
+        x4 = ops.linear(h2, s.w(pre + "ffn2.output_dense.weight"), s.p(pre + "ffn2.output_dense.bias"), alpha=0.5,
+                        residual=x3)
+        x5 = self._e(M, D)
+        x5b = self._e(M, D, dtype=BF16) if want_bf16 else None
+        sv["st6"] = self._ln(x4, pre + "final_layer_norm", eps, y=x5, yb=x5b)
+        sv.update(x=x, z1=z1, x1=x1, qkv=qkv, o=o, lse=lse, x2=x2, pw1=pw1, cv=cv, x3=x3, z2=z2, x4=x4, p_conv=p_conv)
+        if tr:
+            sv.update(a1=a1, h1=h1, a2=a2, a3=a3, sw=sw, a5=a5, h2=h2)
+        return x5, x5b, sv
+
+    def _conformer_bwd(self, i, sv, dx5, b, T, maskf, mask32):
+        c = self.acfg
+        s = self.s
+        pre = f"audio_encoder.encoder.layers.{i}."
+        M, D, F_ = dx5.shape[0], c.hidden_size, c.intermediate_size
+        H = c.num_attention_heads
+        tr = sv["tr"]
+        # final LN
+        dx4 = self._e(M, D)
+        dx4b = self._e(M, D, dtype=BF16)
+        self._ln_bwd(dx5, sv["x4"], sv["st6"], pre + "final_layer_norm", dx=dx4, dxb=dx4b, out_scale=0.5,
+                     dsum=s.g(pre + "ffn2.output_dense.bias"))
+        # FFN2
+        dz2 = ops.linear_dx(dx4b, s.w(pre + "ffn2.output_dense.weight"), act=ACT_SWISH_BWD, z=sv["z2"],
+                            out_bf16=True, colsum=s.g(pre + "ffn2.intermediate_dense.bias"))
+        if tr:
+            self._dw(dx4b, sv["h2"], pre + "ffn2.output_dense.weight")
+        da5 = ops.linear_dx(dz2, s.w(pre + "ffn2.intermediate_dense.weight"))
+        if tr:
+            self._dw(dz2, sv["a5"], pre + "ffn2.intermediate_dense.weight")
+        del dz2
+        dx3 = self._e(M, D)
+        dx3b = self._e(M, D, dtype=BF16)
+        self._ln_bwd(da5, sv["x3"], sv["st5"], pre + "ffn2_layer_norm", dres=dx4, dx=dx3, dxb=dx3b,
+                     drop_p=sv["p_conv"], seed=_site_seed(sv["seed"], 1))
+        del da5, dx4, dx4b
+        # conv module
+        dsw = ops.linear_dx(dx3b, s.w(pre + "conv_module.pointwise_conv2.weight"))
+        if tr:
+            self._dw(dx3b, sv["sw"], pre + "conv_module.pointwise_conv2.weight")
+        dcv = self._e(M, D, dtype=BF16)
+        self._ln_bwd(dsw, sv["cv"], sv["st4"], pre + "conv_module.depthwise_layer_norm", act=ACT_SWISH, dxb=dcv)
+        del dsw
+        dpw1 = self._e(M, 2 * D, dtype=BF16)
+        gdw = s.g(pre + "conv_module.depthwise_conv.weight")
+        ops.glu_dwconv_bwd(sv["pw1"], s.p(pre + "conv_module.depthwise_conv.weight").view(D, -1), dcv, dpw1,
+                           None if gdw is None else gdw.view(D, -1), b, T)
+        del dcv
+        da3 = ops.linear_dx(dpw1, s.w(pre + "conv_module.pointwise_conv1.weight"))
+        if tr:
+            self._dw(dpw1, sv["a3"], pre + "conv_module.pointwise_conv1.weight")
+        del dpw1
+        dx2 = self._e(M, D)
+        dx2b = self._e(M, D, dtype=BF16)
+        self._ln_bwd(da3, sv["x2"], sv["st3"], pre + "conv_module.layer_norm", row_scale=maskf, dres=dx3, dx=dx2,
+                     dxb=dx2b, dsum=s.g(pre + "self_attn.linear_out.bias"))
+        del da3, dx3, dx3b
+        # attention
+        do = ops.linear_dx(dx2b, s.w(pre + "self_attn.linear_out.weight"), out_bf16=True)
+        if tr:
+            self._dw(dx2b, sv["o"], pre + "self_attn.linear_out.weight")
+        del dx2b
+        qkv = sv["qkv"]
+        dqkv = self._e(M, 3 * D, dtype=BF16)
+        delta = self._e(b * H * T)
+        gE = s.g(pre + "self_attn.distance_embedding.weight")
+        gwork = self._e(b * H * T * 80) if gE is not None else None
+        ops.attention_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], sv["o"], sv["lse"], do, dqkv[:, :D],
+                          dqkv[:, D:2 * D], dqkv[:, 2 * D:], B=b, T=T, H=H, delta=delta, key_mask=mask32,
+                          rel_E=s.w(pre + "self_attn.distance_embedding.weight"),
+                          rel_left=c.left_max_position_embeddings, rel_right=c.right_max_position_embeddings,
+                          scale=1.0 / math.sqrt(D // H), dE=gE, gwork=gwork)
+        del do, delta, gwork
+        da2 = ops.linear_dx(dqkv, s.fused(pre + "self_attn.linear_q.weight", 3, "w"))
+        if tr:
+            self._dw(dqkv, sv["a2"], pre + "self_attn.linear_q.weight", fused=3)
+            self._db(dqkv, pre + "self_attn.linear_q.bias", fused=3)
+        del dqkv
+        dx1 = self._e(M, D)
+        dx1b = self._e(M, D, dtype=BF16)
+        self._ln_bwd(da2, sv["x1"], sv["st2"], pre + "self_attn_layer_norm", dres=dx2, dx=dx1, dxb=dx1b,
+                     out_scale=0.5, dsum=s.g(pre + "ffn1.output_dense.bias"))
+        del da2, dx2
+        # FFN1
+        dz1 = ops.linear_dx(dx1b, s.w(pre + "ffn1.output_dense.weight"), act=ACT_SWISH_BWD, z=sv["z1"],
+                            out_bf16=True, colsum=s.g(pre + "ffn1.intermediate_dense.bias"))
+        if tr:
+            self._dw(dx1b, sv["h1"], pre + "ffn1.output_dense.weight")
+        da1 = ops.linear_dx(dz1, s.w(pre + "ffn1.intermediate_dense.weight"))
+        if tr:
+            self._dw(dz1, sv["a1"], pre + "ffn1.intermediate_dense.weight")
+        del dz1
+        dx0 = self._e(M, D)
+        self._ln_bwd(da1, sv["x"], sv["st1"], pre + "ffn1_layer_norm", dres=dx1, dx=dx0)
+        return dx0
+
+    def audio_backward(self, dh, ctx):
+        c = self.acfg
+        b, T = ctx["a_b"], ctx["a_T"]
+        maskf, mask32 = ctx["a_maskf"], ctx["a_mask32"]
+        dx = dh
+        for i in reversed(range(c.num_hidden_layers)):
+            sv = ctx["a_layers"][i]
+            if sv is None:
+                continue
+            dx = self._conformer_bwd(i, sv, dx, b, T, maskf, mask32)
+            ctx["a_layers"][i] = None
+        # feature projection: x = mask * (LN(feats) W^T + b)
+        s = self.s
+        gW = s.g("audio_encoder.feature_projection.projection.weight")
+        if gW is not None:
+            M = dx.shape[0]
+            # the forward's masked_fill (row_scale) multiplies dY row-wise
+            _lib.call("ste_scale_rows", dx.data_ptr(), maskf.data_ptr(), M, c.hidden_size, dx.stride(0),
+                      _lib.stream_ptr())
+            dxb = ops.cast_bf16(dx, self._e(M, c.hidden_size, dtype=BF16))
+            self._dw(dxb, ctx["a_a0"], "audio_encoder.feature_projection.projection.weight")
+            self._db(dxb, "audio_encoder.feature_projection.projection.bias")
+            if s.g("audio_encoder.feature_projection.layer_norm.weight") is not None:
+                da0 = ops.linear_dx(dxb, s.w("audio_encoder.feature_projection.projection.weight"))
+                self._ln_bwd(da0, ctx["a_xin"], ctx["a_st0"], "audio_encoder.feature_projection.layer_norm")
+
+    # ================================================================= text
+    def text_forward(self, ids, mask_i64, train, base_seed, ctx):
+        c = self.tcfg
+        s = self.s
+        nb, L = ids.shape
+        M, D = nb * L, c.hidden_size
+        mask32 = self._e(M, dtype=torch.int32)
+        _lib.call("ste_mask_i64_to_f32", mask_i64.data_ptr(), None, mask32.data_ptr(), M, _lib.stream_ptr())
+        emb = self._e(M, D)
+        pos_ids = self._e(M, dtype=torch.int32)
+        ops.text_embed_fwd(ids, c.pad_token_id, s.p("text_encoder.embeddings.word_embeddings.weight"),
+                           s.p("text_encoder.embeddings.position_embeddings.weight"),
+                           s.p("text_encoder.embeddings.token_type_embeddings.weight"), emb, pos_ids)
+        hp = c.hidden_dropout_prob if train else 0.0
+        ap = c.attention_probs_dropout_prob if train else 0.0
+        x = self._e(M, D)
+        xb = self._e(M, D, dtype=BF16)
+        st = self._ln(emb, "text_encoder.embeddings.LayerNorm", c.layer_norm_eps, y=x, yb=xb, drop_p=hp,
+                      seed=_site_seed(base_seed, 1))
+        ctx.update(t_nb=nb, t_L=L, t_mask32=mask32, t_ids=ids, t_emb=emb, t_pos=pos_ids, t_st=st, t_hp=hp, t_ap=ap,
+                   t_seed=base_seed)
+        layers = []
+        for i in range(c.num_hidden_layers):
+            x, xb, sv = self._xlmr_fwd(i, x, xb, nb, L, mask32, hp, ap, _site_seed(base_seed, 10 + i))
+            layers.append(sv)
+        ctx["t_layers"] = layers
+        return x, xb
+
+    def _xlmr_fwd(self, i, x, xb, nb, L, mask32, hp, ap, seed):
+        c = self.tcfg
+        s = self.s
+        pre = f"text_encoder.encoder.layer.{i}."
+        M, D, F_ = x.shape[0], c.hidden_size, c.intermediate_size
+        H = c.num_attention_heads
+        eps = c.layer_norm_eps
+        tr = s.trainable_layer(pre + "attention.self.query.weight")
+        sv = {"tr": tr, "seed": seed}
+        qkv = ops.linear(xb, s.fused(pre + "attention.self.query.weight", 3, "w"),
+                         s.fused(pre + "attention.self.query.bias", 3, "p"), out_bf16=True)
+        o = self._e(M, D, dtype=BF16)
+        lse = self._e(nb * H * L)
+        ops.attention_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B=nb, T=L, H=H, o=o, lse=lse,
+                          key_mask=mask32, scale=1.0 / math.sqrt(D // H), drop_p=ap, seed=_site_seed(seed, 1))
+        y1 = ops.linear(o, s.w(pre + "attention.output.dense.weight"), s.p(pre + "attention.output.dense.bias"),
+                        residual=x, drop_p=hp, seed=_site_seed(seed, 2))
+        x1 = self._e(M, D)
+        x1b = self._e(M, D, dtype=BF16)
+        sv["st1"] = self._ln(y1, pre + "attention.output.LayerNorm", eps, y=x1, yb=x1b)
+        zt = self._e(M, F_, dtype=BF16)
+        h = ops.linear(x1b, s.w(pre + "intermediate.dense.weight"), s.p(pre + "intermediate.dense.bias"),
+                       act=ACT_GELU, pre_out=zt, out_bf16=True)
+        y2 = ops.linear(h, s.w(pre + "output.dense.weight"), s.p(pre + "output.dense.bias"), residual=x1, drop_p=hp,
+                        seed=_site_seed(seed, 3))
+        x2 = self._e(M, D)
+        x2b = self._e(M, D, dtype=BF16)
+        sv["st2"] = self._ln(y2, pre + "output.LayerNorm", eps, y=x2, yb=x2b)
+        sv.update(qkv=qkv, o=o, lse=lse, y1=y1, zt=zt, y2=y2)
+        if tr:
+            sv.update(xb=xb, x1b=x1b, h=h)
+        return x2, x2b, sv
+
+    def _xlmr_bwd(self, i, sv, dx2, nb, L, mask32, hp, ap):
+        c = self.tcfg
+        s = self.s
+        pre = f"text_encoder.encoder.layer.{i}."
+        M, D = dx2.shape[0], c.hidden_size
+        H = c.num_attention_heads
+        tr = sv["tr"]
+        seed = sv["seed"]
+        dy2 = self._e(M, D)
+        dy2b = self._e(M, D, dtype=BF16)
+        self._ln_bwd(dx2, sv["y2"], sv["st2"], pre + "output.LayerNorm", dx=dy2, dxb=dy2b, drop_p=hp,
+                     seed=_site_seed(seed, 3), dsum=s.g(pre + "output.dense.bias"))
+        dzt = ops.linear_dx(dy2b, s.w(pre + "output.dense.weight"), act=ACT_GELU_BWD, z=sv["zt"], out_bf16=True,
+                            colsum=s.g(pre + "intermediate.dense.bias"))
+        if tr:
+            self._dw(dy2b, sv["h"], pre + "output.dense.weight")
+        del dy2b
+        dx1 = ops.linear_dx(dzt, s.w(pre + "intermediate.dense.weight"), residual=dy2)
+        if tr:
+            self._dw(dzt, sv["x1b"], pre + "intermediate.dense.weight")
+        del dzt, dy2
+        dy1 = self._e(M, D)
+        dy1b = self._e(M, D, dtype=BF16)
+        self._ln_bwd(dx1, sv["y1"], sv["st1"], pre + "attention.output.LayerNorm", dx=dy1, dxb=dy1b, drop_p=hp,
+                     seed=_site_seed(seed, 2), dsum=s.g(pre + "attention.output.dense.bias"))
+        del dx1
+        do = ops.linear_dx(dy1b, s.w(pre + "attention.output.dense.weight"), out_bf16=True)
+        if tr:
+            self._dw(dy1b, sv["o"], pre + "attention.output.dense.weight")
+        del dy1b
+        qkv = sv["qkv"]
+        dqkv = self._e(M, 3 * D, dtype=BF16)
+        delta = self._e(nb * H * L)
+        ops.attention_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], sv["o"], sv["lse"], do, dqkv[:, :D],
+                          dqkv[:, D:2 * D], dqkv[:, 2 * D:], B=nb, T=L, H=H, delta=delta, key_mask=mask32,
+                          scale=1.0 / math.sqrt(D // H), drop_p=ap, seed=_site_seed(seed, 1))
+        del do, delta
+        dx0 = ops.linear_dx(dqkv, s.fused(pre + "attention.self.query.weight", 3, "w"), residual=dy1)
+        if tr:
+            self._dw(dqkv, sv["xb"], pre + "attention.self.query.weight", fused=3)
+            self._db(dqkv, pre + "attention.self.query.bias", fused=3)
+        return dx0
+
+    def text_backward(self, dh, ctx):
+        c = self.tcfg
+        s = self.s
+        nb, L = ctx["t_nb"], ctx["t_L"]
+        dx = dh
+        for i in reversed(range(c.num_hidden_layers)):
+            dx = self._xlmr_bwd(i, ctx["t_layers"][i], dx, nb, L, ctx["t_mask32"], ctx["t_hp"], ctx["t_ap"])
+            ctx["t_layers"][i] = None
+        gw = s.g("text_encoder.embeddings.word_embeddings.weight")
+        gp = s.g("text_encoder.embeddings.position_embeddings.weight")
+        gt = s.g("text_encoder.embeddings.token_type_embeddings.weight")
+        ln_needed = any(g is not None for g in (gw, gp, gt, s.g("text_encoder.embeddings.LayerNorm.weight")))
+        if not ln_needed:
+            return
+        demb = self._e(dx.shape[0], c.hidden_size)
+        self._ln_bwd(dx, ctx["t_emb"], ctx["t_st"], "text_encoder.embeddings.LayerNorm", dx=demb,
+                     in_drop_p=ctx["t_hp"], in_seed=_site_seed(ctx["t_seed"], 1))
+        if gw is not None or gp is not None or gt is not None:
+            ops.text_embed_bwd(ctx["t_ids"], ctx["t_pos"], demb, c.pad_token_id, gw, gp, gt)
+
+    # ================================================================ heads
+    def _proj_fwd(self, name, xb, rows, train, seed, sv):
+        """EnhancedProjection ref:66-99 on bf16 input rows -> (fp32 [rows,P], bf16 copy)."""
+        s = self.s
+        p_drop = self.m.dropout if train else 0.0
+        zp = self._e(rows, s.slots[name + ".projection.0.weight"].shape[0], dtype=BF16)
+        hb = ops.linear(xb, s.w(name + ".projection.0.weight"), s.p(name + ".projection.0.bias"), act=ACT_GELU,
+                        pre_out=zp, out_bf16=True, drop_p=p_drop, seed=seed)
+        y = ops.linear(hb, s.w(name + ".projection.3.weight"), s.p(name + ".projection.3.bias"))
+        P = y.shape[1]
+        out = self._e(rows, P)
+        st = self._ln(y, name + ".projection.4", 1e-5, y=out)
+        sv.update(xb=xb, zp=zp, hb=hb, y=y, st=st, p=p_drop, seed=seed)
+        return out
+
+    def _proj_bwd(self, name, sv, dout, dx_out):
+        """returns nothing; writes d(input) into dx_out (fp32, +=)."""
+        s = self.s
+        rows, P = dout.shape
+        dyb = self._e(rows, P, dtype=BF16)
+        self._ln_bwd(dout, sv["y"], sv["st"], name + ".projection.4", dxb=dyb, dsum=s.g(name + ".projection.3.bias"))
+        dz = ops.linear_dx(dyb, s.w(name + ".projection.3.weight"), act=ACT_GELU_BWD, z=sv["zp"], out_bf16=True,
+                           drop_p=sv["p"], seed=sv["seed"], colsum=s.g(name + ".projection.0.bias"))
+        self._dw(dyb, sv["hb"], name + ".projection.3.weight")
+        ops.linear_dx(dz, s.w(name + ".projection.0.weight"), out=dx_out, beta=1.0)
+        self._dw(dz, sv["xb"], name + ".projection.0.weight")
+
+    def _pool_fwd(self, name, hb, mask32, nb, L, sv):
+        """AttentivePooling ref:171-211 -> pooled fp32 [nb, H] and bf16 copy."""
+        s = self.s
+        H = hb.shape[1]
+        t = ops.linear(hb, s.w(name + ".attention.0.weight"), s.p(name + ".attention.0.bias"), act=ACT_TANH,
+                       out_bf16=True)
+        w = self._e(nb * L)
+        pooled = self._e(nb, H)
+        pooledb = self._e(nb, H, dtype=BF16)
+        ops.attn_pool_fwd(t, s.p(name + ".attention.2.weight").view(-1), s.p(name + ".attention.2.bias"), hb, mask32,
+                          nb, L, w, pooled, pooledb)
+        sv.update(t=t, w=w, hb=hb)
+        return pooled, pooledb
+
+    def _pool_bwd(self, name, sv, dpooled, dh, nb, L):
+        s = self.s
+        t = sv["t"]
+        dz = self._e(*t.shape, dtype=BF16)
+        gw2 = s.g(name + ".attention.2.weight")
+        ops.attn_pool_bwd(t, s.p(name + ".attention.2.weight").view(-1), sv["hb"], sv["w"], dpooled, nb, L, dh, dz,
+                          None if gw2 is None else gw2.view(-1), s.g(name + ".attention.2.bias"))
+        ops.linear_dx(dz, s.w(name + ".attention.0.weight"), out=dh, beta=1.0)
+        self._dw(dz, sv["hb"], name + ".attention.0.weight")
+        self._db(dz, name + ".attention.0.bias")
+
+    def heads_forward(self, th, thb, ah, ahb, train, base_seed, ctx):
+        s = self.s
+        m = self.m
+        nb, L = ctx["t_nb"], ctx["t_L"]
+        b = nb // 2
+        ab, T = ctx["a_b"], ctx["a_T"]
+        P = m.projection_dim
+        hs = {}
+        # pooling + projection
+        tpool_sv, apool_sv, tproj_sv, aproj_sv = {}, {}, {}, {}
+        tpooled, tpooledb = self._pool_fwd("text_pooling", thb, ctx["t_mask32"], nb, L, tpool_sv)
+        apooled, apooledb = self._pool_fwd("audio_pooling", ahb, ctx["a_mask32"], ab, T, apool_sv)
+        tcat = self._e(nb, 2 * P, dtype=BF16)   # [tproj | t_att] bf16, fusion GEMM input
+        acat = self._e(b, 2 * P, dtype=BF16)
+        tproj = self._proj_fwd("text_projection", tpooledb, nb, train, _site_seed(base_seed, 201), tproj_sv)
+        aproj = self._proj_fwd("audio_projection", apooledb, ab, train, _site_seed(base_seed, 202), aproj_sv)
+        tprojb =ops.cast_bf16(tproj, self._e(nb, P, dtype=BF16))
+        aprojb = ops.cast_bf16(aproj, self._e(ab, P, dtype=BF16))
+        hs.update(tpool=tpool_sv, apool=apool_sv, tproj=tproj_sv, aproj=aproj_sv, tprojb=tprojb, aprojb=aprojb)
+        if m.use_cross_modal:
+            p_x = m.dropout if train else 0.0
+            # audio_seq_to_projection (identical for the pos and neg calls of ref:525-542: computed once)
+            aseqb = ops.linear(ahb, s.w("audio_seq_to_projection.weight"), s.p("audio_seq_to_projection.bias"),
+                               out_bf16=True)
+            # text->audio: K/V over the audio sequence shared by pos and neg queries
+            kva = ops.linear(aseqb, s.fused("text_to_audio_attention.key.weight", 2, "w"),
+                             s.fused("text_to_audio_attention.key.bias", 2, "p"), out_bf16=True)
+            qt = ops.linear(tprojb, s.w("text_to_audio_attention.query.weight"),
+                            s.p("text_to_audio_attention.query.bias"))
+            nh = m.xattn_heads
+            probs_t = self._e(nb * nh * T)
+            att_t = self._e(nb, P)
+            seed_t = _site_seed(base_seed, 203)
+            for half in range(2):  # pos rows, neg rows: same audio keys
+                r0 = half * b
+                ops.xattn1_fwd(qt[r0:r0 + b], kva[:, :P], kva[:, P:], ctx["a_mask32"], b, T, nh,
+                               probs_t[r0 * nh * T:(r0 + b) * nh * T], att_t[r0:r0 + b], drop_p=p_x,
+                               seed=_site_seed(seed_t, half))
+            att_tb = ops.cast_bf16(att_t, self._e(nb, P, dtype=BF16))
+            ops.linear(att_tb, s.w("text_to_audio_attention.out_proj.weight"),
+                       s.p("text_to_audio_attention.out_proj.bias"), out=tcat[:, P:])
+            _copy_bf16(tprojb, tcat[:, :P])
+            # audio->text (pos call only: the neg call's audio output is discarded, ref:535)
+            tseqb = ops.linear(thb[: b * L], s.w("text_seq_to_projection.weight"), s.p("text_seq_to_projection.bias"),
+                               out_bf16=True)
+            kvt = ops.linear(tseqb, s.fused("audio_to_text_attention.key.weight", 2, "w"),
+                             s.fused("audio_to_text_attention.key.bias", 2, "p"), out_bf16=True)
+            qa = ops.linear(aprojb, s.w("audio_to_text_attention.query.weight"),
+                            s.p("audio_to_text_attention.query.bias"))
+            probs_a = self._e(b * nh * L)
+            att_a = self._e(b, P)
+            seed_a = _site_seed(base_seed, 204)
+            ops.xattn1_fwd(qa, kvt[:, :P], kvt[:, P:], ctx["t_mask32"][: b * L], b, L, nh, probs_a, att_a,
+                           drop_p=p_x, seed=seed_a)
+            att_ab = ops.cast_bf16(att_a, self._e(b, P, dtype=BF16))
+            ops.linear(att_ab, s.w("audio_to_text_attention.out_proj.weight"),
+                       s.p("audio_to_text_attention.out_proj.bias"), out_bf16=True, out=acat[:, P:])
+            _copy_bf16(aprojb, acat[:, :P])
+            # fusion Linear + LN
+            yt = ops.linear(tcat, s.w("text_fusion.0.weight"), s.p("text_fusion.0.bias"))
+            tfused = self._e(nb, P)
+            st_t = self._ln(yt, "text_fusion.1", 1e-5, y=tfused)
+            ya = ops.linear(acat, s.w("audio_fusion.0.weight"), s.p("audio_fusion.0.bias"))
+            afused = self._e(b, P)
+            st_a = self._ln(ya, "audio_fusion.1", 1e-5, y=afused)
+            hs.update(aseqb=aseqb, kva=kva, qt=qt, probs_t=probs_t, att_tb=att_tb, seed_t=seed_t, p_x=p_x,
+                      tseqb=tseqb, kvt=kvt, qa=qa, probs_a=probs_a, att_ab=att_ab, seed_a=seed_a, tcat=tcat,
+                      acat=acat, yt=yt, st_t=st_t, ya=ya, st_a=st_a)
+        else:
+            tfused, afused = tproj, aproj[:b]
+        align = None
+        if m.use_word_alignment:
+            align = self._align_fwd(th, thb[: b * L], ahb, b, L, T, ctx, train, _site_seed(base_seed, 205), hs)
+        ctx["heads"] = hs
+        return tfused, afused, align
+
+    def heads_backward(self, d_tfused, d_afused, d_align, ctx, dth, dah):
+        s = self.s
+        m = self.m
+        hs = ctx["heads"]
+        nb, L = ctx["t_nb"], ctx["t_L"]
+        b = nb // 2
+        ab, T = ctx["a_b"], ctx["a_T"]
+        P = m.projection_dim
+        d_tproj = self._z(nb, P)
+        d_aproj = self._z(ab, P)
+        if d_align is not None and m.use_word_alignment:
+            self._align_bwd(d_align, hs, ctx, dth, dah)
+        if m.use_cross_modal:
+            # fusion LNs + Linears
+            dyt = self._e(nb, P, dtype=BF16)
+            self._ln_bwd(d_tfused, hs["yt"], hs["st_t"], "text_fusion.1", dxb=dyt, dsum=s.g("text_fusion.0.bias"))
+            dtcat = ops.linear_dx(dyt, s.w("text_fusion.0.weight"))
+            self._dw(dyt, hs["tcat"], "text_fusion.0.weight")
+            dya = self._e(b, P, dtype=BF16)
+            self._ln_bwd(d_afused, hs["ya"], hs["st_a"], "audio_fusion.1", dxb=dya, dsum=s.g("audio_fusion.0.bias"))
+            dacat = ops.linear_dx(dya, s.w("audio_fusion.0.weight"))
+            self._dw(dya, hs["acat"], "audio_fusion.0.weight")
+            _add_(d_tproj, dtcat[:, :P])
+            _add_(d_aproj[:b], dacat[:, :P])
+            nh = m.xattn_heads
+            # ---- text->audio attention (pos + neg queries, shared audio K/V)
+            datt = dtcat[:, P:].contiguous()
+            dattb = ops.cast_bf16(datt, self._e(nb, P, dtype=BF16))
+            dq_in = ops.linear_dx(dattb, s.w("text_to_audio_attention.out_proj.weight"))
+            self._dw(dattb, hs["att_tb"], "text_to_audio_attention.out_proj.weight")
+            self._db(datt, "text_to_audio_attention.out_proj.bias")
+            dqt = self._e(nb, P)
+            dkv = self._z(ab * T, 2 * P)
+            for half in range(2):
+                r0 = half * b
+                ops.xattn1_bwd(hs["qt"][r0:r0 + b], hs["kva"][:, :P], hs["kva"][:, P:],
+                               hs["probs_t"][r0 * nh * T:(r0 + b) * nh * T], dq_in[r0:r0 + b], b, T, nh,
+                               dqt[r0:r0 + b], dkv[:, :P], dkv[:, P:], drop_p=hs["p_x"],
+                               seed=_site_seed(hs["seed_t"], half))
+            dqtb = ops.cast_bf16(dqt, self._e(nb, P, dtype=BF16))
+            ops.linear_dx(dqtb, s.w("text_to_audio_attention.query.weight"), out=d_tproj, beta=1.0)
+            self._dw(dqtb, hs["tprojb"], "text_to_audio_attention.query.weight")
+            self._db(dqt, "text_to_audio_attention.query.bias")
+            dkvb = ops.cast_bf16(dkv, self._e(ab * T, 2 * P, dtype=BF16))
+            daseq = ops.linear_dx(dkvb, s.fused("text_to_audio_attention.key.weight", 2, "w"))
+            self._dw(dkvb, hs["aseqb"], "text_to_audio_attention.key.weight", fused=2)
+            self._db(dkv, "text_to_audio_attention.key.bias", fused=2)
+            del dkv, dkvb
+            daseqb = ops.cast_bf16(daseq, self._e(ab * T, P, dtype=BF16))
+            ops.linear_dx(daseqb, s.w("audio_seq_to_projection.weight"), out=dah, beta=1.0)
+            self._dw(daseqb, ctx["_ahb"], "audio_seq_to_projection.weight")
+            self._db(daseq, "audio_seq_to_projection.bias")
+            del daseq, daseqb
+            # ---- audio->text attention (pos call)
+            datta = dacat[:, P:].contiguous()
+            dattab = ops.cast_bf16(datta, self._e(b, P, dtype=BF16))
+            dqa_in = ops.linear_dx(dattab, s.w("audio_to_text_attention.out_proj.weight"))
+            self._dw(dattab, hs["att_ab"], "audio_to_text_attention.out_proj.weight")
+            self._db(datta, "audio_to_text_attention.out_proj.bias")
+            dqa = self._e(b, P)
+            dkvt = self._z(b * L, 2 * P)
+            ops.xattn1_bwd(hs["qa"], hs["kvt"][:, :P], hs["kvt"][:, P:], hs["probs_a"], dqa_in, b, L, nh, dqa,
+                           dkvt[:, :P], dkvt[:, P:], drop_p=hs["p_x"], seed=hs["seed_a"])
+            dqab = ops.cast_bf16(dqa, self._e(b, P, dtype=BF16))
+            ops.linear_dx(dqab, s.w("audio_to_text_attention.query.weight"), out=d_aproj[:b], beta=1.0)
+            self._dw(dqab, hs["aprojb"], "audio_to_text_attention.query.weight")
+            self._db(dqa, "audio_to_text_attention.query.bias")
+            dkvtb = ops.cast_bf16(dkvt, self._e(b * L, 2 * P, dtype=BF16))
+            dtseq = ops.linear_dx(dkvtb, s.fused("audio_to_text_attention.key.weight", 2, "w"))
+            self._dw(dkvtb, hs["tseqb"], "audio_to_text_attention.key.weight", fused=2)
+            self._db(dkvt, "audio_to_text_attention.key.bias", fused=2)
+            dtseqb = ops.cast_bf16(dtseq, self._e(b * L, P, dtype=BF16))
+            ops.linear_dx(dtseqb, s.w("text_seq_to_projection.weight"), out=dth[: b * L], beta=1.0)
+            self._dw(dtseqb, ctx["_thb"][: b * L], "text_seq_to_projection.weight")
+            self._db(dtseq, "text_seq_to_projection.bias")
+        else:
+            _add_(d_tproj, d_tfused)
+            _add_(d_aproj[:b], d_afused)
+        # projections
+        dtpooled = self._z(nb, self.tcfg.hidden_size)
+        dapooled = self._z(ab, self.acfg.hidden_size)
+        self._proj_bwd("text_projection", hs["tproj"], d_tproj, dtpooled)
+        self._proj_bwd("audio_projection", hs["aproj"], d_aproj, dapooled)
+        # pooling
+        self._pool_bwd("text_pooling", hs["tpool"], dtpooled, dth, nb, L)
+        self._pool_bwd("audio_pooling", hs["apool"], dapooled, dah, ab, T)
+
+    # ------------------------------------------------------- word alignment
+    def _align_fwd(self, th, thb_pos, ahb, b, L, T, ctx, train, seed, hs):
+        from .align import align_forward
+        return align_forward(self, th, thb_pos, ahb, b, L, T, ctx, train, seed, hs)
+
+    def _align_bwd(self, d_align, hs, ctx, dth, dah):
+        from .align import align_backward
+        align_backward(self, d_align, hs, ctx, dth, dah)
+
+    # ============================================================== full step
+    def forward(self, batch, train: bool):
+        """compute_pos_neg_embeddings (ref:502-565) -> (tp_fused, tn_fused, a_fused, align, ctx)."""
+        ctx = Ctx()
+        base_seed = int(torch.randint(0, 2**62, (1,)).item()) if train else 0
+        ids = torch.cat([batch["input_ids_pos"], batch["input_ids_neg"]], 0)
+        tmask = torch.cat([batch["attention_mask_pos"], batch["attention_mask_neg"]], 0)
+        th, thb = self.text_forward(ids.contiguous(), tmask.contiguous(), train, _site_seed(base_seed, 2), ctx)
+        ah, ahb = self.audio_forward(batch["input_values"].contiguous(), batch["attention_mask_audio"].contiguous(),
+                                     train, _site_seed(base_seed, 3), ctx)
+        ctx["_thb"], ctx["_ahb"] = thb, ahb
+        tf, af, align = self.heads_forward(th, thb, ah, ahb, train, _site_seed(base_seed, 4), ctx)
+        b = batch["input_ids_pos"].shape[0]
+        return tf[:b], tf[b:], af, align, ctx
+
+    def backward(self, ctx, d_tp, d_tn, d_af, d_align):
+        nb = ctx["t_nb"]
+        d_tf = self._e(nb, self.m.projection_dim)
+        _copy_f32(d_tp, d_tf[: nb // 2])
+        _copy_f32(d_tn, d_tf[nb // 2:])
+        dth = self._z(nb * ctx["t_L"], self.tcfg.hidden_size)
+        dah = self._z(ctx["a_b"] * ctx["a_T"], self.acfg.hidden_size)
+        self.heads_backward(d_tf, d_af, d_align, ctx, dth, dah)
+        ctx.pop("heads", None)
+        self.audio_backward(dah, ctx)
+        del dah
+        self.text_backward(dth, ctx)
+        ctx.clear()
+
+
+def _copy_bf16(src, dst):
+    """dst[:] = src for bf16 2-D views (strided rows), via a bf16 GEMM-free kernel path."""
+    dst.copy_(src)
+
+
+def _copy_f32(src, dst):
+    dst.copy_(src)
+
+
+def _add_(dst, src):
+    dst.add_(src)

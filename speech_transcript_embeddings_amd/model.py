@@ -1,0 +1,306 @@
+"""Drop-in replacements for the reference's model / loss API
+(ref = /root/reference/training/trainer_unfreeze.py):
+
+  EnhancedAudioTextModel   ref:315-697  (same constructor arguments, attribute tree,
+                                          compute_pos_neg_embeddings, forward, last_alignment_scores)
+  AlignmentAwareInfoNCE    ref:702-742  (same constructor / forward signature)
+
+`train_epoch` (ref:1026-1162) runs unmodified on top of these: its
+compute_pos_neg_embeddings -> (aud*txt).sum(1) -> loss_fn -> loss.backward() ->
+clip_grad_norm_ -> optimizer.step() sequence works because the whole model forward
+is ONE autograd node whose backward is the HIP schedule of engine.py and which
+leaves the parameter gradients in `param.grad` (views of the flat gradient buffer).
+"""
+from __future__ import annotations
+
+import logging
+
+import torch
+from torch import nn
+
+from . import ops
+from .engine import Engine
+from .modules import (AttentivePooling, AudioConfig, AudioEncoder, CrossModalAttention, EnhancedProjection,
+                      TextConfig, TextEncoder, WordLevelAlignmentModule)
+from .store import ParamStore
+
+logger = logging.getLogger(__name__)
+
+# encoder names the reference passes to AutoModel.from_pretrained -> architecture configs
+_TEXT_CONFIGS = {
+    "sentence-transformers/paraphrase-multilingual-mpnet-base-v2": TextConfig(),
+    "xlm-roberta-base": TextConfig(),
+}
+_AUDIO_CONFIGS = {"facebook/w2v-bert-2.0": AudioConfig()}
+
+
+def _resolve(name_or_cfg, table, default_cls):
+    if isinstance(name_or_cfg, (TextConfig, AudioConfig)):
+        return name_or_cfg
+    if name_or_cfg in table:
+        return table[name_or_cfg]
+    logger.warning("unknown encoder name %r: using the default %s architecture (random init, no download)",
+                   name_or_cfg, default_cls.__name__)
+    return default_cls()
+
+
+class EnhancedAudioTextModel(nn.Module):
+    """ref:315-697.  Encoders are built from architecture configs (there is no
+    network: weights are random-initialised or loaded with load_state_dict)."""
+
+    def __init__(self, text_model_name="sentence-transformers/paraphrase-multilingual-mpnet-base-v2",
+                 audio_model_name="facebook/w2v-bert-2.0", projection_dim=768, text_embedding_dim=768,
+                 audio_embedding_dim=1024, dropout=0.1, use_cross_modal=True, use_attentive_pooling=True,
+                 use_word_alignment=False, freeze_encoders="partial", text_layers_to_unfreeze=5,
+                 audio_layers_to_unfreeze=5, device="cuda", spec_augment=False):
+        super().__init__()
+        if not use_attentive_pooling:
+            raise NotImplementedError("use_attentive_pooling=False (CLS / mean pooling) is not built yet")
+        self.text_cfg = _resolve(text_model_name, _TEXT_CONFIGS, TextConfig)
+        self.audio_cfg = _resolve(audio_model_name, _AUDIO_CONFIGS, AudioConfig)
+        with torch.device("meta"):  # no host-side weights: values are initialised in the HBM store
+            self._build(projection_dim, text_embedding_dim, audio_embedding_dim, dropout, use_cross_modal,
+                        use_attentive_pooling, use_word_alignment, freeze_encoders, text_layers_to_unfreeze,
+                        audio_layers_to_unfreeze, spec_augment)
+        has_grad = {n for n, p in self.named_parameters() if p.requires_grad}
+        has_grad -= {n for n in has_grad if n.startswith("text_encoder.pooler.")}
+        if not spec_augment:
+            has_grad.discard("audio_encoder.masked_spec_embed")
+        self.store = ParamStore(self, device, has_grad)
+        self._init_params()
+        self.store.sync_shadow(force=True)
+        self.engine = Engine(self)
+        self.last_alignment_scores = None
+        trainable = sum(p.numel() for p in self.parameters() if p.requires_grad)
+        total = sum(p.numel() for p in self.parameters())
+        logger.info("Model initialized with %s trainable parameters out of %s total", f"{trainable:,}",
+                    f"{total:,}")
+
+    def _build(self, projection_dim, text_embedding_dim, audio_embedding_dim, dropout, use_cross_modal,
+               use_attentive_pooling, use_word_alignment, freeze_encoders, text_layers_to_unfreeze,
+               audio_layers_to_unfreeze, spec_augment):
+        self.text_encoder = TextEncoder(self.text_cfg)
+        self.audio_encoder = AudioEncoder(self.audio_cfg)
+        self.text_hidden_dim = self.text_cfg.hidden_size
+        self.audio_hidden_dim = self.audio_cfg.hidden_size
+        self.projection_dim = projection_dim
+        self.use_cross_modal = use_cross_modal
+        self.use_attentive_pooling = use_attentive_pooling
+        self.use_word_alignment = use_word_alignment
+        self.dropout = dropout
+        self.xattn_heads = 8
+        self.spec_augment = spec_augment
+        self._apply_freezing(freeze_encoders, text_layers_to_unfreeze, audio_layers_to_unfreeze)
+        self.text_projection = EnhancedProjection(text_embedding_dim, projection_dim, dropout=dropout)
+        self.audio_projection = EnhancedProjection(audio_embedding_dim, projection_dim, dropout=dropout)
+        if use_cross_modal:
+            self.text_seq_to_projection = nn.Linear(self.text_hidden_dim, projection_dim)
+            self.audio_seq_to_projection = nn.Linear(self.audio_hidden_dim, projection_dim)
+            self.text_to_audio_attention = CrossModalAttention(projection_dim, dropout=dropout)
+            self.audio_to_text_attention = CrossModalAttention(projection_dim, dropout=dropout)
+            self.text_fusion = nn.Sequential(nn.Linear(2 * projection_dim, projection_dim),
+                                             nn.LayerNorm(projection_dim))
+            self.audio_fusion = nn.Sequential(nn.Linear(2 * projection_dim, projection_dim),
+                                              nn.LayerNorm(projection_dim))
+        self.text_pooling = AttentivePooling(text_embedding_dim)
+        self.audio_pooling = AttentivePooling(audio_embedding_dim)
+        if use_word_alignment:
+            self.word_level_alignment = WordLevelAlignmentModule(self.text_hidden_dim, self.audio_hidden_dim,
+                                                                 projection_dim, dropout=dropout)
+
+    # ref:355-434
+    def _apply_freezing(self, mode, k_text, k_audio):
+        if mode == "full" or mode is True:
+            for p in list(self.text_encoder.parameters()) + list(self.audio_encoder.parameters()):
+                p.requires_grad = False
+        elif mode == "partial":
+            layers = self.text_encoder.encoder.layer
+            for i, layer in enumerate(layers):
+                if i < len(layers) - k_text:
+                    for p in layer.parameters():
+                        p.requires_grad = False
+            for p in self.text_encoder.pooler.parameters():
+                p.requires_grad = True
+            layers = self.audio_encoder.encoder.layers
+            for i, layer in enumerate(layers):
+                if i < len(layers) - k_audio:
+                    for p in layer.parameters():
+                        p.requires_grad = False
+            for p in self.audio_encoder.feature_projection.parameters():
+                p.requires_grad = True
+
+    def _init_params(self, seed: int = 0):
+        """Random init (no checkpoint download is possible): encoders N(0, 0.02) like the HF
+        initializers, LayerNorms 1/0, heads like torch's nn.Linear defaults (xavier for the
+        cross-modal attention projections, ref:121-124)."""
+        if self.store.device.type == "meta":
+            return
+        g = torch.Generator(device=self.store.device).manual_seed(seed)
+        with torch.no_grad():
+            for n, p in self.named_parameters():
+                leaf = n.rsplit(".", 1)[-1]
+                is_norm = ("norm" in n.lower() or "LayerNorm" in n) and leaf in ("weight", "bias")
+                if is_norm:
+                    p.fill_(1.0 if leaf == "weight" else 0.0)
+                elif n.startswith(("text_encoder", "audio_encoder")):
+                    if leaf == "bias":
+                        p.zero_()
+                    elif n.endswith("masked_spec_embed"):
+                        p.uniform_(0.0, 1.0, generator=g)
+                    else:
+                        p.normal_(0.0, 0.02, generator=g)
+                elif leaf in ("in_proj_bias",) or (leaf == "bias" and "_attention" in n):
+                    p.zero_() if leaf == "in_proj_bias" else p.uniform_(-p.shape[0] ** -0.5, p.shape[0] ** -0.5,
+                                                                         generator=g)
+                else:
+                    fan_in = p.shape[-1] if p.dim() > 1 else p.shape[0]
+                    fan_out = p.shape[0]
+                    if "_attention." in n and leaf == "weight" or leaf == "in_proj_weight":
+                        a = (6.0 / (fan_in + fan_out)) ** 0.5
+                    else:
+                        a = fan_in ** -0.5
+                    p.uniform_(-a, a, generator=g)
+
+    # ---------------------------------------------------------------- API
+    @staticmethod
+    def compute_pos_neg_embeddings(model, batch):
+        """ref:502-565: returns L2-normalised (txt_pos, txt_neg, aud) [B, P]; sets
+        model.last_alignment_scores when use_word_alignment."""
+        return model._embed(batch)
+
+    def forward(self, batch):
+        if "input_ids_pos" not in batch or "input_ids_neg" not in batch:
+            raise ValueError("Batch must contain 'input_ids_pos' and 'input_ids_neg'. "
+                             "Got keys: {}".format(list(batch.keys())))
+        return EnhancedAudioTextModel.compute_pos_neg_embeddings(self, batch)
+
+    def _embed(self, batch):
+        for k in ("input_ids_pos", "attention_mask_pos", "input_ids_neg", "attention_mask_neg", "input_values",
+                  "attention_mask_audio"):
+            if batch[k].device.type != "cuda":
+                raise RuntimeError(f"batch[{k!r}] must be on the GPU (libste.so has no CPU path)")
+        self.store.sync_shadow()
+        dummy = self.store.master[:1]
+        outs = _ModelFn.apply(self, batch, dummy.detach().requires_grad_(torch.is_grad_enabled()))
+        tpn, tnn, an = outs[:3]
+        self.last_alignment_scores = outs[3] if self.use_word_alignment else None
+        return tpn, tnn, an
+
+    # the sub-steps of the reference API, forward-only (inference utilities)
+    @torch.no_grad()
+    def encode_text(self, input_ids, attention_mask=None):
+        """ref:567-585 (forward only): (projection [B,P], last_hidden_state [B,L,H])."""
+        e = self.engine
+        ctx = {}
+        if attention_mask is None:
+            attention_mask = torch.ones_like(input_ids)
+        h, hb = e.text_forward(input_ids.contiguous(), attention_mask.contiguous(), False, 0, ctx)
+        sv = {}
+        B, L = input_ids.shape
+        _, pb = e._pool_fwd("text_pooling", hb, ctx["t_mask32"], B, L, sv)
+        proj = e._proj_fwd("text_projection", pb, B, False, 0, {})
+        return proj, h.view(B, L, -1)
+
+    @torch.no_grad()
+    def encode_audio(self, input_values, attention_mask=None):
+        """ref:587-641 (forward only): (projection [B,P], last_hidden_state [B,T,H])."""
+        e = self.engine
+        ctx = {}
+        B, T, _ = input_values.shape
+        if attention_mask is None:
+            attention_mask = torch.ones(B, T, dtype=torch.int64, device=input_values.device)
+        h, hb = e.audio_forward(input_values.contiguous(), attention_mask.contiguous(), False, 0, ctx)
+        _, pb = e._pool_fwd("audio_pooling", hb, ctx["a_mask32"], B, T, {})
+        proj = e._proj_fwd("audio_projection", pb, B, False, 0, {})
+        return proj, h.view(B, T, -1)
+
+
+class _ModelFn(torch.autograd.Function):
+    """The whole model forward as one autograd node (backward = engine.backward)."""
+
+    @staticmethod
+    def forward(fctx, model, batch, dummy):
+        tf_p, tf_n, af, align, ctx = model.engine.forward(batch, model.training)
+        tpn, tnn, an = (torch.empty_like(t) for t in (tf_p, tf_n, af))
+        norms = [torch.empty(t.shape[0], device=t.device) for t in (tf_p, tf_n, af)]
+        for x, y, nrm in zip((tf_p, tf_n, af), (tpn, tnn, an), norms):
+            ops.l2norm_fwd(x.contiguous(), y, nrm)
+        fctx.model, fctx.ctx = model, ctx
+        fctx.saved = (tpn, tnn, an, norms)
+        outs = (tpn, tnn, an)
+        if align is not None:
+            outs = outs + (align,)
+        else:
+            outs = outs + (torch.zeros(0, device=tpn.device),)
+        return outs
+
+    @staticmethod
+    def backward(fctx, d_tpn, d_tnn, d_an, d_align):
+        model = fctx.model
+        tpn, tnn, an, norms = fctx.saved
+        grads = []
+        for y, nrm, dy in zip((tpn, tnn, an), norms, (d_tpn, d_tnn, d_an)):
+            if dy is None:
+                dy = torch.zeros_like(y)
+            dx = torch.empty_like(y)
+            ops.l2norm_bwd(y, nrm, dy.contiguous(), dx)
+            grads.append(dx)
+        model.store.attach_grads()
+        if d_align is not None and d_align.numel() == 0:
+            d_align = None
+        model.engine.backward(fctx.ctx, grads[0], grads[1], grads[2],
+                              None if d_align is None else d_align.contiguous())
+        fctx.ctx = None
+        return None, None, None
+
+
+class AlignmentAwareInfoNCE(nn.Module):
+    """ref:702-742 — 2-way CE over [s_pos, s_neg]/τ, alignment weighting, corrupt penalty."""
+
+    def __init__(self, temperature=0.1, alignment_weight=0.3, corrupt_gamma=0.35):
+        super().__init__()
+        self.temperature = temperature
+        self.alignment_weight = alignment_weight
+        self.corrupt_gamma = corrupt_gamma
+
+    def forward(self, s_pos, s_neg, alignment_scores=None):
+        return _LossFn.apply(s_pos, s_neg, alignment_scores, self)
+
+
+class _LossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(fctx, s_pos, s_neg, align, mod):
+        B = s_pos.shape[0]
+        S = torch.stack([s_pos, s_neg], 1).contiguous()  # [B, 2]: diag of S[:, :1] trick -> use ldS=2
+        # pair_loss reads s_pos at S[i*ldS + i] and s_neg at S[i*ldS + off + i]; with ldS=1, off=B
+        flat = torch.cat([s_pos, s_neg]).contiguous().view(1, 2 * B)
+        sp = torch.empty(B, device=s_pos.device)
+        sn = torch.empty(B, device=s_pos.device)
+        loss = torch.empty(1, device=s_pos.device)
+        L = align.shape[1] if align is not None else 0
+        al = align.contiguous().float() if align is not None else None
+        _pair_loss_1d(flat, B, al, L, mod, sp, sn, loss)
+        fctx.save_for_backward(sp, sn, al if al is not None else torch.empty(0, device=s_pos.device))
+        fctx.mod, fctx.has_align, fctx.L = mod, align is not None, L
+        del S
+        return loss[0]
+
+    @staticmethod
+    def backward(fctx, dloss):
+        sp, sn, al = fctx.saved_tensors
+        mod = fctx.mod
+        B = sp.shape[0]
+        dsp, dsn = torch.empty_like(sp), torch.empty_like(sn)
+        dal = torch.empty(B, fctx.L, device=sp.device) if fctx.has_align else None
+        gs = dloss.reshape(1).float().contiguous()
+        ops.pair_loss_bwd(sp, sn, al if fctx.has_align else None, B, fctx.L, mod.temperature, mod.alignment_weight,
+                          mod.corrupt_gamma, gs, dsp, dsn, dal)
+        return dsp, dsn, dal, None
+
+
+def _pair_loss_1d(flat, B, al, L, mod, sp, sn, loss):
+    # ste_pair_loss_fwd indexes S[i*ldS + i] / S[i*ldS + off_neg + i]: with ldS = 0 that is flat[i] / flat[B + i]
+    from . import _lib
+    _lib.call("ste_pair_loss_fwd", flat.data_ptr(), 0, B, None if al is None else al.data_ptr(), B, L,
+              float(mod.temperature), float(mod.alignment_weight), float(mod.corrupt_gamma), sp.data_ptr(),
+              sn.data_ptr(), loss.data_ptr(), _lib.stream_ptr())

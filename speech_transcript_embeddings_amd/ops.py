@@ -221,8 +221,9 @@ def xattn1_fwd(q, k, v, mask, B, S, nh, probs, out, drop_p=0.0, seed=0):
 
 def xattn1_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, drop_p=0.0, seed=0):
     P = q.shape[-1]
+    assert _ld(dk) == _ld(dv)
     call("ste_xattn1_bwd", ptr(q), ptr(k), ptr(v), _ld(k), ptr(probs), ptr(dout), B, S, P, nh,
-         float((P // nh) ** -0.5), float(drop_p), int(seed) & (2**64 - 1), ptr(dq), ptr(dk), ptr(dv), _s())
+         float((P // nh) ** -0.5), float(drop_p), int(seed) & (2**64 - 1), ptr(dq), ptr(dk), ptr(dv), _ld(dk), _s())
 
 
 def l2norm_fwd(x, y, norms):

@@ -1,0 +1,192 @@
+r"""Flat parameter storage in HBM.
+
+Every parameter of the model tree becomes a view into ONE fp32 master buffer;
+trainable parameters that receive gradients come first, so their gradients,
+Adam moments and the fused optimizer work on contiguous ranges:
+
+  [ encoder params with grad | head params with grad | trainable-without-grad | frozen ]
+    \_____ grad / exp_avg / exp_avg_sq cover this prefix ____/
+
+The encoder / head split mirrors the reference's two AdamW param groups
+(ref:training/trainer_unfreeze.py:1496-1511: names containing 'text_encoder' or
+'audio_encoder' get lr/50).  Parameters the reference never gives a gradient
+(text pooler, masked_spec_embed without SpecAugment: grad None -> AdamW skips them)
+sit in the third segment.
+
+A bf16 shadow with the same offsets holds the MFMA operands.  The fused optimizer
+refreshes it for updated ranges; anything else that writes parameters (load_state_dict,
+a torch optimizer) bumps the tensor version counter and the shadow is re-cast lazily.
+
+Fused groups (q/k/v weights and biases, key/value of the cross-modal attentions) are
+laid out adjacently so one GEMM serves them and one dW GEMM writes their gradients.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import ops
+
+ALIGN = 8  # elements: 32 B for fp32, 16 B for the bf16 shadow
+
+
+def _fuse_groups(names):
+    """Return name -> tuple(group) for parameters that must be adjacent."""
+    groups = {}
+    sets = [("attention.self.query", "attention.self.key", "attention.self.value"),
+            ("self_attn.linear_q", "self_attn.linear_k", "self_attn.linear_v"),
+            ("_attention.key", "_attention.value")]
+    nameset = set(names)
+    for n in names:
+        for trio in sets:
+            for leaf in ("weight", "bias"):
+                head = trio[0] + "." + leaf
+                if n.endswith(head):
+                    prefix = n[: -len(head)]
+                    grp = tuple(prefix + t + "." + leaf for t in trio)
+                    if all(g in nameset for g in grp):
+                        for g in grp:
+                            groups[g] = grp
+    return groups
+
+
+@dataclass
+class Slot:
+    name: str
+    offset: int
+    numel: int
+    shape: tuple
+    segment: str
+
+
+class ParamStore:
+    def __init__(self, model: torch.nn.Module, device, has_grad: set[str]):
+        named = list(model.named_parameters())
+        names = [n for n, _ in named]
+        params = dict(named)
+        groups = _fuse_groups(names)
+
+        def seg_of(n, p):
+            if not p.requires_grad:
+                return "frozen"
+            if n not in has_grad:
+                return "nograd"
+            return "enc" if ("text_encoder" in n or "audio_encoder" in n) else "head"
+
+        order = {"enc": [], "head": [], "nograd": [], "frozen": []}
+        seen = set()
+        for n, p in named:
+            if n in seen:
+                continue
+            grp = groups.get(n, (n,))
+            segs = {seg_of(g, params[g]) for g in grp}
+            if len(segs) != 1:
+                grp = (n,)
+            for g in grp:
+                order[seg_of(g, params[g])].append(g)
+                seen.add(g)
+        self.slots: dict[str, Slot] = {}
+        off = 0
+        self.seg_range = {}
+        for seg in ("enc", "head", "nograd", "frozen"):
+            start = off
+            for n in order[seg]:
+                p = params[n]
+                grp = groups.get(n)
+                if grp is None or n == grp[0]:
+                    off = (off + ALIGN - 1) // ALIGN * ALIGN
+                self.slots[n] = Slot(n, off, p.numel(), tuple(p.shape), seg)
+                off += p.numel()
+            off = (off + ALIGN - 1) // ALIGN * ALIGN
+            self.seg_range[seg] = (start, off)
+        self.numel = off
+        self.n_grad = self.seg_range["head"][1]
+        self.device = torch.device(device)
+        self.master = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
+        self.shadow = torch.zeros(self.numel, device=self.device, dtype=torch.bfloat16)
+        self.grad = torch.zeros(self.n_grad, device=self.device, dtype=torch.float32)
+        # re-seat every parameter as a view of the flat buffer (module trees may be built on
+        # the meta device: values are initialised afterwards, directly in HBM)
+        for n, s in self.slots.items():
+            p = params[n]
+            view = self.master[s.offset:s.offset + s.numel].view(s.shape)
+            if p.device.type != "meta":
+                with torch.no_grad():
+                    view.copy_(p.detach().to(self.device, torch.float32))
+            owner, leaf = (model.get_submodule(n.rsplit(".", 1)[0]), n.rsplit(".", 1)[1]) if "." in n \
+                else (model, n)
+            newp = torch.nn.Parameter(view, requires_grad=p.requires_grad)
+            owner._parameters[leaf] = newp
+            params[n] = newp
+        self.params = params
+        self._versions = {}
+        self.sync_shadow(force=True)
+
+    # ------------------------------------------------------------------ views
+    def p(self, name):
+        s = self.slots[name]
+        return self.master[s.offset:s.offset + s.numel].view(s.shape)
+
+    def w(self, name, rows=None):
+        """bf16 shadow as a 2-D [out, in] matrix (conv weights [out,in,1] flattened)."""
+        s = self.slots[name]
+        v = self.shadow[s.offset:s.offset + s.numel]
+        return v.view(s.shape[0], -1) if rows is None else v.view(rows, -1)
+
+    def g(self, name):
+        s = self.slots[name]
+        if s.segment not in ("enc", "head"):
+            return None
+        return self.grad[s.offset:s.offset + s.numel].view(s.shape)
+
+    def fused(self, first: str, count: int, which: str):
+        """Adjacent group starting at `first` as one tensor: which in {'w','p','g'}."""
+        s = self.slots[first]
+        n = s.numel * count
+        if which == "w":
+            return self.shadow[s.offset:s.offset + n].view(s.shape[0] * count, -1)
+        if which == "p":
+            base = self.master[s.offset:s.offset + n]
+            return base.view(s.shape[0] * count, *s.shape[1:]) if len(s.shape) > 1 else base
+        if s.segment not in ("enc", "head"):
+            return None
+        base = self.grad[s.offset:s.offset + n]
+        return base.view(s.shape[0] * count, *s.shape[1:]) if len(s.shape) > 1 else base
+
+    def trainable_layer(self, name: str) -> bool:
+        return self.slots[name].segment in ("enc", "head")
+
+    # ----------------------------------------------------------------- shadow
+    def sync_shadow(self, force=False):
+        """Re-cast the bf16 shadow of any parameter modified outside the fused optimizer."""
+        if self.device.type != "cuda":
+            return  # meta / cpu stores only serve module-tree inspection; no kernel can run there
+        for n, s in self.slots.items():
+            v = self.params[n]._version
+            if force or self._versions.get(n) != v:
+                src = self.master[s.offset:s.offset + s.numel]
+                dst = self.shadow[s.offset:s.offset + s.numel]
+                ops.cast_bf16(src, dst)
+                self._versions[n] = self.params[n]._version
+
+    def mark_synced(self):
+        for n in self.slots:
+            self._versions[n] = self.params[n]._version
+
+    # ------------------------------------------------------------------ grads
+    def attach_grads(self):
+        """Point .grad of every gradient-receiving parameter at its slice of the flat buffer.
+        Returns True if the buffer must be zeroed first (grads were reset to None)."""
+        reset = False
+        for n, s in self.slots.items():
+            if s.segment in ("enc", "head"):
+                p = self.params[n]
+                if p.grad is None:
+                    reset = True
+        if reset:
+            self.grad.zero_()
+            for n, s in self.slots.items():
+                if s.segment in ("enc", "head"):
+                    self.params[n].grad = self.grad[s.offset:s.offset + s.numel].view(s.shape)
+        return reset

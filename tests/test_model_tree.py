@@ -1,0 +1,57 @@
+"""CPU checks of the drop-in boundary: the model's module tree, state_dict keys, shapes,
+freezing rules and optimizer grouping equal the reference's (param_counts.json was
+produced from the real reference model by tests/golden/make_golden.py)."""
+import json
+
+import pytest
+
+from conftest import GOLDEN
+
+
+@pytest.fixture(scope="module")
+def counts():
+    return json.loads((GOLDEN / "param_counts.json").read_text())
+
+
+@pytest.mark.parametrize("key,align,k", [("align=False,k=3", False, 3), ("align=True,k=3", True, 3),
+                                         ("align=True,k=5", True, 5)])
+def test_full_size_tree_matches_reference(counts, key, align, k):
+    from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
+    ref = counts[key]
+    m = EnhancedAudioTextModel(use_word_alignment=align, text_layers_to_unfreeze=k, audio_layers_to_unfreeze=k,
+                               device="meta")
+    shapes = {n: list(p.shape) for n, p in m.named_parameters()}
+    assert list(shapes) == list(ref["shapes"])
+    assert shapes == ref["shapes"]
+    assert sum(p.numel() for p in m.parameters()) == ref["total"]
+    tr = [n for n, p in m.named_parameters() if p.requires_grad]
+    assert sorted(tr) == sorted(ref["trainable_names"])
+    assert sum(p.numel() for p in m.parameters() if p.requires_grad) == ref["trainable"]
+    # flat store: gradient-receiving params first, encoder group then head group (ref:1496-1511)
+    st = m.store
+    enc = [n for n, s in st.slots.items() if s.segment == "enc"]
+    head = [n for n, s in st.slots.items() if s.segment == "head"]
+    assert all("text_encoder" in n or "audio_encoder" in n for n in enc)
+    assert not any("text_encoder" in n or "audio_encoder" in n for n in head)
+    nograd = {n for n, s in st.slots.items() if s.segment == "nograd"}
+    assert nograd == {"text_encoder.pooler.dense.weight", "text_encoder.pooler.dense.bias",
+                      "audio_encoder.masked_spec_embed"}
+    # fused q/k/v adjacency
+    for i in range(24):
+        pre = f"audio_encoder.encoder.layers.{i}.self_attn."
+        o = [st.slots[pre + f"linear_{c}.weight"].offset for c in "qkv"]
+        assert o[1] - o[0] == o[2] - o[1] == 1024 * 1024
+
+
+def test_forward_requires_gpu_tensors():
+    """No CPU fallback: the product path refuses host tensors."""
+    import torch
+    from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
+    m = EnhancedAudioTextModel(device="meta")
+    batch = {k: torch.zeros(1, 4, dtype=torch.long) for k in
+             ("input_ids_pos", "attention_mask_pos", "input_ids_neg", "attention_mask_neg", "attention_mask_audio")}
+    batch["input_values"] = torch.zeros(1, 4, 160)
+    with pytest.raises(RuntimeError):
+        EnhancedAudioTextModel.compute_pos_neg_embeddings(m, batch)
+    with pytest.raises(ValueError):
+        m({"input_values": batch["input_values"]})
