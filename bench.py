@@ -1,0 +1,192 @@
+#!/usr/bin/env python
+"""Throughput benchmark of the MI355X contrastive training step (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1] per GPU): synthetic 10 s @ 16 kHz clips + 64-token clean
+and corrupted transcripts, local batch 64 per GPU (weak scaling: global 64·N), w2v-bert-2.0
+Conformer + XLM-R-base text encoder with 3+3 unfrozen layers, bf16 MFMA / fp32 master weights.
+One timed step = GPU fbank from raw waveforms -> forward -> AlignmentAwareInfoNCE -> backward
+-> RCCL gradient all-reduce (N>1) -> clip_grad_norm_ + AdamW.  Training semantics with
+dropout on, layerdrop 0 and SpecAugment off, random-init weights.
+
+Rank 0 prints one JSON line.  `roofline` is for the dominant kernel (the bf16 GEMM
+instantiation with the largest share of step time), timed per launch with HIP events on the
+launch stream during the timed steps; `cpu_baseline` times the oracle (CPU fp32 restatement of
+the same step, oracle/) on the host at N=1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BF16_PEAK_TFLOPS = 2516.6          # MI355X dense bf16 MFMA (256 CU x 4096 FLOP/clk x 2.4 GHz)
+GFLOP_PER_PAIR = {3: 1370.4, 5: 1429.5}   # SURVEY §8(d) algorithmic fwd+bwd FLOPs per pair (c2/c3, c4)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="local (per-GPU) batch")
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--tokens", type=int, default=64)
+    ap.add_argument("--unfreeze", type=int, default=3)
+    ap.add_argument("--align", action="store_true", help="config 4: word-alignment head")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=1)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """Oracle (CPU fp32 restatement of the step, pinned to the reference) on a bounded sample."""
+    from oracle import fbank_ref, ref_model as R
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    cfg = R.ModelCfg(use_word_alignment=args.align, text_layers_to_unfreeze=args.unfreeze,
+                     audio_layers_to_unfreeze=args.unfreeze)
+    shapes = R.param_shapes(cfg, spec_augment=False)
+    trainable = R.trainable_names([n for n, _ in shapes], cfg)
+    g = torch.Generator().manual_seed(0)
+    p = {}
+    for n, s in shapes:
+        t = torch.randn(s, generator=g) * 0.02
+        if n.endswith(".weight") and ("norm" in n.lower() or "LayerNorm" in n):
+            t = torch.ones(s)
+        p[n] = t.requires_grad_(n in trainable and not n.startswith("text_encoder.pooler"))
+    B, N, L = args.cpu_batch, int(args.seconds * 16000), args.tokens
+    m = {n: torch.zeros_like(t) for n, t in p.items() if t.requires_grad}
+    v = {n: torch.zeros_like(t) for n, t in p.items() if t.requires_grad}
+
+    def one_step(step):
+        feats = [fbank_ref.extract(fbank_ref.synth_wave(1000 + i, N))[0] for i in range(B)]
+        f, am = fbank_ref.collate(feats)
+        ids = torch.randint(5, 250000, (B, L))
+        ids[:, 0], ids[:, -1] = 0, 2
+        neg = ids.clone()
+        neg[:, 1:L // 5] = torch.randint(5, 250000, (B, L // 5 - 1))
+        mask = torch.ones(B, L, dtype=torch.long)
+        batch = {"input_ids_pos": ids, "attention_mask_pos": mask, "input_ids_neg": neg, "attention_mask_neg": mask,
+                 "input_values": torch.from_numpy(f), "attention_mask_audio": torch.from_numpy(am)}
+        loss, *_ = R.step_loss(p, batch, cfg)
+        loss.backward()
+        with torch.no_grad():
+            gs = [t.grad for t in p.values() if t.grad is not None]
+            tot = torch.sqrt(sum((x.double() ** 2).sum() for x in gs)).item()
+            coef = min(1.0, 1.0 / (tot + 1e-6))
+            for n, t in p.items():
+                if t.grad is None:
+                    continue
+                lr = 2.1e-3 / 50 if ("text_encoder" in n or "audio_encoder" in n) else 2.1e-3
+                t2, m[n], v[n] = R.adamw_step(t, t.grad * coef, m[n], v[n], lr=lr, step=step)
+                t.copy_(t2)
+                t.grad = None
+
+    one_step(1)
+    t0 = time.perf_counter()
+    for s in range(args.cpu_steps):
+        one_step(2 + s)
+    dt = (time.perf_counter() - t0) / args.cpu_steps
+    return {"value": round(B / dt, 4), "unit": "audio-text pairs/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ (CPU fp32 torch restatement pinned to the reference) full train step incl. numpy "
+                      f"fbank + AdamW, {args.seconds:g} s clips + {L}-token transcripts, {args.unfreeze} unfrozen "
+                      f"layers, batch {B}, {args.cpu_steps} timed steps after 1 warmup, {dt:.2f} s/step"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from speech_transcript_embeddings_amd import ops
+    from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
+    from speech_transcript_embeddings_amd.train import TrainStep, synthetic_batch
+
+    model = EnhancedAudioTextModel(use_word_alignment=args.align, text_layers_to_unfreeze=args.unfreeze,
+                                   audio_layers_to_unfreeze=args.unfreeze, device=f"cuda:{local}")
+    model.audio_cfg.layerdrop = 0.0
+    step = TrainStep(model, warmup=100, total_steps=100000)
+    B, nsamp, L = args.batch, int(args.seconds * 16000), args.tokens
+    data = synthetic_batch(B, nsamp, L, device=f"cuda:{local}", rank=rank)
+
+    for _ in range(args.warmup):
+        step(*data)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ops.GEMM_TRACE = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(*data)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    trace, ops.GEMM_TRACE = ops.GEMM_TRACE, None
+    loss = float(step.last["loss"].item())
+    if world > 1:
+        t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # dominant-kernel roofline from per-launch HIP event timings of the timed steps
+    agg = {}
+    for name, flops, e0, e1 in trace:
+        a = agg.setdefault(name, [0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += flops
+        a[2] += e0.elapsed_time(e1) * 1e-3
+    dom = max(agg, key=lambda k: agg[k][2])
+    n_l, fl, tm = agg[dom]
+    achieved = fl / tm / 1e12
+    gemm_time = sum(a[2] for a in agg.values()) / args.steps
+    pairs = world * B * args.steps / elapsed
+    gflop = GFLOP_PER_PAIR.get(args.unfreeze, 1370.4)
+    out = {
+        "metric": "audio–text pairs/sec (whole node), 10s@16kHz + 64-tok, 1/2/4/8 MI355X",
+        "value": round(pairs, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (SURVEY §8d waveforms + token ids), random-init weights",
+        "config": {"workload": f"c2 per GPU: {B} pairs x ({args.seconds:g}s@16kHz audio + {L}-tok clean + {L}-tok "
+                               f"corrupt), w2v-bert-2.0 Conformer 24L + XLM-R-base 12L, {args.unfreeze}+"
+                               f"{args.unfreeze} unfrozen{', alignment head' if args.align else ''}; GPU fbank -> "
+                               f"fwd -> InfoNCE -> bwd -> allreduce -> clip+AdamW",
+                   "global_batch": world * B, "local_batch": B, "seq_len_audio_frames": ((1 + (nsamp - 400) // 160) + 1) // 2,
+                   "seq_len_text": L, "parallelism": f"dp{world}"},
+        "step_roofline_frac": round(pairs * gflop / (world * BF16_PEAK_TFLOPS * 1e3), 4),
+        "roofline": {"bound": "mfma", "kernel": dom, "launches_per_step": n_l // args.steps,
+                     "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                     "avg_launch_us": round(tm / n_l * 1e6, 2), "algorithmic_gflop_per_launch": round(fl / n_l / 1e9, 3),
+                     "gemm_ms_per_step_all_variants": round(gemm_time * 1e3, 2)},
+        "loss": round(loss, 5),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

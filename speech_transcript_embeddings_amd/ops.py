@@ -69,8 +69,24 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
         args.row_scale = ptr(row_scale)
     args.alpha, args.beta, args.act = float(alpha), float(beta), int(act)
     args.drop_p, args.seed, args.drop_ld = float(drop_p), int(seed) & (2**64 - 1), int(drop_ld)
-    call("ste_gemm", C.byref(args), _s())
+    if GEMM_TRACE is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        call("ste_gemm", C.byref(args), _s())
+        ev1.record()
+        GEMM_TRACE.append((gemm_kernel_name(a_kc, b_kc), 2.0 * M * N * K * batch, ev0, ev1))
+    else:
+        call("ste_gemm", C.byref(args), _s())
     return out
+
+
+GEMM_TRACE = None  # list while bench.py measures per-launch GEMM durations with HIP events
+
+
+def gemm_kernel_name(a_kc, b_kc):
+    """The kernel symbol rocprofv3 reports for a GEMM launch (csrc/gemm.hip instantiation)."""
+    return f"gemm_bf16_kernel<{str(bool(a_kc)).lower()}, {str(bool(b_kc)).lower()}>"
 
 
 def linear(x, w, bias=None, **kw):

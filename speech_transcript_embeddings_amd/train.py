@@ -1,0 +1,197 @@
+"""The fused training step and its optimizer tail, single GPU or data-parallel.
+
+One step (the body of ref:training/trainer_unfreeze.py:train_epoch, ref:1057-1117, with
+accumulation_steps = 1):
+    GPU fbank from raw waveforms (replaces the 12 CPU DataLoader workers' extractor calls)
+ -> forward (engine.py)  -> L2-normalise -> B x 2B similarity on the fp32 MFMA
+ -> AlignmentAwareInfoNCE -> backward (engine.py)
+ -> [DP] RCCL all-reduce (average) of the flat fp32 gradient buffer, bucketed
+ -> clip_grad_norm_(1.0) + two-group AdamW + linear warmup schedule, fused in HBM.
+
+Data parallel: the loss is a mean of per-sample terms, so averaging
+per-rank gradients of equal local batches equals the global-batch gradient exactly;
+the only collectives are the gradient all-reduce and a small all-gather of the
+normalised embeddings (global similarity metrics; optional in-batch negatives).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.distributed as dist
+
+from . import _lib, ops
+from .model import EnhancedAudioTextModel
+
+F32 = torch.float32
+
+
+class LinearWarmupSchedule:
+    """transformers.get_linear_schedule_with_warmup (ref:1537-1541); lr(0) = 0."""
+
+    def __init__(self, warmup: int, total: int):
+        self.warmup, self.total, self.step_count = warmup, total, 0
+
+    def factor(self, step=None):
+        s = self.step_count if step is None else step
+        if s < self.warmup:
+            return s / max(1, self.warmup)
+        return max(0.0, (self.total - s) / max(1, self.total - self.warmup))
+
+    def step(self):
+        self.step_count += 1
+
+
+class FusedAdamW:
+    """torch.optim.AdamW over the two reference param groups (encoder lr/50, heads lr,
+    weight_decay 0.01, betas (0.9, 0.999), eps 1e-8; ref:1487-1511) with
+    clip_grad_norm_(max_norm) (ref:1108) folded in: one Σg² pass, then one AdamW pass per
+    group that reads the clip coefficient on device (no host sync)."""
+
+    def __init__(self, model: EnhancedAudioTextModel, lr=2.1e-3, encoder_lr_div=50.0, weight_decay=0.01,
+                 betas=(0.9, 0.999), eps=1e-8, max_norm=1.0):
+        st = model.store
+        self.store = st
+        self.groups = [{"range": st.seg_range["enc"], "lr": lr / encoder_lr_div},
+                       {"range": st.seg_range["head"], "lr": lr}]
+        self.wd, self.betas, self.eps, self.max_norm = weight_decay, betas, eps, max_norm
+        self.exp_avg = torch.zeros(st.n_grad, device=st.device, dtype=F32)
+        self.exp_avg_sq = torch.zeros(st.n_grad, device=st.device, dtype=F32)
+        self.sumsq = torch.zeros(1, device=st.device, dtype=torch.float64)
+        self.t = 0
+
+    def step(self, lr_factor: float = 1.0):
+        st = self.store
+        self.t += 1
+        self.sumsq.zero_()
+        if self.max_norm is not None:
+            ops.sumsq(st.grad[: st.n_grad], self.sumsq)
+        for gr in self.groups:
+            a, b = gr["range"]
+            if b <= a:
+                continue
+            ops.adamw(st.master[a:b], st.grad[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b], st.shadow[a:b],
+                      lr=gr["lr"] * lr_factor, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps, wd=self.wd,
+                      step=self.t, sumsq_acc=self.sumsq if self.max_norm is not None else None,
+                      max_norm=self.max_norm or 1.0)
+        st.mark_synced()
+
+    def zero_grad(self):
+        self.store.grad.zero_()
+
+
+class GradAllReduce:
+    """Average the flat fp32 gradient buffer across ranks in fixed-size buckets (RCCL
+    ring over xGMI; buckets issued back-to-back so the rings pipeline)."""
+
+    def __init__(self, store, bucket_mb: int = 256):
+        self.store = store
+        self.bucket = max(1, bucket_mb * 1024 * 1024 // 4)
+
+    def __call__(self):
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return
+        ws = dist.get_world_size()
+        g = self.store.grad[: self.store.n_grad]
+        g.div_(ws)
+        works = []
+        for a in range(0, g.numel(), self.bucket):
+            works.append(dist.all_reduce(g[a:a + self.bucket], op=dist.ReduceOp.SUM, async_op=True))
+        for w in works:
+            w.wait()
+
+
+class TrainStep:
+    """fbank -> forward -> loss -> backward -> all-reduce -> clip + AdamW (+ schedule)."""
+
+    def __init__(self, model: EnhancedAudioTextModel, lr=2.1e-3, warmup=100, total_steps=10000, temperature=0.1,
+                 alignment_weight=0.5, corrupt_gamma=0.35, max_norm=1.0, pad_value=1.0, gather_embeddings=True):
+        self.model = model
+        self.opt = FusedAdamW(model, lr=lr, max_norm=max_norm)
+        self.sched = LinearWarmupSchedule(warmup, total_steps)
+        self.allreduce = GradAllReduce(model.store)
+        self.tau, self.aw, self.gamma = temperature, alignment_weight, corrupt_gamma
+        self.pad_value = pad_value
+        self.gather_embeddings = gather_embeddings
+        self.last = {}
+
+    def features(self, wav, lengths):
+        """GPU fbank for a batch of raw 16 kHz waveforms -> (input_values, attention_mask_audio)."""
+        n = int(wav.shape[1])
+        T = ((1 + (n - 400) // 160) + 1) // 2
+        return ops.fbank(wav, lengths, T, pad_value=self.pad_value, mask_mode=0)
+
+    def __call__(self, wav, lengths, ids_pos, mask_pos, ids_neg, mask_neg):
+        m = self.model
+        m.train()
+        feats, amask = self.features(wav, lengths)
+        batch = {"input_ids_pos": ids_pos, "attention_mask_pos": mask_pos, "input_ids_neg": ids_neg,
+                 "attention_mask_neg": mask_neg, "input_values": feats, "attention_mask_audio": amask}
+        st = m.store
+        st.sync_shadow()
+        eng = m.engine
+        tf_p, tf_n, af, align, ctx = eng.forward(batch, True)
+        B, P = af.shape
+        # L2 normalise, similarity matrix S = A·[Tp;Tn]^T (fp32 MFMA), loss on its diagonals
+        e = lambda *s: torch.empty(s, device=st.device, dtype=F32)  # noqa: E731
+        tn_all = e(2 * B, P)
+        an = e(B, P)
+        nrm = e(3 * B)
+        ops.l2norm_fwd(tf_p, tn_all[:B], nrm[:B])
+        ops.l2norm_fwd(tf_n, tn_all[B:], nrm[B:2 * B])
+        ops.l2norm_fwd(af, an, nrm[2 * B:])
+        S = e(B, 2 * B)
+        ops.similarity(an, tn_all, S)
+        sp, sn, loss = e(B), e(B), e(1)
+        L = align.shape[1] if align is not None else 0
+        ops.pair_loss_fwd(S, B, align, B, L, self.tau, self.aw, self.gamma, sp, sn, loss)
+        if self.gather_embeddings and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            self._gather_metrics(an, tn_all)
+        # backward
+        dsp, dsn = e(B), e(B)
+        dal = e(B, L) if align is not None else None
+        ops.pair_loss_bwd(sp, sn, align, B, L, self.tau, self.aw, self.gamma, None, dsp, dsn, dal)
+        dan, dtp, dtn = e(B, P), e(B, P), e(B, P)
+        ops.pair_sim_bwd(an, tn_all[:B], tn_all[B:], dsp, dsn, dan, dtp, dtn)
+        g_tp, g_tn, g_a = e(B, P), e(B, P), e(B, P)
+        ops.l2norm_bwd(tn_all[:B], nrm[:B], dtp, g_tp)
+        ops.l2norm_bwd(tn_all[B:], nrm[B:2 * B], dtn, g_tn)
+        ops.l2norm_bwd(an, nrm[2 * B:], dan, g_a)
+        st.grad.zero_()
+        eng.backward(ctx, g_tp, g_tn, g_a, dal)
+        self.allreduce()
+        self.opt.step(self.sched.factor())  # reference order: optimizer.step() then scheduler.step()
+        self.sched.step()
+        self.last = {"loss": loss, "s_pos": sp, "s_neg": sn}
+        return loss
+
+    def _gather_metrics(self, an, tn_all):
+        ws = dist.get_world_size()
+        ga = [torch.empty_like(an) for _ in range(ws)]
+        dist.all_gather(ga, an)
+        gt = [torch.empty_like(tn_all) for _ in range(ws)]
+        dist.all_gather(gt, tn_all)
+        self.last["global_emb"] = (ga, gt)
+
+
+def synthetic_batch(B, n_samples, L, vocab=250000, device="cuda", seed=0, rank=0):
+    """SURVEY §8d synthetic inputs: 0.1·N(0,1) + 3 sinusoids waveforms, ids ~ U[5, vocab) with
+    BOS=0 / EOS=2, full masks, corrupted = 20% of positions re-drawn.  Built on the GPU."""
+    g = torch.Generator(device=device).manual_seed(seed * 1000 + rank)
+    t = torch.arange(n_samples, device=device, dtype=F32) / 16000.0
+    wav = 0.1 * torch.randn(B, n_samples, device=device, generator=g)
+    freqs = 100 + 2900 * torch.rand(B, 3, 1, device=device, generator=g)
+    wav = wav + 0.05 * torch.sin(2 * math.pi * freqs * t.view(1, 1, -1)).sum(1)
+    wav = wav.clamp_(-1, 1).contiguous()
+    lengths = torch.full((B,), n_samples, device=device, dtype=torch.int32)
+    ids = torch.randint(5, vocab, (B, L), device=device, generator=g)
+    ids[:, 0], ids[:, -1] = 0, 2
+    corrupt = torch.rand(B, L, device=device, generator=g) < 0.2
+    corrupt[:, 0] = False
+    corrupt[:, -1] = False
+    neg = torch.where(corrupt, torch.randint(5, vocab, (B, L), device=device, generator=g), ids)
+    mask = torch.ones(B, L, device=device, dtype=torch.int64)
+    return wav, lengths, ids, mask, neg.contiguous(), mask.clone()
+
+
+__all__ = ["TrainStep", "FusedAdamW", "LinearWarmupSchedule", "GradAllReduce", "synthetic_batch", "_lib"]
