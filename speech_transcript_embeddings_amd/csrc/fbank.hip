@@ -23,9 +23,67 @@ constexpr int MAXNZ = 640;  // non-zero filter taps (501 for these parameters)
 
 __device__ double hz_to_mel(double f) { return 1127.0 * log(1.0 + f / 700.0); }
 
+// Constant tables (built once per call by one block, read by every frame block):
+//   [0, 512)   twiddles e^{-2πik/512} (float2 x 256)     [512, 912)  povey window
+//   [912, 992) mel start bin  [992, 1072) mel length  [1072, 1152) mel offset (ints)
+//   [1152, 1152+MAXNZ) mel weights (kaldi scale, triangles in mel space, fp64 -> fp32)
+constexpr int T_TW = 0, T_WIN = 512, T_MSTART = 912, T_MLEN = 992, T_MOFF = 1072, T_MW = 1152;
+constexpr int TABLE_FLOATS = 2048;
+
+__global__ __launch_bounds__(256) void fbank_tables_kernel(float* __restrict__ tab) {
+  __shared__ double fk[NBIN];
+  __shared__ int slen[NMEL], soff[NMEL];
+  const int tid = threadIdx.x;
+  for (int k = tid; k < NFFT / 2; k += 256) {
+    double s, c;
+    sincos(-2.0 * M_PI * (double)k / (double)NFFT, &s, &c);
+    tab[T_TW + 2 * k] = (float)c;
+    tab[T_TW + 2 * k + 1] = (float)s;
+  }
+  for (int n = tid; n < FRAME; n += 256) {
+    const double hann = 0.5 - 0.5 * cos(2.0 * M_PI * (double)n / (double)(FRAME - 1));
+    tab[T_WIN + n] = (float)pow(hann, 0.85);
+  }
+  for (int k = tid; k < NBIN; k += 256) fk[k] = hz_to_mel(31.25 * k);
+  __syncthreads();
+  const double mel_lo = hz_to_mel(20.0), mel_hi = hz_to_mel(8000.0);
+  int start = 0, len = 0;
+  double f0 = 0, f1 = 0, f2 = 0;
+  if (tid < NMEL) {
+    f0 = mel_lo + (mel_hi - mel_lo) * tid / (NMEL + 1);
+    f1 = mel_lo + (mel_hi - mel_lo) * (tid + 1) / (NMEL + 1);
+    f2 = mel_lo + (mel_hi - mel_lo) * (tid + 2) / (NMEL + 1);
+    start = -1;
+    for (int k = 0; k < NBIN; ++k) {
+      const double wv = fmax(0.0, fmin((fk[k] - f0) / (f1 - f0), (f2 - fk[k]) / (f2 - f1)));
+      if (wv > 0.0) { if (start < 0) start = k; ++len; }
+    }
+    if (start < 0) start = 0;
+    slen[tid] = len;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int off = 0;
+    for (int m = 0; m < NMEL; ++m) { soff[m] = off; off += slen[m]; }
+  }
+  __syncthreads();
+  if (tid < NMEL) {
+    int* ti = reinterpret_cast<int*>(tab);
+    ti[T_MSTART + tid] = start;
+    ti[T_MLEN + tid] = len;
+    ti[T_MOFF + tid] = soff[tid];
+    for (int i = 0; i < len && soff[tid] + i < MAXNZ; ++i) {
+      const int k = start + i;
+      tab[T_MW + soff[tid] + i] = (float)fmax(0.0, fmin((fk[k] - f0) / (f1 - f0), (f2 - fk[k]) / (f2 - f1)));
+    }
+  }
+}
+
+constexpr int FRAMES_PER_WAVE = 4;
+
 __global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restrict__ wav, int64_t ld_wav,
                                                          const int32_t* __restrict__ lengths, int Fmax,
-                                                         float* __restrict__ work) {
+                                                         const float* __restrict__ tab, float* __restrict__ work) {
   __shared__ float2 sbuf[4][NFFT];
   __shared__ float2 stw[NFFT / 2];
   __shared__ float swin[FRAME];
@@ -35,45 +93,21 @@ __global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restri
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int b = blockIdx.y;
-  // ---- constant tables (per block; cheap next to the streaming work)
-  for (int k = tid; k < NFFT / 2; k += 256) {
-    double s, c;
-    sincos(-2.0 * M_PI * (double)k / (double)NFFT, &s, &c);
-    stw[k] = make_float2((float)c, (float)s);
+  for (int k = tid; k < NFFT / 2; k += 256) stw[k] = make_float2(tab[T_TW + 2 * k], tab[T_TW + 2 * k + 1]);
+  for (int n = tid; n < FRAME; n += 256) swin[n] = tab[T_WIN + n];
+  if (tid < NMEL) {
+    const int* ti = reinterpret_cast<const int*>(tab);
+    sm_start[tid] = ti[T_MSTART + tid];
+    sm_len[tid] = ti[T_MLEN + tid];
+    sm_off[tid] = ti[T_MOFF + tid];
   }
-  for (int n = tid; n < FRAME; n += 256) {
-    const double hann = 0.5 - 0.5 * cos(2.0 * M_PI * (double)n / (double)(FRAME - 1));
-    swin[n] = (float)pow(hann, 0.85);
-  }
-  if (tid == 0) {
-    const double mel_lo = hz_to_mel(20.0), mel_hi = hz_to_mel(8000.0);
-    int off = 0;
-    for (int m = 0; m < NMEL; ++m) {
-      const double f0 = mel_lo + (mel_hi - mel_lo) * m / (NMEL + 1);
-      const double f1 = mel_lo + (mel_hi - mel_lo) * (m + 1) / (NMEL + 1);
-      const double f2 = mel_lo + (mel_hi - mel_lo) * (m + 2) / (NMEL + 1);
-      int start = -1, len = 0;
-      for (int k = 0; k < NBIN; ++k) {
-        const double fk = hz_to_mel(31.25 * k);
-        const double down = (fk - f0) / (f1 - f0), up = (f2 - fk) / (f2 - f1);
-        const double wv = fmax(0.0, fmin(down, up));
-        if (wv > 0.0) {
-          if (start < 0) start = k;
-          if (off + len < MAXNZ) sm_w[off + len] = (float)wv;
-          ++len;
-        }
-      }
-      sm_start[m] = start < 0 ? 0 : start;
-      sm_len[m] = len;
-      sm_off[m] = off;
-      off += len;
-    }
-  }
+  for (int i = tid; i < MAXNZ; i += 256) sm_w[i] = tab[T_MW + i];
   __syncthreads();
 
-  const int f = blockIdx.x * 4 + w;
   const int len = lengths[b];
   const int F = len >= FRAME ? 1 + (len - FRAME) / HOP : 0;
+  for (int fi = 0; fi < FRAMES_PER_WAVE; ++fi) {
+  const int f = (blockIdx.x * 4 + w) * FRAMES_PER_WAVE + fi;
   if (f >= F || f >= Fmax) return;  // whole wave exits; no block barrier follows
   const float* x = wav + (int64_t)b * ld_wav + (int64_t)f * HOP;
   float v[7];
@@ -148,6 +182,9 @@ __global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restri
     for (int i = 0; i < ln; ++i) acc += sm_w[of + i] * pw[st + i];
     out[m] = logf(fmaxf(acc, 1.192092955078125e-07f));
   }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  }  // frames of this wave
 }
 
 __global__ __launch_bounds__(256) void fbank_cmvn_kernel(const int32_t* __restrict__ lengths, int Fmax, int Tmax,
@@ -211,10 +248,16 @@ extern "C" int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* length
   if (B <= 0 || Tmax <= 0 || !wav || !lengths || !feats || !mask || !work) return STE_ERR_ARG;
   const int Fmax = 2 * Tmax;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(fbank_logmel_kernel, dim3((Fmax + 3) / 4, B), dim3(256), 0, s, wav, ld_wav, lengths, Fmax, work);
+  float* tab = work;
+  float* logmel = work + TABLE_FLOATS;
+  hipLaunchKernelGGL(fbank_tables_kernel, dim3(1), dim3(256), 0, s, tab);
   STE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(fbank_cmvn_kernel, dim3(B), dim3(256), 0, s, lengths, Fmax, Tmax, work, pad_value, feats, mask,
-                     mask_mode);
+  const int fpb = 4 * FRAMES_PER_WAVE;
+  hipLaunchKernelGGL(fbank_logmel_kernel, dim3((Fmax + fpb - 1) / fpb, B), dim3(256), 0, s, wav, ld_wav, lengths,
+                     Fmax, tab, logmel);
+  STE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(fbank_cmvn_kernel, dim3(B), dim3(256), 0, s, lengths, Fmax, Tmax, logmel, pad_value, feats,
+                     mask, mask_mode);
   STE_CHECK_LAUNCH();
   return 0;
 }

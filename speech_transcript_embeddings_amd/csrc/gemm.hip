@@ -14,87 +14,24 @@
 // KM tiles are staged k-major in LDS and read with ds_read_b64_tr_b16 (hardware
 // transpose), so no operand is ever transposed in HBM.
 //
-// Tile 128x128x64, 256 threads (4 waves in 2x2, 64x64 per wave, 4x4 v_mfma_f32_16x16x32_bf16),
-// register-staged double-buffered LDS (issue next tile's global loads before the MFMAs,
-// write them after), XOR-swizzled LDS images (conflict-free ds_read_b128 / tr reads),
-// XCD-aware bijective block remap, LDS-staged epilogue with row-contiguous stores.
+// Two kernels, chosen per shape:
+//  * gemm_big: 256x256x64 tile, 512 threads (8 waves as 2(M)x4(N), 128x64 per wave,
+//    8x4 v_mfma_f32_16x16x32_bf16), operands streamed global->LDS with global_load_lds
+//    (16 B/lane, no VGPR staging) into a 2-deep LDS ring whose XOR swizzle is realised
+//    through the per-lane SOURCE address (the LDS image is lane-linear).  Used when the
+//    grid has >= ~1 wave of 256 CUs and K % 64 == 0 (all big encoder GEMMs).
+//  * gemm_bf16_kernel: 128x128x64 tile, 256 threads, register-staged (zero-filled
+//    tails in every dimension): small / ragged GEMMs and the dW reductions.
+// Both: XCD-aware bijective block remap + grouped tile order for L2 reuse, and an
+// LDS-staged epilogue with row-contiguous (16 B/lane) loads and stores.
 #include "common.h"
 #include "../../include/ste.h"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
-constexpr int TILE_BYTES = BM * BK * 2;            // 16 KiB per operand tile
-constexpr int EPI_LD = 68;                          // fp32 row stride of the epilogue staging
-constexpr int EPI_BYTES = 4 * 64 * EPI_LD * 4;      // 4 waves x 64 rows
-constexpr int LDS_BYTES = (4 * TILE_BYTES > EPI_BYTES) ? 4 * TILE_BYTES : EPI_BYTES;
-
-struct Stage {
-  bf16x8 v[4];
-};
-
-// ---- KC tile: [128 rows][64 k], 128 B per row, 16-B chunk c stored at (c ^ (row&7)).
-template <bool KC>
-STE_DEV void stage_load(Stage& st, const bf16* __restrict__ base, int64_t ld, int row0, int rows, int k0,
-                        int K, int tid) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int c = tid + NT * i;
-    int r, kk;
-    bool ok;
-    const bf16* p;
-    if (KC) {
-      r = c >> 3; kk = (c & 7) * 8;
-      ok = (row0 + r < rows) && (k0 + kk < K);
-      p = base + (int64_t)(row0 + r) * ld + (k0 + kk);
-    } else {
-      kk = c >> 4; r = (c & 15) * 8;
-      ok = (k0 + kk < K) && (row0 + r < rows);
-      p = base + (int64_t)(k0 + kk) * ld + (row0 + r);
-    }
-    if (ok) st.v[i] = *reinterpret_cast<const bf16x8*>(p);
-    else st.v[i] = bf16x8{};
-  }
-}
+typedef __attribute__((address_space(3))) void lds_void;
 
 STE_DEV int km_chunk_xor(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
-
-template <bool KC>
-STE_DEV void stage_store(const Stage& st, char* tile, int tid) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int c = tid + NT * i;
-    int off;
-    if (KC) {
-      int r = c >> 3, ch = c & 7;
-      off = r * 128 + ((ch ^ (r & 7)) << 4);
-    } else {
-      int k = c >> 4, ch = c & 15;
-      off = k * 256 + ((ch ^ km_chunk_xor(k)) << 4);
-    }
-    *reinterpret_cast<bf16x8*>(tile + off) = st.v[i];
-  }
-}
-
-// fragment for mfma_f32_16x16x32_bf16: lane l holds X[row=rb+(l&15)][k=32s+8(l>>4)+j], j=0..7
-template <bool KC>
-STE_DEV bf16x8 frag_load(const char* tile, int rb, int s, int lane) {
-  if (KC) {
-    int r = rb + (lane & 15);
-    int ch = s * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8*>(tile + r * 128 + ((ch ^ (r & 7)) << 4));
-  } else {
-    int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-    int k = s * 32 + 8 * g + q;
-    int quad = (rb >> 2) + p;
-    int a0 = k * 256 + ((quad ^ (km_chunk_xor(k) << 1)) << 3);
-    int k1 = k + 4;
-    int a1 = k1 * 256 + ((quad ^ (km_chunk_xor(k1) << 1)) << 3);
-    s16x4 lo = ds_read_tr16(tile + a0);
-    s16x4 hi = ds_read_tr16(tile + a1);
-    return join_tr(lo, hi);
-  }
-}
 
 STE_DEV float apply_act(float v, int act) {
   switch (act) {
@@ -115,34 +52,211 @@ STE_DEV float act_grad(float z, int act) {
   }
 }
 
-template <bool A_KC, bool B_KC>
-__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(ste_gemm_args p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // LDS_BYTES dynamic
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+// ------------------------------------------------------------------ epilogue
+// The calling wave has staged a [nrows x 64] fp32 tile (row stride EPI_LD) at `epi`;
+// rows map to output rows row0.., columns to col0..col0+63.  16 lanes per row, 4 cols/lane.
+constexpr int EPI_LD = 68;
 
-  // ---- block -> tile (bijective XCD remap, then grouped ordering for L2 reuse)
-  const int num_m = (p.M + BM - 1) / BM, num_n = (p.N + BN - 1) / BN;
-  const int tiles = num_m * num_n;
-  const int nwg = gridDim.x;
+struct EpiState {
+  f32x4 csum;
+};
+
+STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, int row0, int col0, int batch,
+                           int lane, f32x4& csum) {
+  const int col = col0 + (lane & 15) * 4;
+  const int nval = p.N - col;  // valid columns from `col` (>= 4: vector path)
+  if (nval <= 0) return;
+  f32x4 bias = {0.f, 0.f, 0.f, 0.f};
+  if (p.bias) {
+    if (nval >= 4) bias = *reinterpret_cast<const f32x4*>(p.bias + col);
+    else for (int e = 0; e < nval; ++e) bias[e] = p.bias[col + e];
+  }
+  const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
+  const float inv_keep = p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f;
+  const int64_t offC = (int64_t)batch * p.strideC;
+  const int64_t offR = (int64_t)batch * p.strideR;
+  for (int lr = lane >> 4; lr < nrows; lr += 4) {
+    const int row = row0 + lr;
+    if (row >= p.M) break;
+    f32x4 v = *reinterpret_cast<const f32x4*>(epi + lr * EPI_LD + (lane & 15) * 4);
+    v = (v + bias) * p.alpha;
+    if (p.act >= STE_ACT_SWISH && p.act <= STE_ACT_RELU) {
+      if (p.C2) {
+        bf16* c2 = (bf16*)p.C2 + offC + (int64_t)row * p.ldc2 + col;
+        if (nval >= 4) store_bf16x4(c2, v);
+        else for (int e = 0; e < nval; ++e) c2[e] = (bf16)v[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act);
+    } else if (p.act >= STE_ACT_SWISH_BWD) {
+      const bf16* zp = (const bf16*)p.Z + offC + (int64_t)row * p.ldz + col;
+      f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      if (nval >= 4) z = load_bf16x4(zp);
+      else for (int e = 0; e < nval; ++e) z[e] = (float)zp[e];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] *= act_grad(z[e], p.act);
+    }
+    if (p.drop_p > 0.f) {
+      const uint64_t base = (uint64_t)row * (uint64_t)p.drop_ld + (uint64_t)col;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] *= drop_scale(p.seed, base + e, thresh, inv_keep);
+    }
+    if (p.row_scale) v = v * p.row_scale[row];
+    if (nval < 4) for (int e = nval; e < 4; ++e) v[e] = 0.f;
+    if (p.colsum) csum += v;
+    if (p.R) {
+      if (p.r_bf16) {
+        const bf16* rp = (const bf16*)p.R + offR + (int64_t)row * p.ldr + col;
+        if (nval >= 4) v += load_bf16x4(rp);
+        else for (int e = 0; e < nval; ++e) v[e] += (float)rp[e];
+      } else {
+        const float* rp = (const float*)p.R + offR + (int64_t)row * p.ldr + col;
+        if (nval >= 4) v += *reinterpret_cast<const f32x4*>(rp);
+        else for (int e = 0; e < nval; ++e) v[e] += rp[e];
+      }
+    }
+    if (p.c_bf16) {
+      bf16* c = (bf16*)p.C + offC + (int64_t)row * p.ldc + col;
+      if (nval >= 4) {
+        if (p.beta != 0.f) v += load_bf16x4(c) * p.beta;
+        store_bf16x4(c, v);
+      } else {
+        for (int e = 0; e < nval; ++e) c[e] = (bf16)(v[e] + (p.beta != 0.f ? p.beta * (float)c[e] : 0.f));
+      }
+    } else {
+      float* c = (float*)p.C + offC + (int64_t)row * p.ldc + col;
+      if (nval >= 4) {
+        if (p.beta != 0.f) v += *reinterpret_cast<const f32x4*>(c) * p.beta;
+        *reinterpret_cast<f32x4*>(c) = v;
+      } else {
+        for (int e = 0; e < nval; ++e) c[e] = v[e] + (p.beta != 0.f ? p.beta * c[e] : 0.f);
+      }
+    }
+    if (p.C3) {
+      bf16* c3 = (bf16*)p.C3 + offC + (int64_t)row * p.ldc3 + col;
+      if (nval >= 4) store_bf16x4(c3, v);
+      else for (int e = 0; e < nval; ++e) c3[e] = (bf16)v[e];
+    }
+  }
+}
+
+STE_DEV void colsum_flush(const ste_gemm_args& p, f32x4 csum, int col0, int batch, int lane) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    csum[e] += __shfl_xor(csum[e], 16, 64);
+    csum[e] += __shfl_xor(csum[e], 32, 64);
+  }
+  const int col = col0 + (lane & 15) * 4;
+  if (lane < 16) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (col + e < p.N) atomicAdd(p.colsum + (int64_t)batch * p.N + col + e, csum[e]);
+  }
+}
+
+// block id -> (batch, tile_m, tile_n): bijective XCD remap, then groups of 8 m-tiles
+STE_DEV void map_tile(int nwg, int num_m, int num_n, int& batch, int& tm, int& tn) {
   int bid = blockIdx.x;
   {
     int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int batch = bid / tiles;
+  const int tiles = num_m * num_n;
+  batch = bid / tiles;
   int t = bid - batch * tiles;
   constexpr int GROUP = 8;
   int group = t / (GROUP * num_n);
   int first_m = group * GROUP;
   int gsize = min(num_m - first_m, GROUP);
-  int tm = first_m + (t % (GROUP * num_n)) % gsize;
-  int tn = (t % (GROUP * num_n)) / gsize;
-  const int m0 = tm * BM, n0 = tn * BN;
+  tm = first_m + (t % (GROUP * num_n)) % gsize;
+  tn = (t % (GROUP * num_n)) / gsize;
+}
 
+// =========================================================== small/ragged kernel
+namespace small {
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_BYTES = BM * BK * 2;
+constexpr int EPI_BYTES = 4 * 64 * EPI_LD * 4;
+constexpr int LDS_BYTES = (4 * TILE_BYTES > EPI_BYTES) ? 4 * TILE_BYTES : EPI_BYTES;
+
+struct Stage {
+  bf16x8 v[4];
+};
+
+template <bool KC>
+STE_DEV void stage_load(Stage& st, const bf16* __restrict__ base, int64_t ld, int row0, int rows, int k0, int K,
+                        int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int c = tid + NT * i;
+    int r, kk;
+    bool ok;
+    const bf16* p;
+    if (KC) {
+      r = c >> 3; kk = (c & 7) * 8;
+      ok = (row0 + r < rows) && (k0 + kk < K);
+      p = base + (int64_t)(row0 + r) * ld + (k0 + kk);
+    } else {
+      kk = c >> 4; r = (c & 15) * 8;
+      ok = (k0 + kk < K) && (row0 + r < rows);
+      p = base + (int64_t)(k0 + kk) * ld + (row0 + r);
+    }
+    if (ok) st.v[i] = *reinterpret_cast<const bf16x8*>(p);
+    else st.v[i] = bf16x8{};
+  }
+}
+
+template <bool KC>
+STE_DEV void stage_store(const Stage& st, char* tile, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int c = tid + NT * i;
+    int off;
+    if (KC) {
+      int r = c >> 3, ch = c & 7;
+      off = r * 128 + ((ch ^ (r & 7)) << 4);
+    } else {
+      int k = c >> 4, ch = c & 15;
+      off = k * 256 + ((ch ^ km_chunk_xor(k)) << 4);
+    }
+    *reinterpret_cast<bf16x8*>(tile + off) = st.v[i];
+  }
+}
+}  // namespace small
+
+// fragment for mfma_f32_16x16x32_bf16: lane l holds X[row=rb+(l&15)][k=32s+8(l>>4)+j], j=0..7.
+// KC image: [rows][64 k] (128 B rows, chunk ^ (row&7));  KM image: [64 k][ROWB bytes] (chunk ^ km_xor(k)).
+template <bool KC, int KM_ROW_BYTES>
+STE_DEV bf16x8 frag_load(const char* tile, int rb, int s, int lane) {
+  if (KC) {
+    int r = rb + (lane & 15);
+    int ch = s * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(tile + r * 128 + ((ch ^ (r & 7)) << 4));
+  } else {
+    int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    int k = s * 32 + 8 * g + q;
+    int quad = (rb >> 2) + p;
+    int a0 = k * KM_ROW_BYTES + ((quad ^ (km_chunk_xor(k) << 1)) << 3);
+    int k1 = k + 4;
+    int a1 = k1 * KM_ROW_BYTES + ((quad ^ (km_chunk_xor(k1) << 1)) << 3);
+    s16x4 lo = ds_read_tr16(tile + a0);
+    s16x4 hi = ds_read_tr16(tile + a1);
+    return join_tr(lo, hi);
+  }
+}
+
+template <bool A_KC, bool B_KC>
+__global__ __launch_bounds__(small::NT, 2) void gemm_bf16_kernel(ste_gemm_args p) {
+  using namespace small;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // LDS_BYTES dynamic
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int num_m = (p.M + BM - 1) / BM, num_n = (p.N + BN - 1) / BN;
+  int batch, tm, tn;
+  map_tile(gridDim.x, num_m, num_n, batch, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
   const bf16* A = (const bf16*)p.A + (int64_t)batch * p.strideA;
   const bf16* B = (const bf16*)p.B + (int64_t)batch * p.strideB;
-
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -171,9 +285,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(ste_gemm_args p) {
     for (int s = 0; s < 2; ++s) {
       bf16x8 fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = frag_load<A_KC>(ta, wm * 64 + i * 16, s, lane);
+      for (int i = 0; i < 4; ++i) fa[i] = frag_load<A_KC, 256>(ta, wm * 64 + i * 16, s, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = frag_load<B_KC>(tb, wn * 64 + j * 16, s, lane);
+      for (int j = 0; j < 4; ++j) fb[j] = frag_load<B_KC, 256>(tb, wn * 64 + j * 16, s, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -187,7 +301,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(ste_gemm_args p) {
     __syncthreads();
   }
 
-  // ---- epilogue: stage the wave's 64x64 fp32 tile through LDS, then row-contiguous I/O
   float* epi = reinterpret_cast<float*>(smem) + wave * 64 * EPI_LD;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -196,77 +309,146 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(ste_gemm_args p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         epi[(i * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[i][j][r];
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own-wave LDS writes done (wave-private region)
+  __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
-
-  const int col = n0 + wn * 64 + (lane & 15) * 4;
-  const bool col_ok = col < p.N;
-  f32x4 bias = {0.f, 0.f, 0.f, 0.f};
-  if (p.bias && col_ok) bias = *reinterpret_cast<const f32x4*>(p.bias + col);
-  const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
-  const float inv_keep = p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f;
   f32x4 csum = {0.f, 0.f, 0.f, 0.f};
-  const int64_t offC = (int64_t)batch * p.strideC;
-  const int64_t offR = (int64_t)batch * p.strideR;
+  epilogue_tile(p, epi, 64, m0 + wm * 64, n0 + wn * 64, batch, lane, csum);
+  if (p.colsum) colsum_flush(p, csum, n0 + wn * 64, batch, lane);
+}
 
-#pragma unroll 4
-  for (int it = 0; it < 16; ++it) {
-    const int lr = it * 4 + (lane >> 4);
-    const int row = m0 + wm * 64 + lr;
-    if (row >= p.M || !col_ok) continue;
-    f32x4 v = *reinterpret_cast<const f32x4*>(epi + lr * EPI_LD + (lane & 15) * 4);
-    v = (v + bias) * p.alpha;
-    if (p.act >= STE_ACT_SWISH && p.act <= STE_ACT_RELU) {
-      if (p.C2) store_bf16x4((bf16*)p.C2 + offC + (int64_t)row * p.ldc2 + col, v);
+// ================================================================= big kernel
+namespace big {
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+constexpr int TILE_BYTES = BM * BK * 2;        // 32 KiB per operand per stage
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;     // 128 KiB: 2-deep ring
+constexpr int EPI_ROWS = 32;                   // rows staged per epilogue pass per wave
+
+// issue this wave's 4 global_load_lds pieces (1 KiB each) of one operand tile.
+// KC tile [256 rows][64 k]: piece p = rows 8p..8p+7; lane L -> row 8p+L/8, chunk (L%8)^(L/8).
+// KM tile [64 k][256 rows] (512 B k-rows): piece p = k-rows 2p,2p+1; lane L -> k-row 2p+L/32,
+//   logical chunk (L%32) ^ km_xor(k-row).  Row indices past the operand are clamped (their
+//   products only reach discarded outputs); K % 64 == 0 is required.
+template <bool KC>
+STE_DEV void issue_tile(const bf16* base, int64_t ld, int row0, int rows, int k0, char* tile, int wave, int lane) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act);
-    } else if (p.act >= STE_ACT_SWISH_BWD) {
-      f32x4 z = load_bf16x4((const bf16*)p.Z + offC + (int64_t)row * p.ldz + col);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] *= act_grad(z[e], p.act);
-    }
-    if (p.drop_p > 0.f) {
-      const uint64_t base = (uint64_t)row * (uint64_t)p.drop_ld + (uint64_t)col;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] *= drop_scale(p.seed, base + e, thresh, inv_keep);
-    }
-    if (p.row_scale) v = v * p.row_scale[row];
-    if (p.colsum) csum += v;
-    if (p.R) {
-      if (p.r_bf16) v += load_bf16x4((const bf16*)p.R + offR + (int64_t)row * p.ldr + col);
-      else v += *reinterpret_cast<const f32x4*>((const float*)p.R + offR + (int64_t)row * p.ldr + col);
-    }
-    if (p.c_bf16) {
-      bf16* c = (bf16*)p.C + offC + (int64_t)row * p.ldc + col;
-      if (p.beta != 0.f) v += load_bf16x4(c) * p.beta;
-      store_bf16x4(c, v);
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave * 4 + i;
+    const bf16* src;
+    if (KC) {
+      const int r = piece * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ (lane >> 3);
+      const int gr = min(row0 + r, rows - 1);
+      src = base + (int64_t)gr * ld + k0 + ch * 8;
     } else {
-      float* c = (float*)p.C + offC + (int64_t)row * p.ldc + col;
-      if (p.beta != 0.f) v += *reinterpret_cast<const f32x4*>(c) * p.beta;
-      *reinterpret_cast<f32x4*>(c) = v;
+      const int kk = piece * 2 + (lane >> 5);
+      const int ch = (lane & 31) ^ km_chunk_xor(kk);
+      const int gc = min(row0 + ch * 8, rows - 8);
+      src = base + (int64_t)(k0 + kk) * ld + gc;
     }
-    if (p.C3) store_bf16x4((bf16*)p.C3 + offC + (int64_t)row * p.ldc3 + col, v);
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(tile + piece * 1024), 16, 0, 0);
   }
-  if (p.colsum) {
+}
+}  // namespace big
+
+template <bool A_KC, bool B_KC>
+__global__ __launch_bounds__(big::NT, 2) void gemm_big_kernel(ste_gemm_args p) {
+  using namespace big;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int num_m = (p.M + BM - 1) / BM, num_n = (p.N + BN - 1) / BN;
+  int batch, tm, tn;
+  map_tile(gridDim.x, num_m, num_n, batch, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const bf16* A = (const bf16*)p.A + (int64_t)batch * p.strideA;
+  const bf16* B = (const bf16*)p.B + (int64_t)batch * p.strideB;
+
+  f32x4 acc[8][4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      csum[e] += __shfl_xor(csum[e], 16, 64);
-      csum[e] += __shfl_xor(csum[e], 32, 64);
-    }
-    if (lane < 16 && col_ok) {
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(p.colsum + (int64_t)batch * p.N + col + e, csum[e]);
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / BK;
+  issue_tile<A_KC>(A, p.lda, m0, p.M, 0, smem, wave, lane);
+  issue_tile<B_KC>(B, p.ldb, n0, p.N, 0, smem + TILE_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      char* nxt = smem + (cur ^ 1) * STAGE_BYTES;
+      issue_tile<A_KC>(A, p.lda, m0, p.M, (kt + 1) * BK, nxt, wave, lane);
+      issue_tile<B_KC>(B, p.ldb, n0, p.N, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
     }
+    const char* ta = smem + cur * STAGE_BYTES;
+    const char* tb = ta + TILE_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag_load<B_KC, 512>(tb, wn * 64 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8 fa = frag_load<A_KC, 512>(ta, wm * 128 + i * 16, s, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa, fb[j], acc[i][j]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
+
+  // epilogue: 4 passes of 32 rows x 64 cols per wave through LDS
+  float* epi = reinterpret_cast<float*>(smem) + wave * EPI_ROWS * EPI_LD;
+  f32x4 csum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ps = 0; ps < 4; ++ps) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          epi[(ii * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[2 * ps + ii][j][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    epilogue_tile(p, epi, EPI_ROWS, m0 + wm * 128 + ps * EPI_ROWS, n0 + wn * 64, batch, lane, csum);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (p.colsum) colsum_flush(p, csum, n0 + wn * 64, batch, lane);
 }
 
 template <bool A_KC, bool B_KC>
-int launch(const ste_gemm_args& a, hipStream_t s) {
+int launch_small(const ste_gemm_args& a, hipStream_t s) {
+  using namespace small;
   const int num_m = (a.M + BM - 1) / BM, num_n = (a.N + BN - 1) / BN;
-  const int nb = num_m * num_n * (a.batch > 0 ? a.batch : 1);
+  const int nb = num_m * num_n * a.batch;
   hipLaunchKernelGGL((gemm_bf16_kernel<A_KC, B_KC>), dim3(nb), dim3(NT), LDS_BYTES, s, a);
   STE_CHECK_LAUNCH();
   return 0;
+}
+
+template <bool A_KC, bool B_KC>
+int launch_big(const ste_gemm_args& a, hipStream_t s) {
+  using namespace big;
+  const int num_m = (a.M + BM - 1) / BM, num_n = (a.N + BN - 1) / BN;
+  const int nb = num_m * num_n * a.batch;
+  hipLaunchKernelGGL((gemm_big_kernel<A_KC, B_KC>), dim3(nb), dim3(NT), LDS_BYTES, s, a);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+bool big_ok(const ste_gemm_args& a) {
+  if (a.K % big::BK) return false;
+  if (!a.a_kc || a.M < 8) return false;                 // dW reductions stay on the small kernel
+  if (!a.b_kc && (a.N % 8)) return false;
+  const long tiles = (long)((a.M + 255) / 256) * ((a.N + 255) / 256) * a.batch;
+  return tiles >= 240;
 }
 
 }  // namespace
@@ -276,15 +458,22 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
   ste_gemm_args a = *args;
   if (a.batch <= 0) a.batch = 1;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) return STE_ERR_ARG;
-  // alignment contract (16-B operand chunks, 16-B epilogue vectors)
-  if ((a.N & 3) != 0) return STE_ERR_SHAPE;
+  // alignment contract (16-B operand chunks)
   if (a.a_kc ? (a.K & 7) || (a.lda & 7) : (a.M & 7) || (a.lda & 7)) return STE_ERR_SHAPE;
   if (a.b_kc ? (a.K & 7) || (a.ldb & 7) : (a.N & 7) || (a.ldb & 7)) return STE_ERR_SHAPE;
-  if ((a.ldc & 3) || (a.C2 && (a.ldc2 & 3)) || (a.C3 && (a.ldc3 & 3)) || (a.R && (a.ldr & 3))) return STE_ERR_SHAPE;
   if (a.drop_ld == 0) a.drop_ld = a.N;
+  static int force_small = -1;
+  if (force_small < 0) {
+    const char* e = getenv("STE_GEMM_SMALL_ONLY");
+    force_small = (e && e[0] == '1') ? 1 : 0;
+  }
   hipStream_t s = (hipStream_t)stream;
-  if (a.a_kc && a.b_kc) return launch<true, true>(a, s);
-  if (a.a_kc && !a.b_kc) return launch<true, false>(a, s);
-  if (!a.a_kc && !a.b_kc) return launch<false, false>(a, s);
-  return launch<false, true>(a, s);
+  if (!force_small && big_ok(a)) {
+    if (a.b_kc) return launch_big<true, true>(a, s);
+    return launch_big<true, false>(a, s);
+  }
+  if (a.a_kc && a.b_kc) return launch_small<true, true>(a, s);
+  if (a.a_kc && !a.b_kc) return launch_small<true, false>(a, s);
+  if (!a.a_kc && !a.b_kc) return launch_small<false, false>(a, s);
+  return launch_small<false, true>(a, s);
 }

@@ -212,7 +212,7 @@ def fbank(wav, lengths, Tmax, *, pad_value=1.0, mask_mode=0, feats=None, mask=No
     if mask is None:
         mask = torch.empty((B, Tmax), device=dev, dtype=torch.int64)
     if work is None:
-        work = torch.empty((B, 2 * Tmax, 80), device=dev, dtype=F32)
+        work = torch.empty(2048 + B * 2 * Tmax * 80, device=dev, dtype=F32)
     call("ste_fbank", ptr(wav), wav.stride(0), ptr(lengths), B, Tmax, float(pad_value), ptr(feats), ptr(mask),
          int(mask_mode), ptr(work), _s())
     return feats, mask

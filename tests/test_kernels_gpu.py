@@ -25,7 +25,9 @@ def rel_err(a, b):
 
 
 # ------------------------------------------------------------------- GEMM
-@pytest.mark.parametrize("M,N,K", [(64, 128, 64), (300, 384, 200), (1000, 1024, 160), (130, 776, 96)])
+@pytest.mark.parametrize("M,N,K", [(64, 128, 64), (300, 384, 200), (1000, 1024, 160), (130, 776, 96),
+                                   # >= 240 256x256 tiles: the global_load_lds kernel (fwd KC.KC / dX KC.KM)
+                                   (4000, 4096, 512), (3999, 512, 4096), (3000, 5128, 256)])
 def test_gemm_layouts(ops, M, N, K):
     torch.manual_seed(M + N)
     x = torch.randn(M, K, device=DEV).bfloat16()
