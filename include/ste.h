@@ -76,6 +76,13 @@ typedef struct {
 
 int ste_gemm(const ste_gemm_args* args, void* stream);
 
+/* Which kernel ste_gemm would launch for these args (no launch, host-only):
+ * STE_GEMM_KERNEL_SMALL/BIG + variant, variant = (a_kc ? 0 : 2) + (b_kc ? 0 : 1).
+ * Lets profilers and bench.py attribute per-launch time to the rocprof kernel name. */
+#define STE_GEMM_KERNEL_SMALL 0
+#define STE_GEMM_KERNEL_BIG 4
+int ste_gemm_kernel(const ste_gemm_args* args);
+
 /* ------------------------------------------------------------- LayerNorm --
  * Replaces nn.LayerNorm forward/backward (every LN of both encoders and the
  * heads: tf:…wav2vec2_bert…:122,169,181,381-394; tf:…xlm_roberta…:64,333,389;
@@ -208,6 +215,23 @@ int ste_xattn1_bwd(const float* q, const void* k, const void* v, int64_t ldkv, c
                    int B, int S, int P, int nh, float scale, float drop_p, uint64_t seed, float* dq, float* dk,
                    float* dv, int64_t lddkv, void* stream);  /* dk/dv: fp32 rows of stride lddkv, += */
 
+/* WordLevelAlignmentModule attention core (ref:training/trainer_unfreeze.py:214-310, the
+ * nn.MultiheadAttention(P, nh=4, batch_first) of :237-242 with key_padding_mask, probs
+ * dropout): q bf16 [B*L, ldq], kv bf16 [B*T, ldkv] = [K | V] (K cols h*d, V cols P+h*d),
+ * kmask int32 [B*T] (0 = padded key), probs fp32 [B,nh,L,T] saved, out bf16 [B*L, ldo].
+ * Backward: dout bf16 -> dq bf16 [B*L, lddq], dkv fp32 [B*T, lddkv] (written), dsbuf
+ * fp32 [B,nh,L,T] workspace. */
+int ste_align_attn_fwd(const void* q, int64_t ldq, const void* kv, int64_t ldkv, const int32_t* kmask, int B, int L,
+                       int T, int P, int nh, float drop_p, uint64_t seed, float* probs, void* out, int64_t ldo,
+                       void* stream);
+int ste_align_attn_bwd(const void* q, int64_t ldq, const void* kv, int64_t ldkv, const float* probs,
+                       const void* dout, int64_t lddo, int B, int L, int T, int P, int nh, float drop_p,
+                       uint64_t seed, float* dsbuf, void* dq, int64_t lddq, float* dkv, int64_t lddkv, void* stream);
+/* Backward of a Linear(K -> 1) + activation pair: out[m][k] = a[m]*w[k]*act'(z[m][k]) (bf16),
+ * dw[k] += Σ_m a[m] z[m][k], db += Σ_m a[m]  (z = the activation OUTPUT for RELU/TANH). */
+int ste_rank1_bwd(const float* a, const float* w, const void* z, int M, int K, int act, void* out, float* dw,
+                  float* db, void* stream);
+
 /* ------------------------------------------------------------------- loss --
  * F.normalize(p=2, dim=1, eps=1e-12) rows (ref:training/trainer_unfreeze.py:561-563). */
 int ste_l2norm_fwd(const float* x, int rows, int cols, float* y, float* norms, void* stream);
@@ -253,6 +277,12 @@ int ste_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_
 
 /* ------------------------------------------------------------ elementwise -- */
 int ste_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+/* y = alpha*x + beta*y over strided fp32 rows (gradient accumulation of head branches). */
+int ste_axpby2d(float* y, int64_t ldy, const float* x, int64_t ldx, int64_t rows, int cols, float alpha, float beta,
+                void* stream);
+/* strided 2-D copy of 2- or 4-byte elements (concatenations feeding fusion GEMMs). */
+int ste_copy2d(void* y, int64_t ldy, const void* x, int64_t ldx, int64_t rows, int cols, int elem_bytes,
+               void* stream);
 /* out[c] += Σ_r x[r, c] over a row-major [rows, cols] fp32/bf16 matrix (bias gradients). */
 int ste_colsum(const void* x, int is_bf16, int64_t rows, int cols, int64_t ld, float* out, void* stream);
 /* y[r, c] = x[r, c] * scale[r]  (fp32, row stride ld) */

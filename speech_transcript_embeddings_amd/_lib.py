@@ -106,6 +106,7 @@ class AttnArgs(C.Structure):
 # name -> (restype, argtypes); every symbol declared in include/ste.h
 _SIGS = {
     "ste_gemm": (c_int, [C.POINTER(GemmArgs), c_void_p]),
+    "ste_gemm_kernel": (c_int, [C.POINTER(GemmArgs)]),
     "ste_layernorm_fwd": (c_int, [C.POINTER(LnFwdArgs), c_void_p]),
     "ste_layernorm_bwd": (c_int, [C.POINTER(LnBwdArgs), c_void_p]),
     "ste_attention_fwd": (c_int, [C.POINTER(AttnArgs), c_void_p]),
@@ -123,6 +124,13 @@ _SIGS = {
                                c_float, c_uint64, c_void_p, c_void_p, c_void_p]),
     "ste_xattn1_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                c_float, c_float, c_uint64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "ste_align_attn_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                   c_float, c_uint64, c_void_p, c_void_p, c_int64, c_void_p]),
+    "ste_align_attn_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int,
+                                   c_int, c_int, c_int, c_float, c_uint64, c_void_p, c_void_p, c_int64, c_void_p,
+                                   c_int64, c_void_p]),
+    "ste_rank1_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                              c_void_p]),
     "ste_l2norm_fwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "ste_l2norm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "ste_similarity": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
@@ -141,6 +149,8 @@ _SIGS = {
                           c_float, c_float, c_int, c_void_p, c_float, c_void_p]),
     "ste_cast_f32_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "ste_colsum": (c_int, [c_void_p, c_int, c_int64, c_int, c_int64, c_void_p, c_void_p]),
+    "ste_axpby2d": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_float, c_float, c_void_p]),
+    "ste_copy2d": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_int, c_void_p]),
     "ste_scale_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int64, c_void_p]),
     "ste_mask_i64_to_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "ste_version": (C.c_char_p, []),

@@ -229,7 +229,8 @@ __global__ __launch_bounds__(256) void fbank_cmvn_kernel(const int32_t* __restri
   for (int i = tid; i < Tmax * 2 * NMEL; i += 256) {
     const int t = i / (2 * NMEL), c = i % (2 * NMEL);
     const int f = 2 * t + (c >= NMEL), mm = c % NMEL;
-    float val = 0.f;
+    // beyond the clip: collate zero-padding (mode 0) or the extractor's batch padding value (mode 1)
+    float val = mask_mode == 0 ? 0.f : pad_value;
     if (t < Tb) val = f < F ? (x[(int64_t)f * NMEL + mm] - smean[mm]) * sinv[mm] : pad_value;
     o[i] = val;
   }

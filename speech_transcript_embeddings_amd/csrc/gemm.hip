@@ -453,6 +453,24 @@ bool big_ok(const ste_gemm_args& a) {
 
 }  // namespace
 
+static bool force_small_only() {
+  static int force_small = -1;
+  if (force_small < 0) {
+    const char* e = getenv("STE_GEMM_SMALL_ONLY");
+    force_small = (e && e[0] == '1') ? 1 : 0;
+  }
+  return force_small == 1;
+}
+
+extern "C" int ste_gemm_kernel(const ste_gemm_args* args) {
+  if (!args) return STE_ERR_ARG;
+  ste_gemm_args a = *args;
+  if (a.batch <= 0) a.batch = 1;
+  const int variant = (a.a_kc ? 0 : 2) + (a.b_kc ? 0 : 1);
+  if (!force_small_only() && big_ok(a)) return STE_GEMM_KERNEL_BIG + variant;
+  return STE_GEMM_KERNEL_SMALL + variant;
+}
+
 extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
   if (!args) return STE_ERR_ARG;
   ste_gemm_args a = *args;
@@ -462,13 +480,8 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
   if (a.a_kc ? (a.K & 7) || (a.lda & 7) : (a.M & 7) || (a.lda & 7)) return STE_ERR_SHAPE;
   if (a.b_kc ? (a.K & 7) || (a.ldb & 7) : (a.N & 7) || (a.ldb & 7)) return STE_ERR_SHAPE;
   if (a.drop_ld == 0) a.drop_ld = a.N;
-  static int force_small = -1;
-  if (force_small < 0) {
-    const char* e = getenv("STE_GEMM_SMALL_ONLY");
-    force_small = (e && e[0] == '1') ? 1 : 0;
-  }
   hipStream_t s = (hipStream_t)stream;
-  if (!force_small && big_ok(a)) {
+  if (!force_small_only() && big_ok(a)) {
     if (a.b_kc) return launch_big<true, true>(a, s);
     return launch_big<true, false>(a, s);
   }

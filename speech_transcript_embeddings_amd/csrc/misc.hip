@@ -12,6 +12,10 @@ __global__ void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, i
 __global__ void scale_rows_kernel(float* x, const float* s, int64_t rows, int cols, int64_t ld) {
   int64_t r = blockIdx.x;
   float f = s[r];
+  if ((cols & 3) || (ld & 3)) {
+    for (int c = threadIdx.x; c < cols; c += blockDim.x) x[r * ld + c] *= f;
+    return;
+  }
   for (int c = threadIdx.x * 4; c < cols; c += blockDim.x * 4) {
     f32x4* p = reinterpret_cast<f32x4*>(x + r * ld + c);
     *p = *p * f;
@@ -51,7 +55,43 @@ __global__ void colsum_kernel(const void* x, int is_bf16, int64_t rows, int cols
     if (cc < cols) atomicAdd(out + cc, s);
   }
 }
+// y[r, c] = alpha * x[r, c] + beta * y[r, c] (fp32, strided rows)
+__global__ void axpby2d_kernel(float* y, int64_t ldy, const float* x, int64_t ldx, int64_t rows, int cols,
+                               float alpha, float beta) {
+  const int64_t r = blockIdx.x;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    float* yp = y + r * ldy + c;
+    *yp = alpha * x[r * ldx + c] + (beta != 0.f ? beta * *yp : 0.f);
+  }
+}
+// 2-D copy of 2- or 4-byte elements between strided row-major views
+__global__ void copy2d_kernel(char* y, int64_t ldy, const char* x, int64_t ldx, int64_t rows, int cols, int esz) {
+  const int64_t r = blockIdx.x;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    if (esz == 4) reinterpret_cast<float*>(y)[r * ldy + c] = reinterpret_cast<const float*>(x)[r * ldx + c];
+    else reinterpret_cast<uint16_t*>(y)[r * ldy + c] = reinterpret_cast<const uint16_t*>(x)[r * ldx + c];
+  }
+}
 }  // namespace
+
+extern "C" int ste_axpby2d(float* y, int64_t ldy, const float* x, int64_t ldx, int64_t rows, int cols, float alpha,
+                           float beta, void* stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  hipLaunchKernelGGL(axpby2d_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, y, ldy, x, ldx, rows,
+                     cols, alpha, beta);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_copy2d(void* y, int64_t ldy, const void* x, int64_t ldx, int64_t rows, int cols, int elem_bytes,
+                          void* stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (elem_bytes != 2 && elem_bytes != 4) return STE_ERR_ARG;
+  hipLaunchKernelGGL(copy2d_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, (char*)y, ldy,
+                     (const char*)x, ldx, rows, cols, elem_bytes);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int ste_colsum(const void* x, int is_bf16, int64_t rows, int cols, int64_t ld, float* out, void* stream) {
   if (rows <= 0) return 0;
@@ -77,7 +117,7 @@ extern "C" int ste_cast_f32_bf16(const float* x, void* y, int64_t n, void* strea
 
 extern "C" int ste_scale_rows(float* x, const float* scale, int64_t rows, int cols, int64_t ld, void* stream) {
   if (rows <= 0) return 0;
-  if ((cols & 3) || (ld & 3)) return STE_ERR_SHAPE;
+  if (cols <= 0 || ld < cols) return STE_ERR_SHAPE;
   hipLaunchKernelGGL(scale_rows_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, x, scale, rows, cols, ld);
   STE_CHECK_LAUNCH();
   return 0;

@@ -630,8 +630,9 @@ class Engine:
         ctx = Ctx()
         base_seed = int(torch.randint(0, 2**62, (1,)).item()) if train else 0
         ids = torch.cat([batch["input_ids_pos"], batch["input_ids_neg"]], 0)
-        tmask = torch.cat([batch["attention_mask_pos"], batch["attention_mask_neg"]], 0)
-        th, thb = self.text_forward(ids.contiguous(), tmask.contiguous(), train, _site_seed(base_seed, 2), ctx)
+        tmask = torch.cat([batch["attention_mask_pos"], batch["attention_mask_neg"]], 0).contiguous()
+        ctx["_tmask_i64"] = tmask  # rows [0, b) = positive transcripts (alignment head's text mask)
+        th, thb = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx)
         ah, ahb = self.audio_forward(batch["input_values"].contiguous(), batch["attention_mask_audio"].contiguous(),
                                      train, _site_seed(base_seed, 3), ctx)
         ctx["_thb"], ctx["_ahb"] = thb, ahb
@@ -655,13 +656,13 @@ class Engine:
 
 
 def _copy_bf16(src, dst):
-    """dst[:] = src for bf16 2-D views (strided rows), via a bf16 GEMM-free kernel path."""
-    dst.copy_(src)
+    """dst[:] = src (strided 2-D views) on the ste_copy2d kernel."""
+    ops.copy2d(dst, src)
 
 
 def _copy_f32(src, dst):
-    dst.copy_(src)
+    ops.copy2d(dst, src)
 
 
 def _add_(dst, src):
-    dst.add_(src)
+    ops.axpby(dst, src, 1.0, 1.0)

@@ -12,7 +12,7 @@ import ctypes as C
 import torch
 
 from . import _lib
-from ._lib import GemmArgs, LnFwdArgs, LnBwdArgs, AttnArgs, ptr, call
+from ._lib import GemmArgs, LnFwdArgs, LnBwdArgs, AttnArgs, ptr, call, fn
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -75,7 +75,7 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
         ev0.record()
         call("ste_gemm", C.byref(args), _s())
         ev1.record()
-        GEMM_TRACE.append((gemm_kernel_name(a_kc, b_kc), 2.0 * M * N * K * batch, ev0, ev1))
+        GEMM_TRACE.append((gemm_kernel_name(args), 2.0 * M * N * K * batch, ev0, ev1))
     else:
         call("ste_gemm", C.byref(args), _s())
     return out
@@ -84,9 +84,12 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
 GEMM_TRACE = None  # list while bench.py measures per-launch GEMM durations with HIP events
 
 
-def gemm_kernel_name(a_kc, b_kc):
-    """The kernel symbol rocprofv3 reports for a GEMM launch (csrc/gemm.hip instantiation)."""
-    return f"gemm_bf16_kernel<{str(bool(a_kc)).lower()}, {str(bool(b_kc)).lower()}>"
+def gemm_kernel_name(args: GemmArgs) -> str:
+    """The kernel symbol rocprofv3 reports for this launch (asks the library which one it picks)."""
+    k = int(fn("ste_gemm_kernel")(C.byref(args)))
+    base = "gemm_big_kernel" if k >= 4 else "gemm_bf16_kernel"
+    v = k & 3
+    return f"{base}<{'false' if v & 2 else 'true'}, {'false' if v & 1 else 'true'}>"
 
 
 def linear(x, w, bias=None, **kw):
@@ -242,6 +245,23 @@ def xattn1_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, drop_p=0.0, seed=0):
          float((P // nh) ** -0.5), float(drop_p), int(seed) & (2**64 - 1), ptr(dq), ptr(dk), ptr(dv), _ld(dk), _s())
 
 
+def align_attn_fwd(q, kv, kmask, B, L, T, nh, probs, out, drop_p=0.0, seed=0):
+    P = kv.shape[-1] // 2
+    call("ste_align_attn_fwd", ptr(q), _ld(q), ptr(kv), _ld(kv), ptr(kmask), B, L, T, P, nh, float(drop_p),
+         int(seed) & (2**64 - 1), ptr(probs), ptr(out), _ld(out), _s())
+
+
+def align_attn_bwd(q, kv, probs, dout, B, L, T, nh, dsbuf, dq, dkv, drop_p=0.0, seed=0):
+    P = kv.shape[-1] // 2
+    call("ste_align_attn_bwd", ptr(q), _ld(q), ptr(kv), _ld(kv), ptr(probs), ptr(dout), _ld(dout), B, L, T, P, nh,
+         float(drop_p), int(seed) & (2**64 - 1), ptr(dsbuf), ptr(dq), _ld(dq), ptr(dkv), _ld(dkv), _s())
+
+
+def rank1_bwd(a, w, z, act, out, dw=None, db=None):
+    M, K = z.shape
+    call("ste_rank1_bwd", ptr(a), ptr(w), ptr(z), M, K, int(act), ptr(out), ptr(dw), ptr(db), _s())
+
+
 def l2norm_fwd(x, y, norms):
     call("ste_l2norm_fwd", ptr(x), x.shape[0], x.shape[1], ptr(y), ptr(norms), _s())
 
@@ -295,6 +315,23 @@ def adamw(p, g, m, v, p_bf16, *, lr, beta1, beta2, eps, wd, step, sumsq_acc=None
 def cast_bf16(x, y):
     call("ste_cast_f32_bf16", ptr(x), ptr(y), x.numel(), _s())
     return y
+
+
+def axpby(y, x, alpha=1.0, beta=1.0):
+    """y = alpha*x + beta*y for fp32 2-D (or 1-D) views."""
+    y2 = y if y.dim() == 2 else y.view(1, -1)
+    x2 = x if x.dim() == 2 else x.view(1, -1)
+    assert y2.shape == x2.shape and y.dtype == F32 and x.dtype == F32
+    call("ste_axpby2d", ptr(y2), _ld(y2), ptr(x2), _ld(x2), y2.shape[0], y2.shape[1], float(alpha), float(beta), _s())
+    return y
+
+
+def copy2d(dst, src):
+    assert dst.shape == src.shape and dst.dtype == src.dtype
+    d2 = dst if dst.dim() == 2 else dst.view(1, -1)
+    s2 = src if src.dim() == 2 else src.view(1, -1)
+    call("ste_copy2d", ptr(d2), _ld(d2), ptr(s2), _ld(s2), d2.shape[0], d2.shape[1], dst.element_size(), _s())
+    return dst
 
 
 def colsum(x, out):

@@ -1,0 +1,78 @@
+"""CPU checks of the C-ABI boundary (include/ste.h <-> libste.so <-> _lib.py).
+
+No kernel is launched: the library is loaded (its HIP runtime dependency resolves to the
+one torch ships), every declared symbol must be exported, the ctypes signature table must
+cover exactly the header, and the host-only entry points (version string, GEMM kernel
+selection, argument validation that returns before any launch) are exercised."""
+import ctypes as C
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = ROOT / "include" / "ste.h"
+
+
+def _declared():
+    txt = HEADER.read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(ste_\w+)\s*\(", txt, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from speech_transcript_embeddings_amd import _lib
+    if not _lib.LIB_PATH.exists():
+        pytest.fail("libste.so not built — run __graft_entry__.build()")
+    return _lib
+
+
+def test_header_declares_the_path():
+    names = _declared()
+    for must in ["ste_gemm", "ste_layernorm_fwd", "ste_layernorm_bwd", "ste_attention_fwd", "ste_attention_bwd",
+                 "ste_glu_dwconv_fwd", "ste_fbank", "ste_pair_loss_fwd", "ste_adamw", "ste_align_attn_fwd"]:
+        assert must in names, must
+
+
+def test_library_exports_every_declared_symbol(lib):
+    so = lib.load()
+    missing = [n for n in _declared() if not hasattr(so, n)]
+    assert not missing, missing
+
+
+def test_ctypes_table_matches_header(lib):
+    assert sorted(lib.SYMBOLS) == _declared()
+
+
+def test_version(lib):
+    assert lib.fn("ste_version")().decode().endswith("gfx950")
+
+
+def test_gemm_kernel_selection(lib):
+    a = lib.GemmArgs()
+    # encoder FFN GEMM at c2: M = 64*499 tokens -> the 256x256 global_load_lds kernel
+    a.M, a.N, a.K, a.batch, a.a_kc, a.b_kc = 31936, 4096, 1024, 1, 1, 1
+    assert lib.fn("ste_gemm_kernel")(C.byref(a)) == 4
+    a.b_kc = 0
+    assert lib.fn("ste_gemm_kernel")(C.byref(a)) == 5
+    # weight-gradient reduction (A = dYᵀ) and small head GEMMs stay on the 128x128 kernel
+    a.a_kc, a.b_kc = 0, 0
+    assert lib.fn("ste_gemm_kernel")(C.byref(a)) == 3
+    a.a_kc, a.b_kc, a.M, a.N = 1, 1, 64, 768
+    assert lib.fn("ste_gemm_kernel")(C.byref(a)) == 0
+    a.K = 1000  # K % 64 != 0 -> small kernel
+    a.M, a.N = 31936, 4096
+    assert lib.fn("ste_gemm_kernel")(C.byref(a)) == 0
+
+
+def test_argument_errors_return_status_without_launch(lib):
+    """Shape/alignment contract violations come back as non-zero status (-> SteError), never a launch."""
+    a = lib.GemmArgs()
+    a.M, a.N, a.K, a.a_kc, a.b_kc, a.lda, a.ldb = 64, 64, 100, 1, 1, 100, 100  # K % 8 != 0
+    assert lib.fn("ste_gemm")(C.byref(a), None) != 0
+    a.K = 0
+    assert lib.fn("ste_gemm")(C.byref(a), None) != 0
+    with pytest.raises(lib.SteError):
+        lib.call("ste_copy2d", None, 1, None, 1, 4, 4, 3, None)  # elem_bytes must be 2 or 4
+    assert lib.fn("ste_scale_rows")(None, None, 4, 0, 1, None) != 0

@@ -202,6 +202,38 @@ def test_fbank_matches_golden(ops):
         np.testing.assert_array_equal(mask1[i, :T].cpu().numpy(), z[f"{c}_mask"])
 
 
+def test_feature_extractor_api():
+    """Drop-in extractor (ref:856-866 call shape) per clip and batched vs the real extractor's output."""
+    from conftest import GOLDEN
+    from speech_transcript_embeddings_amd.features import SeamlessM4TFeatureExtractor, fbank
+    z = np.load(GOLDEN / "fbank_golden.npz")
+    fe = SeamlessM4TFeatureExtractor(padding_value=1.0)
+    cases = list(z["cases"])
+    for c in cases:
+        out = fe(z[f"{c}_wave"], sampling_rate=16000, return_tensors="pt")
+        T = z[f"{c}_feats"].shape[0]
+        assert out["input_features"].shape == (1, T, 160) and out["attention_mask"].shape == (1, T)
+        np.testing.assert_allclose(out["input_features"][0].cpu().numpy(), z[f"{c}_feats"], atol=2e-3, rtol=0)
+        np.testing.assert_array_equal(out["attention_mask"][0].cpu().numpy(), z[f"{c}_mask"])
+    with pytest.raises(ValueError):
+        fe(z[f"{cases[0]}_wave"], sampling_rate=8000)
+    # batched call pads to the longest clip with padding_value, mask 0 there
+    outb = fe([z[f"{c}_wave"] for c in cases], sampling_rate=16000)
+    for i, c in enumerate(cases):
+        T = z[f"{c}_feats"].shape[0]
+        np.testing.assert_allclose(outb["input_features"][i, :T].cpu().numpy(), z[f"{c}_feats"], atol=2e-3, rtol=0)
+        assert outb["input_features"][i, T:].eq(1.0).all() and outb["attention_mask"][i, T:].eq(0).all()
+    # training-path variant: collate semantics
+    N = max(z[f"{c}_wave"].size for c in cases)
+    wav = torch.zeros(len(cases), N, device=DEV)
+    for i, c in enumerate(cases):
+        wav[i, : z[f"{c}_wave"].size] = torch.from_numpy(z[f"{c}_wave"])
+    lens = torch.tensor([z[f"{c}_wave"].size for c in cases], dtype=torch.int32)
+    feats, mask = fbank(wav, lens)
+    np.testing.assert_array_equal(mask.cpu().numpy(), z["batch_mask"])
+    np.testing.assert_allclose(feats.cpu().numpy(), z["batch_feats"], atol=2e-3, rtol=0)
+
+
 # ---------------------------------------------------------------- heads
 def test_attn_pool(ops):
     torch.manual_seed(3)
@@ -272,6 +304,66 @@ def test_xattn1(ops, drop_p):
     assert rel_err(dq, qr.grad) < 1e-5
     assert rel_err(dk, kr.grad) < 1e-5
     assert rel_err(dv, vr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("B,L,T,P,drop_p", [(2, 12, 49, 128, 0.0), (3, 64, 499, 768, 0.0), (2, 20, 130, 256, 0.1)])
+def test_align_attn(ops, B, L, T, P, drop_p):
+    """WordLevelAlignmentModule's nn.MultiheadAttention core (4 heads, key padding mask,
+    probability dropout) fwd + bwd vs torch fp32 (ref:training/trainer_unfreeze.py:285-292)."""
+    torch.manual_seed(L + T)
+    nh = 4
+    q = torch.randn(B * L, P, device=DEV).bfloat16()
+    kv = torch.randn(B * T, 2 * P, device=DEV).bfloat16()
+    mask = torch.ones(B * T, dtype=torch.int32, device=DEV)
+    mask[T - T // 5:T] = 0  # first clip padded
+    probs = torch.empty(B * nh * L * T, device=DEV)
+    out = torch.empty(B * L, P, device=DEV, dtype=torch.bfloat16)
+    seed = 7
+    ops.align_attn_fwd(q, kv, mask, B, L, T, nh, probs, out, drop_p=drop_p, seed=seed)
+    d = P // nh
+    qr = q.float().clone().requires_grad_()
+    kvr = kv.float().clone().requires_grad_()
+    qh = qr.view(B, L, nh, d).transpose(1, 2)
+    kh = kvr[:, :P].reshape(B, T, nh, d).transpose(1, 2)
+    vh = kvr[:, P:].reshape(B, T, nh, d).transpose(1, 2)
+    s = (qh @ kh.transpose(-2, -1)) / math.sqrt(d)
+    s = s.masked_fill(mask.view(B, 1, 1, T) == 0, float("-inf"))
+    pr = s.softmax(-1)
+    assert rel_err(probs.view(B, nh, L, T), pr) < 1e-5
+    if drop_p > 0:
+        idx = np.arange(B * nh * L * T).astype(np.uint64)
+        pr = pr * torch.from_numpy(drop_scale(seed, idx, drop_p)).to(DEV).view(B, nh, L, T)
+    ref = (pr @ vh).transpose(1, 2).reshape(B * L, P)
+    assert rel_err(out, ref) < 5e-3  # bf16 output
+    do = torch.randn(B * L, P, device=DEV).bfloat16()
+    ref.backward(do.float())
+    dq = torch.empty(B * L, P, device=DEV, dtype=torch.bfloat16)
+    dkv = torch.empty(B * T, 2 * P, device=DEV)
+    dsbuf = torch.empty(B * nh * L * T, device=DEV)
+    ops.align_attn_bwd(q, kv, probs, do, B, L, T, nh, dsbuf, dq, dkv, drop_p=drop_p, seed=seed)
+    assert rel_err(dq, qr.grad) < 5e-3
+    assert rel_err(dkv, kvr.grad) < 1e-5
+
+
+def test_rank1_bwd(ops):
+    """Backward of Linear(K -> 1) after ReLU/tanh: dz = a ⊗ w ⊙ act'(z), dw = aᵀz, db = Σa."""
+    from speech_transcript_embeddings_amd import _lib
+    torch.manual_seed(8)
+    M, K = 300, 384
+    a = torch.randn(M, device=DEV)
+    w = torch.randn(K, device=DEV)
+    z = torch.randn(M, K, device=DEV).relu().bfloat16()
+    out = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
+    dw = torch.zeros(K, device=DEV)
+    db = torch.zeros(1, device=DEV)
+    ops.rank1_bwd(a, w, z, _lib.ACT_RELU_BWD, out, dw, db)
+    zf = z.float()
+    assert rel_err(out, a[:, None] * w[None] * (zf > 0)) < 5e-3
+    assert rel_err(dw, a @ zf) < 1e-5
+    assert abs(db.item() - a.sum().item()) < 1e-3
+    zt = torch.randn(M, K, device=DEV).tanh().bfloat16()
+    ops.rank1_bwd(a, w, zt, _lib.ACT_TANH_BWD_OUT, out)
+    assert rel_err(out, a[:, None] * w[None] * (1 - zt.float() ** 2)) < 5e-3
 
 
 def test_loss_chain(ops):
