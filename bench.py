@@ -106,6 +106,20 @@ def cpu_baseline(args):
                       f"layers, batch {B}, {args.cpu_steps} timed steps after 1 warmup, {dt:.2f} s/step"}
 
 
+def hbm_traffic(kernel):
+    """Per-launch HBM bytes of `kernel` from the latest committed PMC reduction
+    (profiles/rNN_hbm_traffic.json, made by profiles/pmc_traffic.py from separate rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes of this bench; gfx950 FETCH_SIZE x2 correction applied)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    if kernel not in d:
+        return None, os.path.relpath(files[-1], ROOT)
+    return d[kernel]["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -158,6 +172,7 @@ def main():
     gemm_time = sum(a[2] for a in agg.values()) / args.steps
     pairs = world * B * args.steps / elapsed
     gflop = GFLOP_PER_PAIR.get(args.unfreeze, 1370.4)
+    traffic, traffic_src = hbm_traffic(dom)
     out = {
         "metric": "audio–text pairs/sec (whole node), 10s@16kHz + 64-tok, 1/2/4/8 MI355X",
         "value": round(pairs, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -173,7 +188,8 @@ def main():
         "step_roofline_frac": round(pairs * gflop / (world * BF16_PEAK_TFLOPS * 1e3), 4),
         "roofline": {"bound": "mfma", "kernel": dom, "launches_per_step": n_l // args.steps,
                      "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
                      "avg_launch_us": round(tm / n_l * 1e6, 2), "algorithmic_gflop_per_launch": round(fl / n_l / 1e9, 3),
                      "gemm_ms_per_step_all_variants": round(gemm_time * 1e3, 2)},
         "loss": round(loss, 5),

@@ -97,6 +97,17 @@ STE_DEV float key_flag(const int32_t* mask, int bT, int key, int T) {
   return (mask == nullptr || mask[bT + key] != 0) ? 1.f : 0.f;
 }
 
+// 1-D grid of ceil(T/64) x H x B tiles; the tiles of one (batch, head) share an XCD so
+// their K/V (or Q/dO) re-reads hit that XCD's L2 instead of HBM.
+STE_DEV void tile_of_block(int T, int H, int& tile, int& h, int& b) {
+  const int ntile = (T + 63) / 64;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  tile = id % ntile;
+  const int bh = id / ntile;
+  h = bh % H;
+  b = bh / H;
+}
+
 // =========================================================================== forward
 template <bool REL, bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(ste_attn_args a) {
@@ -108,8 +119,10 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(ste_attn_args a) {
   float* sMask = sQE + 4 * 16 * NREL;                         // 2 x 64
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
-  const int h = blockIdx.y, b = blockIdx.z, T = a.T, H = a.H, bT = b * T;
-  const int q0 = blockIdx.x * TQ + w * 16, myq = q0 + li;
+  int tile, h, b;
+  tile_of_block(a.T, a.H, tile, h, b);
+  const int T = a.T, H = a.H, bT = b * T;
+  const int q0 = tile * TQ + w * 16, myq = q0 + li;
   const bf16* Qb = (const bf16*)a.q + h * HD;
   const bf16* Kb = (const bf16*)a.k + h * HD;
   const bf16* Vb = (const bf16*)a.v + h * HD;
@@ -269,8 +282,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(ste_attn_args a) {
   float* sMask = sG + 4 * 16 * 96;                             // 64
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
-  const int h = blockIdx.y, b = blockIdx.z, T = a.T, H = a.H, bT = b * T;
-  const int q0 = blockIdx.x * TQ + w * 16, myq = q0 + li;
+  int tile, h, b;
+  tile_of_block(a.T, a.H, tile, h, b);
+  const int T = a.T, H = a.H, bT = b * T;
+  const int q0 = tile * TQ + w * 16, myq = q0 + li;
   const bool qvalid = myq < T;
   const bf16* Qb = (const bf16*)a.q + h * HD;
   const bf16* Kb = (const bf16*)a.k + h * HD;
@@ -416,8 +431,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(ste_attn_args a) {
   float* sLD = sQE + 64 * NREL;                               // 2 x (64 lse + 64 delta)
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
-  const int h = blockIdx.y, b = blockIdx.z, T = a.T, H = a.H, bT = b * T;
-  const int mykey = blockIdx.x * TK + w * 16 + li;
+  int tile, h, b;
+  tile_of_block(a.T, a.H, tile, h, b);
+  const int T = a.T, H = a.H, bT = b * T;
+  const int mykey = tile * TK + w * 16 + li;
   const bool kvalid = mykey < T;
   const bool kmasked = kvalid && a.key_mask != nullptr && a.key_mask[bT + mykey] == 0;
   const bf16* Qb = (const bf16*)a.q + h * HD;
@@ -616,7 +633,7 @@ extern "C" int ste_attention_fwd(const ste_attn_args* a, void* stream) {
   if (int e = check(a)) return e;
   if (!a->lse || !a->o) return STE_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid((a->T + TQ - 1) / TQ, a->H, a->B);
+  dim3 grid((unsigned)(((a->T + TQ - 1) / TQ) * a->H * a->B));
   const bool rel = a->rel_E != nullptr, drop = a->drop_p > 0.f;
   if (rel && drop) hipLaunchKernelGGL((attn_fwd_kernel<true, true>), grid, dim3(NT), FWD_LDS, s, *a);
   else if (rel) hipLaunchKernelGGL((attn_fwd_kernel<true, false>), grid, dim3(NT), FWD_LDS, s, *a);
@@ -635,7 +652,7 @@ extern "C" int ste_attention_bwd(const ste_attn_args* a, void* stream) {
   const int64_t nrow = (int64_t)a->B * a->T * a->H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((nrow + 255) / 256)), dim3(256), 0, s, *a);
   STE_CHECK_LAUNCH();
-  dim3 grid((a->T + TQ - 1) / TQ, a->H, a->B);
+  dim3 grid((unsigned)(((a->T + TQ - 1) / TQ) * a->H * a->B));
   const bool rel = a->rel_E != nullptr, drop = a->drop_p > 0.f;
 #define STE_LAUNCH2(KER, LDS)                                                            \
   if (rel && drop) hipLaunchKernelGGL((KER<true, true>), grid, dim3(NT), LDS, s, *a);    \

@@ -99,4 +99,13 @@ STE_DEV bf16x8 join_tr(s16x4 lo, s16x4 hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// MI355X dispatches workgroup i of a launch to XCD i % 8, and each XCD has its own L2.
+// Return a logical id such that logically consecutive ids share an XCD (bijective on [0, n)),
+// so blocks that re-read the same operands (GEMM tiles of one row panel, attention q-tiles
+// of one (batch, head)) hit the same L2.
+STE_DEV int xcd_remap(int bid, int n) {
+  const int xcd = bid & 7, q = n >> 3, r = n & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
 #define STE_CHECK_LAUNCH() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)

@@ -156,11 +156,7 @@ STE_DEV void colsum_flush(const ste_gemm_args& p, f32x4 csum, int col0, int batc
 
 // block id -> (batch, tile_m, tile_n): bijective XCD remap, then groups of 8 m-tiles
 STE_DEV void map_tile(int nwg, int num_m, int num_n, int& batch, int& tm, int& tn) {
-  int bid = blockIdx.x;
-  {
-    int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
+  const int bid = xcd_remap(blockIdx.x, nwg);
   const int tiles = num_m * num_n;
   batch = bid / tiles;
   int t = bid - batch * tiles;

@@ -56,6 +56,8 @@ class EnhancedAudioTextModel(nn.Module):
         super().__init__()
         if not use_attentive_pooling:
             raise NotImplementedError("use_attentive_pooling=False (CLS / mean pooling) is not built yet")
+        if spec_augment:
+            raise NotImplementedError("SpecAugment time masking (tf:…wav2vec2_bert…:944-988) is not built yet")
         self.text_cfg = _resolve(text_model_name, _TEXT_CONFIGS, TextConfig)
         self.audio_cfg = _resolve(audio_model_name, _AUDIO_CONFIGS, AudioConfig)
         with torch.device("meta"):  # no host-side weights: values are initialised in the HBM store
