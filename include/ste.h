@@ -77,10 +77,11 @@ typedef struct {
 int ste_gemm(const ste_gemm_args* args, void* stream);
 
 /* Which kernel ste_gemm would launch for these args (no launch, host-only):
- * STE_GEMM_KERNEL_SMALL/BIG + variant, variant = (a_kc ? 0 : 2) + (b_kc ? 0 : 1).
+ * STE_GEMM_KERNEL_SMALL/BIG/8PH + variant, variant = (a_kc ? 0 : 2) + (b_kc ? 0 : 1).
  * Lets profilers and bench.py attribute per-launch time to the rocprof kernel name. */
 #define STE_GEMM_KERNEL_SMALL 0
 #define STE_GEMM_KERNEL_BIG 4
+#define STE_GEMM_KERNEL_8PH 8
 int ste_gemm_kernel(const ste_gemm_args* args);
 
 /* ------------------------------------------------------------- LayerNorm --

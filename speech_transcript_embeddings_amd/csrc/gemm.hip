@@ -54,16 +54,17 @@ STE_DEV float act_grad(float z, int act) {
 
 // ------------------------------------------------------------------ epilogue
 // The calling wave has staged a [nrows x 64] fp32 tile (row stride EPI_LD) at `epi`;
-// rows map to output rows row0.., columns to col0..col0+63.  16 lanes per row, 4 cols/lane.
+// rows map to output rows row0.., staged columns 0..31 to col0.., 32..63 to col1..
+// (col1 = col0 + 32 for a contiguous 64-column slab).  16 lanes per row, 4 cols/lane.
 constexpr int EPI_LD = 68;
 
 struct EpiState {
   f32x4 csum;
 };
 
-STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, int row0, int col0, int batch,
-                           int lane, f32x4& csum) {
-  const int col = col0 + (lane & 15) * 4;
+STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, int row0, int col0, int col1,
+                           int batch, int lane, f32x4& csum) {
+  const int col = ((lane & 8) ? col1 : col0) + (lane & 7) * 4;
   const int nval = p.N - col;  // valid columns from `col` (>= 4: vector path)
   if (nval <= 0) return;
   f32x4 bias = {0.f, 0.f, 0.f, 0.f};
@@ -140,13 +141,13 @@ STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, 
   }
 }
 
-STE_DEV void colsum_flush(const ste_gemm_args& p, f32x4 csum, int col0, int batch, int lane) {
+STE_DEV void colsum_flush(const ste_gemm_args& p, f32x4 csum, int col0, int col1, int batch, int lane) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     csum[e] += __shfl_xor(csum[e], 16, 64);
     csum[e] += __shfl_xor(csum[e], 32, 64);
   }
-  const int col = col0 + (lane & 15) * 4;
+  const int col = ((lane & 8) ? col1 : col0) + (lane & 7) * 4;
   if (lane < 16) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
@@ -308,8 +309,8 @@ __global__ __launch_bounds__(small::NT, 2) void gemm_bf16_kernel(ste_gemm_args p
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
   f32x4 csum = {0.f, 0.f, 0.f, 0.f};
-  epilogue_tile(p, epi, 64, m0 + wm * 64, n0 + wn * 64, batch, lane, csum);
-  if (p.colsum) colsum_flush(p, csum, n0 + wn * 64, batch, lane);
+  epilogue_tile(p, epi, 64, m0 + wm * 64, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane, csum);
+  if (p.colsum) colsum_flush(p, csum, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane);
 }
 
 // ================================================================= big kernel
@@ -412,11 +413,251 @@ __global__ __launch_bounds__(big::NT, 2) void gemm_big_kernel(ste_gemm_args p) {
           epi[(ii * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[2 * ps + ii][j][r];
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    epilogue_tile(p, epi, EPI_ROWS, m0 + wm * 128 + ps * EPI_ROWS, n0 + wn * 64, batch, lane, csum);
+    epilogue_tile(p, epi, EPI_ROWS, m0 + wm * 128 + ps * EPI_ROWS, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane,
+                  csum);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
   }
   if (p.colsum) colsum_flush(p, csum, n0 + wn * 64, batch, lane);
+}
+
+// ============================================================ 8-phase kernel
+// Same 256x256x64 tile and 2(M)x4(N) waves as gemm_big, but each K-tile is split into
+// four half-tiles (A rows / B cols that one C-quadrant of every wave needs) and the
+// K-loop runs 4 phases per K-tile:
+//   phase 0: read B-half0 + A-half0 -> MFMA quadrant (A0,B0)     stage B-half1 of tile t+1
+//   phase 1: read B-half1           -> MFMA (A0,B1)              stage A-half1 of tile t+1
+//   phase 2: read A-half1           -> MFMA (A1,B1)              stage A-half0 of tile t+2
+//   phase 3: (registers)            -> MFMA (A1,B0)              stage B-half0 of tile t+2
+// Every phase issues one half-tile of global_load_lds (2 per lane) and waits with a COUNTED
+// vmcnt(8) (4 half-tiles stay in flight across the barriers, never drained in steady state),
+// so HBM/L2 latency hides behind ~4 phases of MFMA.  Buffer safety (2 LDS buffers of 4
+// half-tiles): a half-tile is restaged >= 2 phases after its last ds_read (its data then
+// lives in registers), and read >= 1 phase after the wait+barrier that retires it.
+namespace ph8 {
+constexpr int NT = 512;
+constexpr int HALF = 16384;                   // 128 rows x 64 k bf16
+constexpr int BUF = 4 * HALF;                 // A0 | A1 | B0 | B1 of one K-tile
+constexpr int LDS_BYTES = 2 * BUF;            // 128 KiB
+
+// physical row pr (0..127) of half-tile h -> row of the 256-row tile.  A (G = 64): each
+// 64-row group (one per wave row wm) holds that wave's h-th 64 rows.  B (G = 128): half h
+// is the contiguous column range h*128.. (whole 256-B k-rows for the KM image); wave wn
+// owns columns wn*32..+31 of each half.
+template <int G>
+STE_DEV int half_row(int pr, int h) {
+  if (G == 128) return h * 128 + pr;
+  return (pr / G) * (2 * G) + h * G + (pr % G);
+}
+
+template <bool KC, int G>
+STE_DEV void stage_half(const bf16* base, int64_t ld, int row0, int rows, int k0, int h, char* dst, int wave,
+                        int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = wave * 2 + i;  // 1 KiB each, 16 per half-tile
+    const bf16* src;
+    if (KC) {  // image [128 rows][64 k], 128-B rows, chunk ^ (row & 7)
+      const int pr = piece * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ (lane >> 3);
+      const int gr = min(row0 + half_row<G>(pr, h), rows - 1);
+      src = base + (int64_t)gr * ld + k0 + ch * 8;
+    } else {   // image [64 k][128 cols], 256-B k-rows, chunk ^ km_xor(k)
+      const int kk = piece * 4 + (lane >> 4);
+      const int lc = (lane & 15) ^ km_chunk_xor(kk);
+      const int gc = min(row0 + half_row<G>(lc * 8, h), rows - 8);
+      src = base + (int64_t)(k0 + kk) * ld + gc;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
+  }
+}
+}  // namespace ph8
+
+#define STE_BARRIER() asm volatile("s_barrier" ::: "memory")
+#define STE_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+// KM fragment through inline-asm ds_read_b64_tr_b16.  The builtin form makes hipcc's
+// waitcnt pass treat the read as aliasing every in-flight global_load_lds and emit
+// vmcnt(0) before it, which drains the 8-phase pipeline; the asm form is invisible to that
+// pass, so the kernel orders these reads itself (lgkmcnt(0) + sched_barrier before the
+// MFMAs that consume them).
+STE_DEV s16x4 ds_read_tr16_asm(const char* p) {
+  typedef __attribute__((address_space(3))) const char lds_cchar;
+  const uint32_t off = (uint32_t)(uintptr_t)(lds_cchar*)p;
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(off) : "memory");
+  return r;
+}
+STE_DEV bf16x8 frag_load_km_asm(const char* tile, int rb, int s, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  const int k = s * 32 + 8 * g + q;
+  const int quad = (rb >> 2) + pp;
+  const int k1 = k + 4;
+  const s16x4 lo = ds_read_tr16_asm(tile + k * 256 + ((quad ^ (km_chunk_xor(k) << 1)) << 3));
+  const s16x4 hi = ds_read_tr16_asm(tile + k1 * 256 + ((quad ^ (km_chunk_xor(k1) << 1)) << 3));
+  return join_tr(lo, hi);
+}
+template <bool B_KC>
+STE_DEV bf16x8 frag_b_8ph(const char* tile, int rb, int s, int lane) {
+  if (B_KC) return frag_load<true, 256>(tile, rb, s, lane);
+  return frag_load_km_asm(tile, rb, s, lane);
+}
+// wait for this wave's LDS reads (incl. the asm ones) before the MFMA cluster
+#define STE_LDS_SYNC()                                  \
+  do {                                                  \
+    if (!B_KC) {                                        \
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+      __builtin_amdgcn_sched_barrier(0);                \
+    }                                                   \
+  } while (0)
+
+template <bool B_KC>
+__global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
+  using namespace ph8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int num_m = (p.M + 255) / 256, num_n = (p.N + 255) / 256;
+  int batch, tm, tn;
+  map_tile(gridDim.x, num_m, num_n, batch, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const bf16* A = (const bf16*)p.A + (int64_t)batch * p.strideA;
+  const bf16* B = (const bf16*)p.B + (int64_t)batch * p.strideB;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / 64;
+#define STAGE_A(t, h) stage_half<true, 64>(A, p.lda, m0, p.M, (t) * 64, h, smem + ((t) & 1) * BUF + (h) * HALF, wave, lane)
+#define STAGE_B(t, h) \
+  stage_half<B_KC, 128>(B, p.ldb, n0, p.N, (t) * 64, h, smem + ((t) & 1) * BUF + (2 + (h)) * HALF, wave, lane)
+  // prologue: tile 0 complete, tile 1's A0/B0 (the phases (-1,*) of the steady state)
+  STAGE_A(0, 0); STAGE_B(0, 0); STAGE_B(0, 1); STAGE_A(0, 1);
+  if (nk > 1) {
+    STAGE_A(1, 0); STAGE_B(1, 0);
+    STE_VMCNT(8);
+  } else {
+    STE_VMCNT(0);
+  }
+  STE_BARRIER();
+
+  bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
+  // Ping-pong: waves 4-7 run one barrier behind waves 0-3, so on every SIMD (one wave of
+  // each group) one wave's MFMA cluster overlaps the other's ds_reads + staging.  Buffer
+  // safety holds with the extra barrier of skew (reads stay >= 1 phase after the retiring
+  // wait+barrier of every producer, restaging >= 2 phases after the last read).
+  if (wm == 1) STE_BARRIER();
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
+    const bool tail = t + 2 >= nk;  // fewer stages in flight: drain fully instead of counting
+    // ---- phase 0
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) b0[j][s] = frag_b_8ph<B_KC>(buf + 2 * HALF, wn * 32 + j * 16, s, lane);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) a0[i][s] = frag_load<true, 256>(buf, wm * 64 + i * 16, s, lane);
+    if (t + 1 < nk) STAGE_B(t + 1, 1);
+    if (tail) STE_VMCNT(0); else STE_VMCNT(8);
+    STE_BARRIER();
+    STE_LDS_SYNC();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(a0[i][s], b0[j][s], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    STE_BARRIER();
+    // ---- phase 1
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) b1[j][s] = frag_b_8ph<B_KC>(buf + 3 * HALF, wn * 32 + j * 16, s, lane);
+    if (t + 1 < nk) STAGE_A(t + 1, 1);
+    if (tail) STE_VMCNT(0); else STE_VMCNT(8);
+    STE_BARRIER();
+    STE_LDS_SYNC();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(a0[i][s], b1[j][s], acc[i][2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    STE_BARRIER();
+    // ---- phase 2
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) a1[i][s] = frag_load<true, 256>(buf + HALF, wm * 64 + i * 16, s, lane);
+    if (t + 2 < nk) STAGE_A(t + 2, 0);
+    STE_BARRIER();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(a1[i][s], b1[j][s], acc[4 + i][2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    STE_BARRIER();
+    // ---- phase 3
+    if (t + 2 < nk) STAGE_B(t + 2, 0);
+    if (tail) STE_VMCNT(0); else STE_VMCNT(8);
+    STE_BARRIER();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(a1[i][s], b0[j][s], acc[4 + i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    STE_BARRIER();
+  }
+#undef STAGE_A
+#undef STAGE_B
+#undef STE_LDS_SYNC
+  if (wm == 0) STE_BARRIER();  // re-align the groups (equal barrier counts) before the LDS epilogue
+
+  // epilogue: acc[i][j] = rows wm*128 + i*16, cols (j >> 1)*128 + wn*32 + (j & 1)*16
+  float* epi = reinterpret_cast<float*>(smem) + wave * big::EPI_ROWS * EPI_LD;
+  f32x4 csum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ps = 0; ps < 4; ++ps) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          epi[(ii * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[2 * ps + ii][j][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    epilogue_tile(p, epi, big::EPI_ROWS, m0 + wm * 128 + ps * big::EPI_ROWS, n0 + wn * 32, n0 + 128 + wn * 32, batch,
+                  lane, csum);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (p.colsum) colsum_flush(p, csum, n0 + wn * 32, n0 + 128 + wn * 32, batch, lane);
+}
+
+template <bool B_KC>
+int launch_8ph(const ste_gemm_args& a, hipStream_t s) {
+  const int nb = ((a.M + 255) / 256) * ((a.N + 255) / 256) * a.batch;
+  hipLaunchKernelGGL((gemm_8ph_kernel<B_KC>), dim3(nb), dim3(ph8::NT), ph8::LDS_BYTES, s, a);
+  STE_CHECK_LAUNCH();
+  return 0;
 }
 
 template <bool A_KC, bool B_KC>
@@ -449,13 +690,16 @@ bool big_ok(const ste_gemm_args& a) {
 
 }  // namespace
 
-static bool force_small_only() {
-  static int force_small = -1;
-  if (force_small < 0) {
-    const char* e = getenv("STE_GEMM_SMALL_ONLY");
-    force_small = (e && e[0] == '1') ? 1 : 0;
-  }
-  return force_small == 1;
+static int env_flag(const char* name) {
+  const char* e = getenv(name);
+  return (e && e[0] == '1') ? 1 : 0;
+}
+// STE_GEMM_SMALL_ONLY=1: every shape on the 128x128 kernel; STE_GEMM_2PH=1: the 2-buffer
+// gemm_big schedule instead of the 8-phase one (A/B comparisons in one process).
+static int gemm_mode() {
+  static int mode = -1;
+  if (mode < 0) mode = env_flag("STE_GEMM_SMALL_ONLY") ? 0 : (env_flag("STE_GEMM_2PH") ? 1 : 2);
+  return mode;
 }
 
 extern "C" int ste_gemm_kernel(const ste_gemm_args* args) {
@@ -463,7 +707,7 @@ extern "C" int ste_gemm_kernel(const ste_gemm_args* args) {
   ste_gemm_args a = *args;
   if (a.batch <= 0) a.batch = 1;
   const int variant = (a.a_kc ? 0 : 2) + (a.b_kc ? 0 : 1);
-  if (!force_small_only() && big_ok(a)) return STE_GEMM_KERNEL_BIG + variant;
+  if (gemm_mode() > 0 && big_ok(a)) return (gemm_mode() == 2 ? STE_GEMM_KERNEL_8PH : STE_GEMM_KERNEL_BIG) + variant;
   return STE_GEMM_KERNEL_SMALL + variant;
 }
 
@@ -477,7 +721,9 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
   if (a.b_kc ? (a.K & 7) || (a.ldb & 7) : (a.N & 7) || (a.ldb & 7)) return STE_ERR_SHAPE;
   if (a.drop_ld == 0) a.drop_ld = a.N;
   hipStream_t s = (hipStream_t)stream;
-  if (!force_small_only() && big_ok(a)) {
+  const int mode = gemm_mode();
+  if (mode > 0 && big_ok(a)) {
+    if (mode == 2) return a.b_kc ? launch_8ph<true>(a, s) : launch_8ph<false>(a, s);
     if (a.b_kc) return launch_big<true, true>(a, s);
     return launch_big<true, false>(a, s);
   }

@@ -87,9 +87,11 @@ GEMM_TRACE = None  # list while bench.py measures per-launch GEMM durations with
 def gemm_kernel_name(args: GemmArgs) -> str:
     """The kernel symbol rocprofv3 reports for this launch (asks the library which one it picks)."""
     k = int(fn("ste_gemm_kernel")(C.byref(args)))
-    base = "gemm_big_kernel" if k >= 4 else "gemm_bf16_kernel"
     v = k & 3
-    return f"{base}<{'false' if v & 2 else 'true'}, {'false' if v & 1 else 'true'}>"
+    a_kc, b_kc = ("false" if v & 2 else "true"), ("false" if v & 1 else "true")
+    if k >= 8:
+        return f"gemm_8ph_kernel<{b_kc}>"
+    return f"{'gemm_big_kernel' if k >= 4 else 'gemm_bf16_kernel'}<{a_kc}, {b_kc}>"
 
 
 def linear(x, w, bias=None, **kw):
