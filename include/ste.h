@@ -41,8 +41,10 @@ extern "C" {
  *   R: v += R[m,n]                              (fp32, or bf16 if r_bf16)
  *   beta != 0: v += beta*C[m,n]
  *   C <- v (fp32, or bf16 if c_bf16);  C3 <- bf16(v) (optional)
- * Contract: N%4==0; KC operands need K%8==0 and ld%8==0; KM operands need
- * (M or N)%8==0 and ld%8==0.
+ * Contract: KC operands need K%8==0 and ld%8==0; KM operands need (M or N)%8==0
+ * and ld%8==0; for N >= 8, C, C2, C3, R, Z and bias start 16-B aligned with
+ * 16-B-multiple row strides (the epilogue moves 8 columns per lane).  Any N (ragged
+ * last columns are handled element-wise).
  */
 enum {
   STE_ACT_NONE = 0,

@@ -55,103 +55,132 @@ STE_DEV float act_grad(float z, int act) {
 // ------------------------------------------------------------------ epilogue
 // The calling wave has staged a [nrows x 64] fp32 tile (row stride EPI_LD) at `epi`;
 // rows map to output rows row0.., staged columns 0..31 to col0.., 32..63 to col1..
-// (col1 = col0 + 32 for a contiguous 64-column slab).  16 lanes per row, 4 cols/lane.
+// (col1 = col0 + 32 for a contiguous 64-column slab).  8 lanes per row, 8 columns per
+// lane: bf16 outputs leave as one 16-B store per lane (the epilogue is store-ISSUE-bound,
+// so instruction count, not bytes, sets its length).
 constexpr int EPI_LD = 68;
 
-struct EpiState {
-  f32x4 csum;
+struct Csum {
+  f32x4 lo, hi;
 };
 
+STE_DEV f32x8 load_bf16x8(const bf16* p) {
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+  f32x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = (float)v[e];
+  return r;
+}
+STE_DEV void store_bf16x8(bf16* p, f32x8 v) {
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+  *reinterpret_cast<bf16x8*>(p) = o;
+}
+STE_DEV f32x8 load_f32x8(const float* p) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+  return f32x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+STE_DEV void store_f32x8(float* p, f32x8 v) {
+  *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+// partial loads/stores for the last columns of a ragged N (e < nval only)
+STE_DEV f32x8 load_part(const void* p, bool is_bf16, int nval) {
+  f32x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = e < nval ? (is_bf16 ? (float)((const bf16*)p)[e] : ((const float*)p)[e]) : 0.f;
+  return r;
+}
+STE_DEV void store_part(void* p, bool is_bf16, f32x8 v, int nval) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    if (e < nval) {
+      if (is_bf16) ((bf16*)p)[e] = (bf16)v[e];
+      else ((float*)p)[e] = v[e];
+    }
+}
+STE_DEV f32x8 ld8(const void* p, bool is_bf16, bool full, int nval) {
+  if (!full) return load_part(p, is_bf16, nval);
+  return is_bf16 ? load_bf16x8((const bf16*)p) : load_f32x8((const float*)p);
+}
+STE_DEV void st8(void* p, bool is_bf16, f32x8 v, bool full, int nval) {
+  if (!full) store_part(p, is_bf16, v, nval);
+  else if (is_bf16) store_bf16x8((bf16*)p, v);
+  else store_f32x8((float*)p, v);
+}
+
 STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, int row0, int col0, int col1,
-                           int batch, int lane, f32x4& csum) {
-  const int col = ((lane & 8) ? col1 : col0) + (lane & 7) * 4;
-  const int nval = p.N - col;  // valid columns from `col` (>= 4: vector path)
+                           int batch, int lane, Csum& csum) {
+  const int cl = (lane & 7) * 8;  // staged column of this lane's 8
+  const int col = cl < 32 ? col0 + cl : col1 + (cl - 32);
+  const int nval = p.N - col;     // valid columns from `col`
   if (nval <= 0) return;
-  f32x4 bias = {0.f, 0.f, 0.f, 0.f};
-  if (p.bias) {
-    if (nval >= 4) bias = *reinterpret_cast<const f32x4*>(p.bias + col);
-    else for (int e = 0; e < nval; ++e) bias[e] = p.bias[col + e];
-  }
+  const bool full = nval >= 8;
+  const f32x8 bias = p.bias ? ld8(p.bias + col, false, full, nval) : f32x8{};
   const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
   const float inv_keep = p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f;
   const int64_t offC = (int64_t)batch * p.strideC;
   const int64_t offR = (int64_t)batch * p.strideR;
-  for (int lr = lane >> 4; lr < nrows; lr += 4) {
+  for (int lr = lane >> 3; lr < nrows; lr += 8) {
     const int row = row0 + lr;
     if (row >= p.M) break;
-    f32x4 v = *reinterpret_cast<const f32x4*>(epi + lr * EPI_LD + (lane & 15) * 4);
+    const float* src = epi + lr * EPI_LD + cl;
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(src), s1 = *reinterpret_cast<const f32x4*>(src + 4);
+    f32x8 v = f32x8{s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
     v = (v + bias) * p.alpha;
     if (p.act >= STE_ACT_SWISH && p.act <= STE_ACT_RELU) {
-      if (p.C2) {
-        bf16* c2 = (bf16*)p.C2 + offC + (int64_t)row * p.ldc2 + col;
-        if (nval >= 4) store_bf16x4(c2, v);
-        else for (int e = 0; e < nval; ++e) c2[e] = (bf16)v[e];
-      }
+      if (p.C2) st8((bf16*)p.C2 + offC + (int64_t)row * p.ldc2 + col, true, v, full, nval);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act);
+      for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act);
     } else if (p.act >= STE_ACT_SWISH_BWD) {
-      const bf16* zp = (const bf16*)p.Z + offC + (int64_t)row * p.ldz + col;
-      f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      if (nval >= 4) z = load_bf16x4(zp);
-      else for (int e = 0; e < nval; ++e) z[e] = (float)zp[e];
+      const f32x8 z = ld8((const bf16*)p.Z + offC + (int64_t)row * p.ldz + col, true, full, nval);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] *= act_grad(z[e], p.act);
+      for (int e = 0; e < 8; ++e) v[e] *= act_grad(z[e], p.act);
     }
     if (p.drop_p > 0.f) {
       const uint64_t base = (uint64_t)row * (uint64_t)p.drop_ld + (uint64_t)col;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] *= drop_scale(p.seed, base + e, thresh, inv_keep);
+      for (int e = 0; e < 8; ++e) v[e] *= drop_scale(p.seed, base + e, thresh, inv_keep);
     }
     if (p.row_scale) v = v * p.row_scale[row];
-    if (nval < 4) for (int e = nval; e < 4; ++e) v[e] = 0.f;
-    if (p.colsum) csum += v;
+    if (!full) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) if (e >= nval) v[e] = 0.f;
+    }
+    if (p.colsum) {
+      csum.lo += f32x4{v[0], v[1], v[2], v[3]};
+      csum.hi += f32x4{v[4], v[5], v[6], v[7]};
+    }
     if (p.R) {
-      if (p.r_bf16) {
-        const bf16* rp = (const bf16*)p.R + offR + (int64_t)row * p.ldr + col;
-        if (nval >= 4) v += load_bf16x4(rp);
-        else for (int e = 0; e < nval; ++e) v[e] += (float)rp[e];
-      } else {
-        const float* rp = (const float*)p.R + offR + (int64_t)row * p.ldr + col;
-        if (nval >= 4) v += *reinterpret_cast<const f32x4*>(rp);
-        else for (int e = 0; e < nval; ++e) v[e] += rp[e];
-      }
+      const char* rp = (const char*)p.R + (offR + (int64_t)row * p.ldr + col) * (p.r_bf16 ? 2 : 4);
+      v += ld8(rp, p.r_bf16, full, nval);
     }
-    if (p.c_bf16) {
-      bf16* c = (bf16*)p.C + offC + (int64_t)row * p.ldc + col;
-      if (nval >= 4) {
-        if (p.beta != 0.f) v += load_bf16x4(c) * p.beta;
-        store_bf16x4(c, v);
-      } else {
-        for (int e = 0; e < nval; ++e) c[e] = (bf16)(v[e] + (p.beta != 0.f ? p.beta * (float)c[e] : 0.f));
-      }
-    } else {
-      float* c = (float*)p.C + offC + (int64_t)row * p.ldc + col;
-      if (nval >= 4) {
-        if (p.beta != 0.f) v += *reinterpret_cast<const f32x4*>(c) * p.beta;
-        *reinterpret_cast<f32x4*>(c) = v;
-      } else {
-        for (int e = 0; e < nval; ++e) c[e] = v[e] + (p.beta != 0.f ? p.beta * c[e] : 0.f);
-      }
-    }
-    if (p.C3) {
-      bf16* c3 = (bf16*)p.C3 + offC + (int64_t)row * p.ldc3 + col;
-      if (nval >= 4) store_bf16x4(c3, v);
-      else for (int e = 0; e < nval; ++e) c3[e] = (bf16)v[e];
-    }
+    char* cp = (char*)p.C + (offC + (int64_t)row * p.ldc + col) * (p.c_bf16 ? 2 : 4);
+    if (p.beta != 0.f) v += ld8(cp, p.c_bf16, full, nval) * p.beta;
+    st8(cp, p.c_bf16, v, full, nval);
+    if (p.C3) st8((bf16*)p.C3 + offC + (int64_t)row * p.ldc3 + col, true, v, full, nval);
   }
 }
 
-STE_DEV void colsum_flush(const ste_gemm_args& p, f32x4 csum, int col0, int col1, int batch, int lane) {
+STE_DEV void colsum_flush(const ste_gemm_args& p, Csum csum, int col0, int col1, int batch, int lane) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    csum[e] += __shfl_xor(csum[e], 16, 64);
-    csum[e] += __shfl_xor(csum[e], 32, 64);
-  }
-  const int col = ((lane & 8) ? col1 : col0) + (lane & 7) * 4;
-  if (lane < 16) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (col + e < p.N) atomicAdd(p.colsum + (int64_t)batch * p.N + col + e, csum[e]);
+    for (int sh = 8; sh < 64; sh <<= 1) {
+      csum.lo[e] += __shfl_xor(csum.lo[e], sh, 64);
+      csum.hi[e] += __shfl_xor(csum.hi[e], sh, 64);
+    }
+  }
+  const int cl = (lane & 7) * 8;
+  const int col = cl < 32 ? col0 + cl : col1 + (cl - 32);
+  if (lane < 8) {
+    float* out = p.colsum + (int64_t)batch * p.N + col;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (col + e < p.N) atomicAdd(out + e, csum.lo[e]);
+      if (col + 4 + e < p.N) atomicAdd(out + 4 + e, csum.hi[e]);
+    }
   }
 }
 
@@ -308,7 +337,7 @@ __global__ __launch_bounds__(small::NT, 2) void gemm_bf16_kernel(ste_gemm_args p
         epi[(i * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[i][j][r];
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
-  f32x4 csum = {0.f, 0.f, 0.f, 0.f};
+  Csum csum = {};
   epilogue_tile(p, epi, 64, m0 + wm * 64, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane, csum);
   if (p.colsum) colsum_flush(p, csum, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane);
 }
@@ -401,24 +430,33 @@ __global__ __launch_bounds__(big::NT, 2) void gemm_big_kernel(ste_gemm_args p) {
 
   // epilogue: 4 passes of 32 rows x 64 cols per wave through LDS
   float* epi = reinterpret_cast<float*>(smem) + wave * EPI_ROWS * EPI_LD;
-  f32x4 csum = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ps = 0; ps < 4; ++ps) {
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          epi[(ii * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[2 * ps + ii][j][r];
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    epilogue_tile(p, epi, EPI_ROWS, m0 + wm * 128 + ps * EPI_ROWS, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane,
-                  csum);
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+  Csum csum = {};
+  // (explicit passes: a rolled pass loop would index acc dynamically and demote it to scratch)
+#define STE_EPI_PASS(PS)                                                                                     \
+  {                                                                                                          \
+    for (int ii = 0; ii < 2; ++ii) {                                                                         \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                                        \
+        _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                                      \
+          epi[(ii * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[2 * (PS) + ii][j][r];   \
+        }                                                                                                    \
+      }                                                                                                      \
+    }                                                                                                        \
+    __builtin_amdgcn_s_waitcnt(0xc07f);                                                                      \
+    __builtin_amdgcn_wave_barrier();                                                                         \
+    for (int hh = 0; hh < big::EPI_ROWS; hh += 16) {                                                         \
+      if (!EPI_SKIP) epilogue_tile(p, epi + hh * EPI_LD, 16, m0 + wm * 128 + (PS) * big::EPI_ROWS + hh,     \
+                                   EPI_COL0, EPI_COL1, batch, lane, csum);                                   \
+    }                                                                                                        \
+    __builtin_amdgcn_s_waitcnt(0xc07f);                                                                      \
+    __builtin_amdgcn_wave_barrier();                                                                         \
   }
-  if (p.colsum) colsum_flush(p, csum, n0 + wn * 64, batch, lane);
+  constexpr bool EPI_SKIP = false;
+#define EPI_COL0 (n0 + wn * 64)
+#define EPI_COL1 (n0 + wn * 64 + 32)
+  STE_EPI_PASS(0) STE_EPI_PASS(1) STE_EPI_PASS(2) STE_EPI_PASS(3)
+#undef EPI_COL0
+#undef EPI_COL1
+  if (p.colsum) colsum_flush(p, csum, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane);
 }
 
 // ============================================================ 8-phase kernel
@@ -511,7 +549,7 @@ STE_DEV bf16x8 frag_b_8ph(const char* tile, int rb, int s, int lane) {
     }                                                   \
   } while (0)
 
-template <bool B_KC>
+template <bool B_KC, bool EPI_SKIP>
 __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
   using namespace ph8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -632,30 +670,30 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
 
   // epilogue: acc[i][j] = rows wm*128 + i*16, cols (j >> 1)*128 + wn*32 + (j & 1)*16
   float* epi = reinterpret_cast<float*>(smem) + wave * big::EPI_ROWS * EPI_LD;
-  f32x4 csum = {0.f, 0.f, 0.f, 0.f};
+  Csum csum = {};
+#define EPI_COL0 (n0 + wn * 32)
+#define EPI_COL1 (n0 + 128 + wn * 32)
+  STE_EPI_PASS(0) STE_EPI_PASS(1) STE_EPI_PASS(2) STE_EPI_PASS(3)
+  if (EPI_SKIP) {
+    float keep = 0.f;
 #pragma unroll
-  for (int ps = 0; ps < 4; ++ps) {
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          epi[(ii * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[2 * ps + ii][j][r];
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    epilogue_tile(p, epi, big::EPI_ROWS, m0 + wm * 128 + ps * big::EPI_ROWS, n0 + wn * 32, n0 + 128 + wn * 32, batch,
-                  lane, csum);
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+      for (int j = 0; j < 4; ++j) keep += acc[i][j][0] + acc[i][j][3];
+    if (keep == 12345.f) *(float*)p.C = keep;
   }
+#undef EPI_COL0
+#undef EPI_COL1
   if (p.colsum) colsum_flush(p, csum, n0 + wn * 32, n0 + 128 + wn * 32, batch, lane);
 }
+#undef STE_EPI_PASS
 
 template <bool B_KC>
 int launch_8ph(const ste_gemm_args& a, hipStream_t s) {
   const int nb = ((a.M + 255) / 256) * ((a.N + 255) / 256) * a.batch;
-  hipLaunchKernelGGL((gemm_8ph_kernel<B_KC>), dim3(nb), dim3(ph8::NT), ph8::LDS_BYTES, s, a);
+  const char* e = getenv("STE_EPI_SKIP");  // experiment only: time the main loop without the epilogue
+  if (e && e[0] == '1') hipLaunchKernelGGL((gemm_8ph_kernel<B_KC, true>), dim3(nb), dim3(ph8::NT), ph8::LDS_BYTES, s, a);
+  else hipLaunchKernelGGL((gemm_8ph_kernel<B_KC, false>), dim3(nb), dim3(ph8::NT), ph8::LDS_BYTES, s, a);
   STE_CHECK_LAUNCH();
   return 0;
 }
@@ -720,6 +758,14 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
   if (a.a_kc ? (a.K & 7) || (a.lda & 7) : (a.M & 7) || (a.lda & 7)) return STE_ERR_SHAPE;
   if (a.b_kc ? (a.K & 7) || (a.ldb & 7) : (a.N & 7) || (a.ldb & 7)) return STE_ERR_SHAPE;
   if (a.drop_ld == 0) a.drop_ld = a.N;
+  // epilogue contract: 16-B aligned rows for every output / epilogue operand (8 columns per lane)
+  // (N < 8: every column goes through the element-wise tail path, any alignment works)
+  auto misaligned = [&a](const void* ptr, int64_t ld, int esz) {
+    return a.N >= 8 && ptr && ((((uintptr_t)ptr) & 15) || ((ld * esz) & 15));
+  };
+  if (misaligned(a.C, a.ldc, a.c_bf16 ? 2 : 4) || misaligned(a.C2, a.ldc2, 2) || misaligned(a.C3, a.ldc3, 2) ||
+      misaligned(a.R, a.ldr, a.r_bf16 ? 2 : 4) || misaligned(a.Z, a.ldz, 2) || misaligned(a.bias, 0, 4))
+    return STE_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   const int mode = gemm_mode();
   if (mode > 0 && big_ok(a)) {

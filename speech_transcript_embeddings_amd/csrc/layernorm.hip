@@ -1,8 +1,10 @@
 // LayerNorm forward/backward, one wavefront per row, fp32 statistics.
 // Replaces nn.LayerNorm in both encoders and the heads (see include/ste.h).
 // HBM-bound: forward reads x once and writes y once; backward reads dy, x once.
-// Rows are processed grid-stride so the dgamma/dbeta/dsum partials of a whole block
-// are reduced in LDS and flushed with one atomic per column per block.
+// Rows are processed grid-stride; launches put ~16 waves on every CU so enough row loads
+// are in flight to cover HBM latency.  When column sums are wanted (dgamma/dbeta/dsum of
+// a trainable layer) the partials of a block are reduced through one reused LDS array and
+// flushed with one atomic per column per block; frozen layers compile without that LDS.
 #include "common.h"
 #include "../../include/ste.h"
 
@@ -72,9 +74,9 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(ste_ln_fwd_args a) {
   }
 }
 
-template <int MAXC>
+template <int MAXC, bool REDUCE>
 __global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
-  __shared__ float red[3][NT / 64][MAXC * 4 * 64];
+  __shared__ float red[REDUCE ? NT / 64 : 1][REDUCE ? MAXC * 4 * 64 : 1];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wave = blockIdx.x * (NT / 64) + wid;
   const int nwaves = gridDim.x * (NT / 64);
@@ -145,32 +147,33 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
       }
     }
   }
-  if (!a.dgamma && !a.dbeta && !a.dsum) return;
+  if (!REDUCE) return;
+  // three column sums through one LDS array: [wave][c*256 + lane*4 + e] -> column (lane + c*64)*4 + e
+  float* const outs[3] = {a.dgamma, a.dbeta, a.dsum};
 #pragma unroll
-  for (int i = 0; i < MAXC * 4; ++i) {
-    const int j = (i >> 2) * 256 + lane * 4 + (i & 3);
-    red[0][wid][j] = dg[i];
-    red[1][wid][j] = db[i];
-    red[2][wid][j] = dsm[i];
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < MAXC * 256; j += NT) {
-    // j = c*256 + lane*4 + e  -> column (lane + c*64)*4 + e
-    const int c = j >> 8, rem = j & 255;
-    const int col = (c * 64 + (rem >> 2)) * 4 + (rem & 3);
-    if (col >= a.cols) continue;
-    float sg = 0.f, sb = 0.f, ss = 0.f;
+  for (int k = 0; k < 3; ++k) {
+    if (!outs[k]) continue;  // uniform
+    const float* src = k == 0 ? dg : (k == 1 ? db : dsm);
+    __syncthreads();
 #pragma unroll
-    for (int w = 0; w < NT / 64; ++w) { sg += red[0][w][j]; sb += red[1][w][j]; ss += red[2][w][j]; }
-    if (a.dgamma) atomicAdd(a.dgamma + col, sg);
-    if (a.dbeta) atomicAdd(a.dbeta + col, sb);
-    if (a.dsum) atomicAdd(a.dsum + col, ss);
+    for (int i = 0; i < MAXC * 4; ++i) red[wid][(i >> 2) * 256 + lane * 4 + (i & 3)] = src[i];
+    __syncthreads();
+    for (int j = threadIdx.x; j < MAXC * 256; j += NT) {
+      const int c = j >> 8, rem = j & 255;
+      const int col = (c * 64 + (rem >> 2)) * 4 + (rem & 3);
+      if (col >= a.cols) continue;
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < NT / 64; ++w) sum += red[w][j];
+      atomicAdd(outs[k] + col, sum);
+    }
   }
 }
 
-inline int grid_for(int rows) {
+// enough 4-wave blocks for ~16 waves per CU (256 CUs), never more than one wave per row
+inline int grid_for(int rows, int cap = 1024) {
   int g = (rows + 3) / 4;
-  return g < 1024 ? g : 1024;
+  return g < cap ? g : cap;
 }
 
 }  // namespace
@@ -191,10 +194,16 @@ extern "C" int ste_layernorm_bwd(const ste_ln_bwd_args* a, void* stream) {
   if (!a || a->rows <= 0 || a->cols <= 0 || (a->cols & 3) || a->cols > 1024) return STE_ERR_ARG;
   if (a->act == STE_ACT_SWISH && !a->beta) return STE_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  int g = (a->rows + 3) / 4;
-  if (g > 256) g = 256;
-  if (a->cols <= 256) hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(g), dim3(NT), 0, s, *a);
-  else hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(g), dim3(NT), 0, s, *a);
+  const bool reduce = a->dgamma || a->dbeta || a->dsum;
+  // column-sum launches pay one atomic per column per block: fewer, longer blocks
+  const dim3 grid(grid_for(a->rows, reduce ? 512 : 1024));
+  if (a->cols <= 256) {
+    if (reduce) hipLaunchKernelGGL((ln_bwd_kernel<1, true>), grid, dim3(NT), 0, s, *a);
+    else hipLaunchKernelGGL((ln_bwd_kernel<1, false>), grid, dim3(NT), 0, s, *a);
+  } else {
+    if (reduce) hipLaunchKernelGGL((ln_bwd_kernel<4, true>), grid, dim3(NT), 0, s, *a);
+    else hipLaunchKernelGGL((ln_bwd_kernel<4, false>), grid, dim3(NT), 0, s, *a);
+  }
   STE_CHECK_LAUNCH();
   return 0;
 }
