@@ -179,54 +179,76 @@ __global__ __launch_bounds__(NT) void xattn1_fwd_kernel(const float* q, const bf
 }
 
 // dk, dv are fp32 and ACCUMULATED (+=); dq is written.
+// One block per (batch, head): the heads are independent, so B*nh blocks fill the chip
+// (one block per batch row left most CUs idle and serialised S*P work per block).
+// Waves take key rows s = w, w+4, ...; lanes take the head's columns (coalesced rows).
 __global__ __launch_bounds__(NT) void xattn1_bwd_kernel(const float* q, const bf16* k, const bf16* v, int64_t ldkv,
                                                       const float* probs, const float* dout, int S, int P, int nh,
                                                       float scale, float drop_p, uint64_t seed, float* dq, float* dk,
                                                       float* dv, int64_t lddkv) {
-  extern __shared__ float sds[];  // nh * S : dp then ds
-  __shared__ float sq[1024], sdo[1024];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int dh = P / nh;
+  extern __shared__ float sds[];  // S: dp, then ds
+  __shared__ float sq[256], sdo[256], red[NT / 64][256];
+  const int b = blockIdx.x, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int dh = P / nh, c0 = hh * dh;
   const uint32_t thresh = (uint32_t)(drop_p * 4294967296.0);
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
-  for (int c = tid; c < P; c += NT) { sq[c] = q[(int64_t)b * P + c]; sdo[c] = dout[(int64_t)b * P + c]; }
+  const float* pr = probs + ((int64_t)b * nh + hh) * S;
+  const uint64_t drop_base = ((uint64_t)b * nh + hh) * S;
+  for (int c = tid; c < dh; c += NT) { sq[c] = q[(int64_t)b * P + c0 + c]; sdo[c] = dout[(int64_t)b * P + c0 + c]; }
   __syncthreads();
-  for (int i = tid; i < nh * S; i += NT) {
-    const int hh = i / S, s = i % S;
-    const bf16* vr = v + (int64_t)(b * S + s) * ldkv + hh * dh;
+  // dp[s] = v[s]·dout_h  (wave per row, lanes over columns)
+  for (int s = w; s < S; s += NT / 64) {
+    const bf16* vr = v + (int64_t)(b * S + s) * ldkv + c0;
     float acc = 0.f;
-    for (int d = 0; d < dh; d += 4) {
-      f32x4 x = load_bf16x4(vr + d);
-      acc += x[0] * sdo[hh * dh + d] + x[1] * sdo[hh * dh + d + 1] + x[2] * sdo[hh * dh + d + 2] + x[3] * sdo[hh * dh + d + 3];
-    }
-    if (drop_p > 0.f) acc *= drop_scale(seed, ((uint64_t)b * nh + hh) * S + s, thresh, inv_keep);
-    sds[i] = acc;  // dp (gradient wrt pre-dropout probability)
-  }
-  __syncthreads();
-  for (int hh = w; hh < nh; hh += NT / 64) {
-    const float* pr = probs + ((int64_t)b * nh + hh) * S;
-    float* row = sds + hh * S;
-    float acc = 0.f;
-    for (int s = lane; s < S; s += 64) acc += pr[s] * row[s];
+    for (int c = lane; c < dh; c += 64) acc += (float)vr[c] * sdo[c];
     acc = wave_sum(acc);
-    for (int s = lane; s < S; s += 64) row[s] = pr[s] * (row[s] - acc) * scale;
+    if (lane == 0) {
+      if (drop_p > 0.f) acc *= drop_scale(seed, drop_base + s, thresh, inv_keep);
+      sds[s] = acc;
+    }
   }
   __syncthreads();
-  // dq[c] = Σ_s ds[h][s] k[s][c]
-  for (int c = tid; c < P; c += NT) {
-    const int hh = c / dh;
-    float acc = 0.f;
-    for (int s = 0; s < S; ++s) acc += sds[hh * S + s] * (float)k[(int64_t)(b * S + s) * ldkv + c];
-    dq[(int64_t)b * P + c] = acc;
+  float part = 0.f;
+  for (int s = tid; s < S; s += NT) part += pr[s] * sds[s];
+  part = wave_sum(part);
+  if (lane == 0) red[w][0] = part;
+  __syncthreads();
+  float rowsum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) rowsum += red[i][0];
+  __syncthreads();
+  for (int s = tid; s < S; s += NT) sds[s] = pr[s] * (sds[s] - rowsum) * scale;
+  __syncthreads();
+  // dq[c] = Σ_s ds[s] k[s][c];  dk[s][c] += ds[s] q[c];  dv[s][c] += p'[s] dout[c]
+  float dqa[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int s = w; s < S; s += NT / 64) {
+    const float ds = sds[s];
+    float pd = pr[s];
+    if (drop_p > 0.f) pd *= drop_scale(seed, drop_base + s, thresh, inv_keep);
+    const bf16* kr = k + (int64_t)(b * S + s) * ldkv + c0;
+    float* dkr = dk + (int64_t)(b * S + s) * lddkv + c0;
+    float* dvr = dv + (int64_t)(b * S + s) * lddkv + c0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = lane + 64 * i;
+      if (c < dh) {
+        dqa[i] += ds * (float)kr[c];
+        dkr[c] += ds * sq[c];
+        dvr[c] += pd * sdo[c];
+      }
+    }
   }
-  // dk[s][c] += ds[h][s] q[c];  dv[s][c] += p'[h][s] dout[c]
-  for (int i = tid; i < S * P; i += NT) {
-    const int s = i / P, c = i % P, hh = c / dh;
-    const int64_t o = (int64_t)(b * S + s) * lddkv + c;
-    dk[o] += sds[hh * S + s] * sq[c];
-    float p = probs[((int64_t)b * nh + hh) * S + s];
-    if (drop_p > 0.f) p *= drop_scale(seed, ((uint64_t)b * nh + hh) * S + s, thresh, inv_keep);
-    dv[o] += p * sdo[c];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = lane + 64 * i;
+    if (c < dh) red[w][c] = dqa[i];
+  }
+  __syncthreads();
+  for (int c = tid; c < dh; c += NT) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) acc += red[i][c];
+    dq[(int64_t)b * P + c0 + c] = acc;
   }
 }
 
@@ -380,8 +402,9 @@ extern "C" int ste_xattn1_fwd(const float* q, const void* k, const void* v, int6
 extern "C" int ste_xattn1_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
                               const float* dout, int B, int S, int P, int nh, float scale, float drop_p, uint64_t seed,
                               float* dq, float* dk, float* dv, int64_t lddkv, void* stream) {
-  if (B <= 0 || S <= 0 || P > 1024 || P % nh || (P / nh) % 4 || nh * S > 16384 || lddkv < P) return STE_ERR_SHAPE;
-  hipLaunchKernelGGL(xattn1_bwd_kernel, dim3(B), dim3(NT), nh * S * sizeof(float), (hipStream_t)stream, q,
+  if (B <= 0 || S <= 0 || P > 1024 || P % nh || (P / nh) % 4 || P / nh > 256 || S > 16384 || lddkv < P)
+    return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(xattn1_bwd_kernel, dim3(B, nh), dim3(NT), S * sizeof(float), (hipStream_t)stream, q,
                      (const bf16*)k, (const bf16*)v, ldkv, probs, dout, S, P, nh, scale, drop_p, seed, dq, dk, dv,
                      lddkv);
   STE_CHECK_LAUNCH();
