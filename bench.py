@@ -108,7 +108,7 @@ def cpu_baseline(args):
 
 def hbm_traffic(kernel):
     """Per-launch HBM bytes of `kernel` from the latest committed PMC reduction
-    (profiles/rNN_hbm_traffic.json, made by profiles/pmc_traffic.py from separate rocprofv3
+    (profiles/rNN_hbm_traffic.json, made by profiles/rocpd_tools.py from separate rocprofv3
     FETCH_SIZE / WRITE_SIZE passes of this bench; gfx950 FETCH_SIZE x2 correction applied)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json")))

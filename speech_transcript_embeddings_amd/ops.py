@@ -90,7 +90,7 @@ def gemm_kernel_name(args: GemmArgs) -> str:
     v = k & 3
     a_kc, b_kc = ("false" if v & 2 else "true"), ("false" if v & 1 else "true")
     if k >= 8:
-        return f"gemm_8ph_kernel<{b_kc}>"
+        return f"gemm_8ph_kernel<{b_kc}, false>"
     return f"{'gemm_big_kernel' if k >= 4 else 'gemm_bf16_kernel'}<{a_kc}, {b_kc}>"
 
 
