@@ -45,6 +45,11 @@ extern "C" {
  * and ld%8==0; for N >= 8, C, C2, C3, R, Z and bias start 16-B aligned with
  * 16-B-multiple row strides (the epilogue moves 8 columns per lane).  Any N (ragged
  * last columns are handled element-wise).
+ * Weight gradients (a_kc=0, b_kc=0: dW = dYᵀ·X over K = batch·time rows, plain
+ * epilogue alpha/beta only): given a workspace ws (fp32, ws_bytes), a shape whose
+ * 256x256 tiles cannot fill the chip is split along K into S slabs
+ * (S·M·N·4 <= ws_bytes), each reduced by one 256x256 MFMA workgroup, then
+ * C = beta·C + alpha·Σ slabs.  ws may be NULL (no split).
  */
 enum {
   STE_ACT_NONE = 0,
@@ -74,6 +79,7 @@ typedef struct {
   float alpha, beta;
   int act;
   float drop_p; uint64_t seed; int64_t drop_ld;
+  float* ws; int64_t ws_bytes;      /* split-K workspace for weight gradients (optional) */
 } ste_gemm_args;
 
 int ste_gemm(const ste_gemm_args* args, void* stream);
@@ -84,6 +90,7 @@ int ste_gemm(const ste_gemm_args* args, void* stream);
 #define STE_GEMM_KERNEL_SMALL 0
 #define STE_GEMM_KERNEL_BIG 4
 #define STE_GEMM_KERNEL_8PH 8
+#define STE_GEMM_KERNEL_SPLITK 12
 int ste_gemm_kernel(const ste_gemm_args* args);
 
 /* ------------------------------------------------------------- LayerNorm --

@@ -44,6 +44,7 @@ class GemmArgs(C.Structure):
         ("alpha", c_float), ("beta", c_float),
         ("act", c_int),
         ("drop_p", c_float), ("seed", c_uint64), ("drop_ld", c_int64),
+        ("ws", c_void_p), ("ws_bytes", c_int64),
     ]
 
 

@@ -88,12 +88,12 @@ def align_backward(eng, d_align, hs, ctx, dth, dah):
     gB = s.g(PRE + "alignment_attention.in_proj_bias")
     dtp = ops.linear_dx(dq, W[:P], out_bf16=True)
     if gW is not None:
-        ops.linear_dw(dq, a["tp"], out=gW[:P], beta=1.0)
+        ops.linear_dw(dq, a["tp"], out=gW[:P], beta=1.0, ws=eng.ws)
         ops.colsum(dq, gB[:P])
     dkvb = ops.cast_bf16(dkv, eng._e(b * T, 2 * P, dtype=BF16))
     dap = ops.linear_dx(dkvb, W[P:], out_bf16=True)
     if gW is not None:
-        ops.linear_dw(dkvb, a["ap"], out=gW[P:], beta=1.0)
+        ops.linear_dw(dkvb, a["ap"], out=gW[P:], beta=1.0, ws=eng.ws)
         ops.colsum(dkv, gB[P:])
     ops.linear_dx(dtp, s.w(PRE + "text_projection.weight"), out=dth[: b * L], beta=1.0)
     eng._dw(dtp, ctx["_thb"][: b * L], PRE + "text_projection.weight")

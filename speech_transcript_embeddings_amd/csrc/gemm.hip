@@ -540,16 +540,23 @@ STE_DEV bf16x8 frag_b_8ph(const char* tile, int rb, int s, int lane) {
   if (B_KC) return frag_load<true, 256>(tile, rb, s, lane);
   return frag_load_km_asm(tile, rb, s, lane);
 }
+template <bool A_KC>
+STE_DEV bf16x8 frag_a_8ph(const char* tile, int rb, int s, int lane) {
+  if (A_KC) return frag_load<true, 256>(tile, rb, s, lane);
+  return frag_load_km_asm(tile, rb, s, lane);
+}
 // wait for this wave's LDS reads (incl. the asm ones) before the MFMA cluster
-#define STE_LDS_SYNC()                                  \
+#define STE_LDS_SYNC(ASM)                               \
   do {                                                  \
-    if (!B_KC) {                                        \
+    if (ASM) {                                          \
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
       __builtin_amdgcn_sched_barrier(0);                \
     }                                                   \
   } while (0)
 
-template <bool B_KC, bool EPI_SKIP>
+// A_KC=false (A k-major, the weight-gradient dYᵀ operand) stages A like a KM B operand and
+// reads it through ds_read_b64_tr_b16; everything else is shared.
+template <bool A_KC, bool B_KC, bool EPI_SKIP>
 __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
   using namespace ph8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -570,7 +577,7 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / 64;
-#define STAGE_A(t, h) stage_half<true, 64>(A, p.lda, m0, p.M, (t) * 64, h, smem + ((t) & 1) * BUF + (h) * HALF, wave, lane)
+#define STAGE_A(t, h) stage_half<A_KC, 64>(A, p.lda, m0, p.M, (t) * 64, h, smem + ((t) & 1) * BUF + (h) * HALF, wave, lane)
 #define STAGE_B(t, h) \
   stage_half<B_KC, 128>(B, p.ldb, n0, p.N, (t) * 64, h, smem + ((t) & 1) * BUF + (2 + (h)) * HALF, wave, lane)
   // prologue: tile 0 complete, tile 1's A0/B0 (the phases (-1,*) of the steady state)
@@ -601,11 +608,11 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) a0[i][s] = frag_load<true, 256>(buf, wm * 64 + i * 16, s, lane);
+      for (int s = 0; s < 2; ++s) a0[i][s] = frag_a_8ph<A_KC>(buf, wm * 64 + i * 16, s, lane);
     if (t + 1 < nk) STAGE_B(t + 1, 1);
     if (tail) STE_VMCNT(0); else STE_VMCNT(8);
     STE_BARRIER();
-    STE_LDS_SYNC();
+    STE_LDS_SYNC(!A_KC || !B_KC);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -623,7 +630,7 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
     if (t + 1 < nk) STAGE_A(t + 1, 1);
     if (tail) STE_VMCNT(0); else STE_VMCNT(8);
     STE_BARRIER();
-    STE_LDS_SYNC();
+    STE_LDS_SYNC(!B_KC);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -637,9 +644,10 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) a1[i][s] = frag_load<true, 256>(buf + HALF, wm * 64 + i * 16, s, lane);
+      for (int s = 0; s < 2; ++s) a1[i][s] = frag_a_8ph<A_KC>(buf + HALF, wm * 64 + i * 16, s, lane);
     if (t + 2 < nk) STAGE_A(t + 2, 0);
     STE_BARRIER();
+    STE_LDS_SYNC(!A_KC);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -688,14 +696,58 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
 }
 #undef STE_EPI_PASS
 
-template <bool B_KC>
+template <bool A_KC, bool B_KC>
 int launch_8ph(const ste_gemm_args& a, hipStream_t s) {
   const int nb = ((a.M + 255) / 256) * ((a.N + 255) / 256) * a.batch;
   const char* e = getenv("STE_EPI_SKIP");  // experiment only: time the main loop without the epilogue
-  if (e && e[0] == '1') hipLaunchKernelGGL((gemm_8ph_kernel<B_KC, true>), dim3(nb), dim3(ph8::NT), ph8::LDS_BYTES, s, a);
-  else hipLaunchKernelGGL((gemm_8ph_kernel<B_KC, false>), dim3(nb), dim3(ph8::NT), ph8::LDS_BYTES, s, a);
+  if (e && e[0] == '1')
+    hipLaunchKernelGGL((gemm_8ph_kernel<A_KC, B_KC, true>), dim3(nb), dim3(ph8::NT), ph8::LDS_BYTES, s, a);
+  else
+    hipLaunchKernelGGL((gemm_8ph_kernel<A_KC, B_KC, false>), dim3(nb), dim3(ph8::NT), ph8::LDS_BYTES, s, a);
   STE_CHECK_LAUNCH();
   return 0;
+}
+
+// C = beta*C + alpha*sum_s ws[s]  (fp32 [M,N] slabs, 4 columns per thread)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ C, int64_t ldc,
+                                                            const float* __restrict__ ws, int M, int N, int S,
+                                                            float alpha, float beta) {
+  const int n4 = N >> 2;
+  const int64_t total = (int64_t)M * n4;
+  const int64_t slab = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / n4), c = (int)(i - (int64_t)m * n4) * 4;
+    const float* w = ws + (int64_t)m * N + c;
+    f32x4 acc = *reinterpret_cast<const f32x4*>(w);
+    for (int k = 1; k < S; ++k) acc += *reinterpret_cast<const f32x4*>(w + k * slab);
+    float* cp = C + (int64_t)m * ldc + c;
+    f32x4 v = acc * alpha;
+    if (beta != 0.f) v += *reinterpret_cast<const f32x4*>(cp) * beta;
+    *reinterpret_cast<f32x4*>(cp) = v;
+  }
+}
+
+// Weight-gradient plan: S K-slabs of Kc 64-deep tiles each on the 8-phase kernel with both
+// operands k-major; the K remainder (< S tiles + a ragged tail) goes to the small kernel.
+struct SplitPlan {
+  int S, Kc;  // S == 0: not applicable
+};
+SplitPlan splitk_plan(const ste_gemm_args& a) {
+  SplitPlan pl{0, 0};
+  if (a.a_kc || a.b_kc || !a.ws || a.batch != 1) return pl;
+  if (a.bias || a.C2 || a.C3 || a.R || a.Z || a.colsum || a.row_scale || a.act || a.drop_p > 0.f || a.c_bf16) return pl;
+  if ((a.M & 7) || (a.N & 7)) return pl;
+  const int nk = a.K / 64;
+  const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  if (nk < 16 || tiles > 256) return pl;
+  int S = 256 / tiles;
+  if (S > nk / 8) S = nk / 8;
+  const int64_t slab = (int64_t)a.M * a.N * 4;
+  while (S > 1 && S * slab > a.ws_bytes) --S;
+  if (S < 1 || S * slab > a.ws_bytes) return pl;
+  pl.S = S;
+  pl.Kc = nk / S;
+  return pl;
 }
 
 template <bool A_KC, bool B_KC>
@@ -745,6 +797,7 @@ extern "C" int ste_gemm_kernel(const ste_gemm_args* args) {
   ste_gemm_args a = *args;
   if (a.batch <= 0) a.batch = 1;
   const int variant = (a.a_kc ? 0 : 2) + (a.b_kc ? 0 : 1);
+  if (gemm_mode() == 2 && splitk_plan(a).S > 0) return STE_GEMM_KERNEL_SPLITK + variant;
   if (gemm_mode() > 0 && big_ok(a)) return (gemm_mode() == 2 ? STE_GEMM_KERNEL_8PH : STE_GEMM_KERNEL_BIG) + variant;
   return STE_GEMM_KERNEL_SMALL + variant;
 }
@@ -768,8 +821,38 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
     return STE_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   const int mode = gemm_mode();
+  if (mode == 2) {
+    const SplitPlan pl = splitk_plan(a);
+    if (pl.S > 0) {
+      ste_gemm_args g = a;
+      const int64_t kc = (int64_t)pl.Kc * 64;
+      g.K = (int)kc;
+      g.batch = pl.S;
+      g.strideA = kc * a.lda;
+      g.strideB = kc * a.ldb;
+      g.C = a.ws; g.ldc = a.N; g.strideC = (int64_t)a.M * a.N; g.c_bf16 = 0;
+      g.alpha = 1.f; g.beta = 0.f;
+      if (int e = launch_8ph<false, false>(g, s)) return e;
+      const int64_t work = (int64_t)a.M * (a.N / 4);
+      const int blocks = (int)((work + 255) / 256 < 2048 ? (work + 255) / 256 : 2048);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, (float*)a.C, a.ldc, a.ws, a.M, a.N,
+                         pl.S, a.alpha, a.beta);
+      STE_CHECK_LAUNCH();
+      const int64_t kdone = kc * pl.S;
+      if (kdone < a.K) {  // remainder rows: accumulate on the small kernel
+        ste_gemm_args r = a;
+        r.K = (int)(a.K - kdone);
+        r.A = (const bf16*)a.A + kdone * a.lda;
+        r.B = (const bf16*)a.B + kdone * a.ldb;
+        r.beta = 1.f;
+        r.ws = nullptr;
+        return launch_small<false, false>(r, s);
+      }
+      return 0;
+    }
+  }
   if (mode > 0 && big_ok(a)) {
-    if (mode == 2) return a.b_kc ? launch_8ph<true>(a, s) : launch_8ph<false>(a, s);
+    if (mode == 2) return a.b_kc ? launch_8ph<true, true>(a, s) : launch_8ph<true, false>(a, s);
     if (a.b_kc) return launch_big<true, true>(a, s);
     return launch_big<true, false>(a, s);
   }

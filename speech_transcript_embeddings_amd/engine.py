@@ -47,6 +47,15 @@ class Engine:
         self.s = model.store
         self.acfg = model.audio_cfg
         self.tcfg = model.text_cfg
+        self._ws = None
+
+    WS_BYTES = 80 << 20   # split-K slabs of the weight-gradient GEMMs (largest: 7 x 3072 x 768 fp32)
+
+    @property
+    def ws(self):
+        if self._ws is None:
+            self._ws = torch.empty(self.WS_BYTES // 4, device=self.s.device, dtype=F32)
+        return self._ws
 
     # ------------------------------------------------------------- helpers
     def _e(self, *shape, dtype=F32):
@@ -61,7 +70,7 @@ class Engine:
         if g is None:
             return
         g2 = g.view(g.shape[0], -1)
-        ops.linear_dw(dy_b, x_b, out=g2, beta=1.0)
+        ops.linear_dw(dy_b, x_b, out=g2, beta=1.0, ws=self.ws)
 
     def _db(self, x, bname, fused=1):
         g = self.s.fused(bname, fused, "g") if fused > 1 else self.s.g(bname)

@@ -31,7 +31,7 @@ def _ld(t: torch.Tensor) -> int:
 def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf16=False, bias=None,
          act=_lib.ACT_NONE, pre_out=None, z=None, residual=None, alpha=1.0, beta=0.0, colsum=None,
          row_scale=None, drop_p=0.0, seed=0, out_bf16_copy=None, batch=1, stride_a=0, stride_b=0, stride_c=0,
-         stride_r=0, drop_ld=0):
+         stride_r=0, drop_ld=0, ws=None):
     """out[M,N] = epilogue(alpha * A·B).  See include/ste.h for the epilogue order.
 
     a_kc: A is [M,K] row-major (else [K,M]);  b_kc: B is [N,K] row-major (else [K,N]).
@@ -69,6 +69,9 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
         args.row_scale = ptr(row_scale)
     args.alpha, args.beta, args.act = float(alpha), float(beta), int(act)
     args.drop_p, args.seed, args.drop_ld = float(drop_p), int(seed) & (2**64 - 1), int(drop_ld)
+    if ws is not None:  # split-K workspace (weight gradients), see include/ste.h
+        assert ws.dtype == F32 and ws.is_contiguous()
+        args.ws, args.ws_bytes = ptr(ws), ws.numel() * 4
     if GEMM_TRACE is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -89,8 +92,8 @@ def gemm_kernel_name(args: GemmArgs) -> str:
     k = int(fn("ste_gemm_kernel")(C.byref(args)))
     v = k & 3
     a_kc, b_kc = ("false" if v & 2 else "true"), ("false" if v & 1 else "true")
-    if k >= 8:
-        return f"gemm_8ph_kernel<{b_kc}, false>"
+    if k >= 8:  # 8-phase (k >= 12: split-K weight gradient, reported under the same kernel symbol)
+        return f"gemm_8ph_kernel<{a_kc}, {b_kc}, false>"
     return f"{'gemm_big_kernel' if k >= 4 else 'gemm_bf16_kernel'}<{a_kc}, {b_kc}>"
 
 

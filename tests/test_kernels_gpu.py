@@ -40,6 +40,29 @@ def test_gemm_layouts(ops, M, N, K):
     assert rel_err(ops.linear_dw(dy, x), dy.float().t() @ x.float()) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K,ws_mb", [(4096, 1024, 31936, 80),   # c2 FFN intermediate dW: S=4, K tail 3 tiles
+                                         (1024, 1024, 15968, 80),   # c3 (b=32) O-proj dW: S=16, ragged 32-row tail
+                                         (3072, 768, 8192, 80),     # text QKV dW over 2bL rows
+                                         (1032, 520, 4160, 8),      # ragged M/N tiles; workspace caps S at 3
+                                         (2048, 1024, 960, 80)])    # K < 16 tiles: no split
+def test_gemm_dw_splitk(ops, M, N, K, ws_mb):
+    """Weight gradient dW += dYᵀ·X (both operands k-major) through the split-K 8-phase path."""
+    from speech_transcript_embeddings_amd import _lib
+    torch.manual_seed(K)
+    dy = torch.randn(K, M, device=DEV).bfloat16()
+    x = torch.randn(K, N, device=DEV).bfloat16()
+    ws = torch.empty(ws_mb << 18, device=DEV)
+    g = torch.randn(M, N, device=DEV)
+    ref = dy.float().t() @ x.float() * 0.5 + g
+    out = g.clone()
+    ops.linear_dw(dy, x, out=out, beta=1.0, alpha=0.5, ws=ws)
+    assert rel_err(out, ref) < 1e-5
+    args = _lib.GemmArgs(M=M, N=N, K=K, batch=1, a_kc=0, b_kc=0, A=1, B=1, C=1, ldc=N, lda=M, ldb=N, alpha=1.0,
+                         ws=1, ws_bytes=ws.numel() * 4)
+    kern = int(_lib.fn("ste_gemm_kernel")(__import__("ctypes").byref(args)))
+    assert (kern >= 12) == (K >= 16 * 64), kern
+
+
 def test_gemm_epilogues(ops):
     from speech_transcript_embeddings_amd import _lib
     torch.manual_seed(1)
