@@ -92,6 +92,9 @@ int ste_gemm(const ste_gemm_args* args, void* stream);
 #define STE_GEMM_KERNEL_8PH 8
 #define STE_GEMM_KERNEL_SPLITK 12
 int ste_gemm_kernel(const ste_gemm_args* args);
+/* The rocprofv3 kernel name (template arguments included) of that launch, NUL-terminated
+ * into buf[len]; bench.py keys its HIP-event timings and PMC traffic by it. */
+int ste_gemm_kernel_name(const ste_gemm_args* args, char* buf, int len);
 
 /* ------------------------------------------------------------- LayerNorm --
  * Replaces nn.LayerNorm forward/backward (every LN of both encoders and the

@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 _PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("STE_LIB", _PKG / "libste.so"))
 
-c_void_p, c_int, c_int64, c_float, c_uint64 = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_uint64
+c_void_p, c_int, c_int64, c_float, c_uint64, c_char_p = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_uint64, C.c_char_p
 c_i32p = C.POINTER(C.c_int32)
 
 ACT_NONE, ACT_SWISH, ACT_GELU, ACT_TANH, ACT_RELU = 0, 1, 2, 3, 4
@@ -108,6 +108,7 @@ class AttnArgs(C.Structure):
 _SIGS = {
     "ste_gemm": (c_int, [C.POINTER(GemmArgs), c_void_p]),
     "ste_gemm_kernel": (c_int, [C.POINTER(GemmArgs)]),
+    "ste_gemm_kernel_name": (c_int, [C.POINTER(GemmArgs), c_char_p, c_int]),
     "ste_layernorm_fwd": (c_int, [C.POINTER(LnFwdArgs), c_void_p]),
     "ste_layernorm_bwd": (c_int, [C.POINTER(LnBwdArgs), c_void_p]),
     "ste_attention_fwd": (c_int, [C.POINTER(AttnArgs), c_void_p]),

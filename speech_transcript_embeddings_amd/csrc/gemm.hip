@@ -24,6 +24,7 @@
 //    tails in every dimension): small / ragged GEMMs and the dW reductions.
 // Both: XCD-aware bijective block remap + grouped tile order for L2 reuse, and an
 // LDS-staged epilogue with row-contiguous (16 B/lane) loads and stores.
+#include <cstdio>
 #include "common.h"
 #include "../../include/ste.h"
 
@@ -184,9 +185,166 @@ STE_DEV void colsum_flush(const ste_gemm_args& p, Csum csum, int col0, int col1,
   }
 }
 
+// ---------------------------------------------------- specialised epilogue (8-phase)
+// The feature set of a launch is a compile-time bitmask for the hot configurations, so a
+// pass carries no per-element runtime switches, and every global load of a pass (Z, R,
+// beta*C) is issued before any of its stores: the compiler's waits then never serialise
+// a row behind the previous row's stores.  EF_GENERIC keeps every feature runtime.
+enum : int {
+  EF_BIAS = 1, EF_C2 = 2, EF_Z = 4, EF_DROP = 8, EF_RS = 16, EF_COLSUM = 32, EF_R = 64, EF_RBF16 = 128,
+  EF_BETA = 256, EF_CBF16 = 512, EF_C3 = 1024, EF_GENERIC = -1
+};
+
+int epi_flags(const ste_gemm_args& a) {
+  int f = 0;
+  const bool fwd_act = a.act >= STE_ACT_SWISH && a.act <= STE_ACT_RELU;
+  const bool bwd_act = a.act >= STE_ACT_SWISH_BWD;
+  if (a.bias) f |= EF_BIAS;
+  if (a.C2 && fwd_act) f |= EF_C2;
+  if (bwd_act) f |= EF_Z;
+  if (a.drop_p > 0.f) f |= EF_DROP;
+  if (a.row_scale) f |= EF_RS;
+  if (a.colsum) f |= EF_COLSUM;
+  if (a.R) f |= EF_R | (a.r_bf16 ? EF_RBF16 : 0);
+  if (a.beta != 0.f) f |= EF_BETA;
+  if (a.c_bf16) f |= EF_CBF16;
+  if (a.C3) f |= EF_C3;
+  return f;
+}
+
+STE_DEV f32x8 act8(f32x8 v, int act) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float x = v[e];
+    if (act == STE_ACT_SWISH) v[e] = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+    else if (act == STE_ACT_GELU) v[e] = gelu_f(x);
+    else if (act == STE_ACT_TANH) v[e] = tanhf(x);
+    else if (act == STE_ACT_RELU) v[e] = fmaxf(x, 0.f);
+  }
+  return v;
+}
+STE_DEV f32x8 actd8(f32x8 z, int act) {
+  f32x8 g;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float x = z[e];
+    if (act == STE_ACT_SWISH_BWD) {
+      const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+      g[e] = sg * (1.0f + x * (1.0f - sg));
+    } else if (act == STE_ACT_GELU_BWD) g[e] = gelu_d(x);
+    else if (act == STE_ACT_TANH_BWD_OUT) g[e] = 1.0f - x * x;
+    else if (act == STE_ACT_RELU_BWD) g[e] = x > 0.f ? 1.f : 0.f;
+    else g[e] = 1.f;
+  }
+  return g;
+}
+
+// One 32-row pass of a wave: staged fp32 [32 x 64] at `epi` (row stride EPI_LD); staged
+// columns 0..31 -> col0.., 32..63 -> col1...  Lane: 8 columns x rows lr, lr+8, lr+16, lr+24.
+// FULL: every row < M and every column < N (no bounds work at all).
+// epi_load32 issues the pass's global loads (Z, R, beta*C) one pass AHEAD (before the
+// previous pass's stores), so waiting for them never waits for in-flight stores.
+struct EpiFlags {
+  int act;
+  bool fwd_act, f_c2, f_z, f_drop, f_rs, f_cs, f_r, r_bf, f_beta, c_bf, f_c3;
+};
+template <int EF, int ACT>
+STE_DEV EpiFlags epi_flags_dev(const ste_gemm_args& p) {
+  constexpr int F = EF < 0 ? 0 : EF;
+  EpiFlags f;
+  f.act = ACT;
+  f.fwd_act = ACT >= STE_ACT_SWISH && ACT <= STE_ACT_RELU;
+  f.f_c2 = (F & EF_C2) != 0;
+  f.f_z = (F & EF_Z) != 0;
+  f.f_drop = (F & EF_DROP) != 0;
+  f.f_rs = (F & EF_RS) != 0;
+  f.f_cs = (F & EF_COLSUM) != 0;
+  f.f_r = (F & EF_R) != 0;
+  f.r_bf = (F & EF_RBF16) != 0;
+  f.f_beta = (F & EF_BETA) != 0;
+  f.c_bf = (F & EF_CBF16) != 0;
+  f.f_c3 = (F & EF_C3) != 0;
+  return f;
+}
+struct EpiLoads {
+  f32x8 z[4], r[4], c[4];
+};
+
+template <int EF, int ACT, bool FULL>
+STE_DEV void epi_load32(const ste_gemm_args& p, int row0, int col0, int col1, int batch, int lane, EpiLoads& L) {
+  const EpiFlags f = epi_flags_dev<EF, ACT>(p);
+  const int cl = (lane & 7) * 8;
+  const int col = cl < 32 ? col0 + cl : col1 + (cl - 32);
+  const int nval = FULL ? 8 : p.N - col;
+  const bool full = FULL || nval >= 8;
+  const int lr = lane >> 3;
+  const int64_t offC = (int64_t)batch * p.strideC;
+  const int64_t offR = (int64_t)batch * p.strideR;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t row = row0 + lr + 8 * k;
+    L.z[k] = f32x8{};
+    L.r[k] = f32x8{};
+    L.c[k] = f32x8{};
+    if (!FULL && (nval <= 0 || row >= p.M)) continue;
+    if (f.f_z) L.z[k] = ld8((const bf16*)p.Z + offC + row * p.ldz + col, true, full, nval);
+    if (f.f_r) L.r[k] = ld8((const char*)p.R + (offR + row * p.ldr + col) * (f.r_bf ? 2 : 4), f.r_bf, full, nval);
+    if (f.f_beta)
+      L.c[k] = ld8((const char*)p.C + (offC + row * p.ldc + col) * (f.c_bf ? 2 : 4), f.c_bf, full, nval);
+  }
+}
+
+template <int EF, int ACT, bool FULL>
+STE_DEV void epi_store32(const ste_gemm_args& p, const float* epi, int row0, int col0, int col1, int batch,
+                         int lane, f32x8 bias, const EpiLoads& L, Csum& csum) {
+  const EpiFlags f = epi_flags_dev<EF, ACT>(p);
+  const int cl = (lane & 7) * 8;
+  const int col = cl < 32 ? col0 + cl : col1 + (cl - 32);
+  const int nval = FULL ? 8 : p.N - col;
+  if (!FULL && nval <= 0) return;
+  const bool full = FULL || nval >= 8;
+  const int lr = lane >> 3;
+  const int64_t offC = (int64_t)batch * p.strideC;
+  f32x8 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float* src = epi + (lr + 8 * k) * EPI_LD + cl;
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(src), s1 = *reinterpret_cast<const f32x4*>(src + 4);
+    v[k] = f32x8{s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+  }
+  const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
+  const float inv_keep = f.f_drop ? 1.0f / (1.0f - p.drop_p) : 1.0f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t row = row0 + lr + 8 * k;
+    if (!FULL && row >= p.M) continue;
+    f32x8 x = (v[k] + bias) * p.alpha;
+    if (f.f_c2) st8((bf16*)p.C2 + offC + row * p.ldc2 + col, true, x, full, nval);
+    if (f.fwd_act) x = act8(x, f.act);
+    if (f.f_z) x = x * actd8(L.z[k], f.act);
+    if (f.f_drop) {
+      const uint64_t base = (uint64_t)row * (uint64_t)p.drop_ld + (uint64_t)col;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] *= drop_scale(p.seed, base + e, thresh, inv_keep);
+    }
+    if (f.f_rs) x = x * p.row_scale[row];
+    if (!full) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) if (e >= nval) x[e] = 0.f;
+    }
+    if (f.f_cs) {
+      csum.lo += f32x4{x[0], x[1], x[2], x[3]};
+      csum.hi += f32x4{x[4], x[5], x[6], x[7]};
+    }
+    if (f.f_r) x += L.r[k];
+    if (f.f_beta) x += L.c[k] * p.beta;
+    st8((char*)p.C + (offC + row * p.ldc + col) * (f.c_bf ? 2 : 4), f.c_bf, x, full, nval);
+    if (f.f_c3) st8((bf16*)p.C3 + offC + row * p.ldc3 + col, true, x, full, nval);
+  }
+}
+
 // block id -> (batch, tile_m, tile_n): bijective XCD remap, then groups of 8 m-tiles
-STE_DEV void map_tile(int nwg, int num_m, int num_n, int& batch, int& tm, int& tn) {
-  const int bid = xcd_remap(blockIdx.x, nwg);
+STE_DEV void map_tile_bid(int bid, int num_m, int num_n, int& batch, int& tm, int& tn) {
   const int tiles = num_m * num_n;
   batch = bid / tiles;
   int t = bid - batch * tiles;
@@ -196,6 +354,9 @@ STE_DEV void map_tile(int nwg, int num_m, int num_n, int& batch, int& tm, int& t
   int gsize = min(num_m - first_m, GROUP);
   tm = first_m + (t % (GROUP * num_n)) % gsize;
   tn = (t % (GROUP * num_n)) / gsize;
+}
+STE_DEV void map_tile(int nwg, int num_m, int num_n, int& batch, int& tm, int& tn) {
+  map_tile_bid(xcd_remap(blockIdx.x, nwg), num_m, num_n, batch, tm, tn);
 }
 
 // =========================================================== small/ragged kernel
@@ -556,7 +717,12 @@ STE_DEV bf16x8 frag_a_8ph(const char* tile, int rb, int s, int lane) {
 
 // A_KC=false (A k-major, the weight-gradient dYᵀ operand) stages A like a KM B operand and
 // reads it through ds_read_b64_tr_b16; everything else is shared.
-template <bool A_KC, bool B_KC, bool EPI_SKIP>
+//
+// Persistent: a grid of min(tiles, CUs) workgroups loops over virtual tiles
+// vb = blockIdx.x, +gridDim.x, ... (same XCD-aware order as one tile per workgroup), so the
+// next tile's operand stream starts right behind this tile's epilogue instead of behind a
+// new workgroup's dispatch.  EF/ACT: compile-time epilogue (epi_pass32).
+template <bool A_KC, bool B_KC, int EF, int ACT>
 __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
   using namespace ph8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -564,8 +730,10 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int num_m = (p.M + 255) / 256, num_n = (p.N + 255) / 256;
+  const int total = num_m * num_n * p.batch;
+  for (int vb = blockIdx.x; vb < total; vb += gridDim.x) {
   int batch, tm, tn;
-  map_tile(gridDim.x, num_m, num_n, batch, tm, tn);
+  map_tile_bid(xcd_remap(vb, total), num_m, num_n, batch, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
   const bf16* A = (const bf16*)p.A + (int64_t)batch * p.strideA;
   const bf16* B = (const bf16*)p.B + (int64_t)batch * p.strideB;
@@ -676,34 +844,115 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
 #undef STE_LDS_SYNC
   if (wm == 0) STE_BARRIER();  // re-align the groups (equal barrier counts) before the LDS epilogue
 
-  // epilogue: acc[i][j] = rows wm*128 + i*16, cols (j >> 1)*128 + wn*32 + (j & 1)*16
+  // epilogue: acc[i][j] = rows wm*128 + i*16, cols (j >> 1)*128 + wn*32 + (j & 1)*16;
+  // 4 passes of 32 rows x 64 columns per wave through LDS
   float* epi = reinterpret_cast<float*>(smem) + wave * big::EPI_ROWS * EPI_LD;
   Csum csum = {};
-#define EPI_COL0 (n0 + wn * 32)
-#define EPI_COL1 (n0 + 128 + wn * 32)
-  STE_EPI_PASS(0) STE_EPI_PASS(1) STE_EPI_PASS(2) STE_EPI_PASS(3)
-  if (EPI_SKIP) {
-    float keep = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) keep += acc[i][j][0] + acc[i][j][3];
-    if (keep == 12345.f) *(float*)p.C = keep;
+  const bool full_tile = m0 + 256 <= p.M && n0 + 256 <= p.N;
+  f32x8 bias = f32x8{};
+  if (EF >= 0 && (EF & EF_BIAS) != 0) {
+    const int cl = (lane & 7) * 8;
+    const int col = cl < 32 ? n0 + wn * 32 + cl : n0 + 128 + wn * 32 + (cl - 32);
+    const int nval = p.N - col;
+    if (nval > 0) bias = ld8(p.bias + col, false, nval >= 8, nval);
   }
-#undef EPI_COL0
-#undef EPI_COL1
-  if (p.colsum) colsum_flush(p, csum, n0 + wn * 32, n0 + 128 + wn * 32, batch, lane);
+#define STE_EPI_STAGE(PS)                                                                                   \
+  {                                                                                                          \
+    for (int ii = 0; ii < 2; ++ii) {                                                                         \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                                        \
+        _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                                      \
+          epi[(ii * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[2 * (PS) + ii][j][r];   \
+        }                                                                                                    \
+      }                                                                                                      \
+    }                                                                                                        \
+    __builtin_amdgcn_s_waitcnt(0xc07f);                                                                      \
+    __builtin_amdgcn_wave_barrier();                                                                         \
+  }
+#define STE_EPI_ROW0(PS) (m0 + wm * 128 + (PS) * 32)
+#define STE_EPI_LOAD(PS, L)                                                                                  \
+  if (full_tile) epi_load32<EF, ACT, true>(p, STE_EPI_ROW0(PS), c0, c1, batch, lane, L);                     \
+  else epi_load32<EF, ACT, false>(p, STE_EPI_ROW0(PS), c0, c1, batch, lane, L);
+#define STE_EPI_STORE(PS, L)                                                                                 \
+  if (full_tile) epi_store32<EF, ACT, true>(p, epi, STE_EPI_ROW0(PS), c0, c1, batch, lane, bias, L, csum);  \
+  else epi_store32<EF, ACT, false>(p, epi, STE_EPI_ROW0(PS), c0, c1, batch, lane, bias, L, csum);           \
+  __builtin_amdgcn_s_waitcnt(0xc07f);                                                                        \
+  __builtin_amdgcn_wave_barrier();
+  const int c0 = n0 + wn * 32, c1 = n0 + 128 + wn * 32;
+  if constexpr (EF < 0) {
+#define STE_EPI_G(PS)                                                                                        \
+    STE_EPI_STAGE(PS)                                                                                        \
+    epilogue_tile(p, epi, 32, STE_EPI_ROW0(PS), c0, c1, batch, lane, csum);                                  \
+    __builtin_amdgcn_s_waitcnt(0xc07f);                                                                      \
+    __builtin_amdgcn_wave_barrier();
+    STE_EPI_G(0) STE_EPI_G(1) STE_EPI_G(2) STE_EPI_G(3)
+#undef STE_EPI_G
+  } else {
+    EpiLoads L0, L1;
+    STE_EPI_LOAD(0, L0)
+    STE_EPI_STAGE(0) STE_EPI_LOAD(1, L1) STE_EPI_STORE(0, L0)
+    STE_EPI_STAGE(1) STE_EPI_LOAD(2, L0) STE_EPI_STORE(1, L1)
+    STE_EPI_STAGE(2) STE_EPI_LOAD(3, L1) STE_EPI_STORE(2, L0)
+    STE_EPI_STAGE(3) STE_EPI_STORE(3, L1)
+  }
+#undef STE_EPI_STAGE
+#undef STE_EPI_ROW0
+#undef STE_EPI_LOAD
+#undef STE_EPI_STORE
+  if (EF < 0 ? p.colsum != nullptr : (EF & EF_COLSUM) != 0)
+    colsum_flush(p, csum, n0 + wn * 32, n0 + 128 + wn * 32, batch, lane);
+  // every wave's epilogue LDS reads are done (lgkmcnt(0) above) before the next tile's
+  // prologue restages the ring over the staging area
+  STE_BARRIER();
+  }
 }
 #undef STE_EPI_PASS
+
+// CUs of the current device (one persistent workgroup each)
+int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0, v = 0;
+    n = (hipGetDevice(&dev) == hipSuccess &&
+         hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+  }
+  return n;
+}
+
+// (A_KC, B_KC, epilogue flags, activation) instantiated with a compile-time epilogue; every
+// other combination runs the EF_GENERIC instantiation of the same kernel.
+#define STE_EPI_SPECS(X)                                                              \
+  X(true, true, EF_BIAS | EF_C2 | EF_CBF16, STE_ACT_SWISH)   /* FFN intermediate   */ \
+  X(true, true, EF_BIAS | EF_C2 | EF_CBF16, STE_ACT_GELU)    /* XLM-R intermediate */ \
+  X(true, true, EF_BIAS | EF_R, STE_ACT_NONE)                /* FFN out, O-proj    */ \
+  X(true, true, EF_BIAS | EF_CBF16, STE_ACT_NONE)            /* QKV                */ \
+  X(true, true, EF_CBF16, STE_ACT_NONE)                      /* pointwise conv 1   */ \
+  X(true, true, EF_R | EF_DROP, STE_ACT_NONE)                /* pointwise conv 2   */ \
+  X(true, true, EF_R, STE_ACT_NONE)                                                   \
+  X(true, false, EF_CBF16, STE_ACT_NONE)                     /* dX, bf16 out       */ \
+  X(true, false, 0, STE_ACT_NONE)                            /* dX, fp32 out       */ \
+  X(true, false, EF_Z | EF_COLSUM | EF_CBF16, STE_ACT_SWISH_BWD)                      \
+  X(true, false, EF_Z | EF_COLSUM | EF_CBF16, STE_ACT_GELU_BWD)                       \
+  X(true, false, EF_Z | EF_CBF16, STE_ACT_SWISH_BWD)         /* frozen layer: no db */ \
+  X(true, false, EF_Z | EF_CBF16, STE_ACT_GELU_BWD)                                   \
+  X(false, false, 0, STE_ACT_NONE)                           /* dW split-K slabs   */
 
 template <bool A_KC, bool B_KC>
 int launch_8ph(const ste_gemm_args& a, hipStream_t s) {
   const int nb = ((a.M + 255) / 256) * ((a.N + 255) / 256) * a.batch;
-  const char* e = getenv("STE_EPI_SKIP");  // experiment only: time the main loop without the epilogue
-  if (e && e[0] == '1')
-    hipLaunchKernelGGL((gemm_8ph_kernel<A_KC, B_KC, true>), dim3(nb), dim3(ph8::NT), ph8::LDS_BYTES, s, a);
-  else
-    hipLaunchKernelGGL((gemm_8ph_kernel<A_KC, B_KC, false>), dim3(nb), dim3(ph8::NT), ph8::LDS_BYTES, s, a);
+  const int grid = nb < num_cus() ? nb : num_cus();
+  const int ef = epi_flags(a);
+#define STE_TRY(AK, BK, E, ACT)                                                                       \
+  if constexpr (AK == A_KC && BK == B_KC) {                                                           \
+    if (ef == (E) && a.act == (ACT)) {                                                                \
+      hipLaunchKernelGGL((gemm_8ph_kernel<A_KC, B_KC, (E), (ACT)>), dim3(grid), dim3(ph8::NT),        \
+                         ph8::LDS_BYTES, s, a);                                                       \
+      STE_CHECK_LAUNCH();                                                                             \
+      return 0;                                                                                       \
+    }                                                                                                 \
+  }
+  STE_EPI_SPECS(STE_TRY)
+#undef STE_TRY
+  hipLaunchKernelGGL((gemm_8ph_kernel<A_KC, B_KC, EF_GENERIC, 0>), dim3(grid), dim3(ph8::NT), ph8::LDS_BYTES, s, a);
   STE_CHECK_LAUNCH();
   return 0;
 }
@@ -800,6 +1049,32 @@ extern "C" int ste_gemm_kernel(const ste_gemm_args* args) {
   if (gemm_mode() == 2 && splitk_plan(a).S > 0) return STE_GEMM_KERNEL_SPLITK + variant;
   if (gemm_mode() > 0 && big_ok(a)) return (gemm_mode() == 2 ? STE_GEMM_KERNEL_8PH : STE_GEMM_KERNEL_BIG) + variant;
   return STE_GEMM_KERNEL_SMALL + variant;
+}
+
+// rocprofv3's (demangled, namespace-stripped) name of the kernel ste_gemm would launch
+extern "C" int ste_gemm_kernel_name(const ste_gemm_args* args, char* buf, int len) {
+  if (!args || !buf || len <= 0) return STE_ERR_ARG;
+  const int k = ste_gemm_kernel(args);
+  const int v = k & 3;
+  const char* ak = (v & 2) ? "false" : "true";
+  const char* bk = (v & 1) ? "false" : "true";
+  if (k >= STE_GEMM_KERNEL_8PH) {
+    ste_gemm_args a = *args;
+    int ef = -1, act = 0;
+    if (k >= STE_GEMM_KERNEL_SPLITK) {
+      ef = 0;
+    } else {
+      const int f = epi_flags(a);
+#define STE_MATCH(AK, BK, E, ACT) \
+  if (AK == (bool)a.a_kc && BK == (bool)a.b_kc && f == (E) && a.act == (ACT)) { ef = (E); act = (ACT); }
+      STE_EPI_SPECS(STE_MATCH)
+#undef STE_MATCH
+    }
+    snprintf(buf, len, "gemm_8ph_kernel<%s, %s, %d, %d>", ak, bk, ef, act);
+  } else {
+    snprintf(buf, len, "%s<%s, %s>", k >= STE_GEMM_KERNEL_BIG ? "gemm_big_kernel" : "gemm_bf16_kernel", ak, bk);
+  }
+  return 0;
 }
 
 extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {

@@ -89,12 +89,9 @@ GEMM_TRACE = None  # list while bench.py measures per-launch GEMM durations with
 
 def gemm_kernel_name(args: GemmArgs) -> str:
     """The kernel symbol rocprofv3 reports for this launch (asks the library which one it picks)."""
-    k = int(fn("ste_gemm_kernel")(C.byref(args)))
-    v = k & 3
-    a_kc, b_kc = ("false" if v & 2 else "true"), ("false" if v & 1 else "true")
-    if k >= 8:  # 8-phase (k >= 12: split-K weight gradient, reported under the same kernel symbol)
-        return f"gemm_8ph_kernel<{a_kc}, {b_kc}, false>"
-    return f"{'gemm_big_kernel' if k >= 4 else 'gemm_bf16_kernel'}<{a_kc}, {b_kc}>"
+    buf = C.create_string_buffer(128)
+    call("ste_gemm_kernel_name", C.byref(args), buf, 128)
+    return buf.value.decode()
 
 
 def linear(x, w, bias=None, **kw):
