@@ -19,6 +19,7 @@
 // read both row-wise (ds_read_b128) and transposed (ds_read_b64_tr_b16).  The
 // "swapped" products (Sᵀ = K·Qᵀ) keep the softmax row on the lane, and accumulator
 // tiles feed the next MFMA directly as B operands (no LDS round trip for P or dS).
+#include <cstdlib>
 #include "common.h"
 #include "../../include/ste.h"
 
@@ -612,12 +613,694 @@ __global__ __launch_bounds__(256) void attn_rel_dE_kernel(ste_attn_args a, int64
   }
 }
 
+// ============================================== relative-key forward, v2 (audio self-attention)
+// 4 waves x 32 queries (two 16-row groups that share every K/V fragment read, halving LDS
+// traffic per MFMA), 128 queries per block.  K/V tiles of 64 keys and their key-mask words
+// are staged by global_load_lds into a 2-deep LDS ring (XOR-swizzled through the source
+// address), one vmcnt(0)+barrier per tile with the next tile already in flight.  Scores live
+// in the exp2 domain.  Relative term: outside the distance band (every key of the tile
+// clamps to the same bin for the group's 16 queries) it is the per-row constant Q·E[0] or
+// Q·E[nrel-1]; inside, an LDS gather from the wave's Q·Eᵀ table.
+namespace rel2 {
+constexpr int WQ = 32, BQ = 128;
+constexpr int QEW = 76;                    // Q·Eᵀ row stride (>= left+right+1 = 73 bins)
+constexpr int KV = 2 * TILE;               // K | V of one tile
+constexpr int MASK_OFF = 2 * KV;           // 2 x 64 int32 key-mask words
+constexpr int QE_OFF = MASK_OFF + 512;
+constexpr int FWD_LDS = QE_OFF + 4 * WQ * QEW * 4;
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+}  // namespace rel2
+
+// piece p (0..7) = rows 8p..8p+7 of a [64][64] bf16 tile, LDS image as swz(); rows past T
+// are clamped to T-1 (their scores are forced to -inf / their probabilities are 0)
+STE_DEV void glds_tile_piece(const bf16* base, int64_t ld, int bT, int r0, int T, char* tile, int piece, int lane) {
+  const int row = piece * 8 + (lane >> 3);
+  const int src_row = min(r0 + row, T - 1);
+  const int ch = (lane & 7) ^ (row & 7);
+  __builtin_amdgcn_global_load_lds((const void*)(base + (int64_t)(bT + src_row) * ld + ch * 8),
+                                   (lds_void*)(tile + piece * 1024), 16, 0, 0);
+}
+STE_DEV void glds_mask(const int32_t* mask, int bT, int r0, int T, char* dst, int lane) {
+  __builtin_amdgcn_global_load_lds((const void*)(mask + bT + min(r0 + lane, T - 1)), (lds_void*)dst, 4, 0, 0);
+}
+// transposed fragment through asm tr reads (see frag_tr)
+STE_DEV bf16x8 frag_tr_asm(const char* t, int cb, int u, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int r0 = 32 * u + 4 * g + q;
+  const int quad = (cb >> 2) + p;
+  return join_tr(ds_read_tr16_asm(t + tr_off(r0, quad)), ds_read_tr16_asm(t + tr_off(r0 + 16, quad)));
+}
+
+__global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
+  using namespace rel2;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T = a.T, H = a.H;
+  const int ntile = (T + BQ - 1) / BQ;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = id % ntile, bh = id / ntile, h = bh % H, b = bh / H, bT = b * T;
+  const int left = a.rel_left, right = a.rel_right, nrel = left + right + 1;
+  const bf16* Qb = (const bf16*)a.q + h * HD;
+  const bf16* Kb = (const bf16*)a.k + h * HD;
+  const bf16* Vb = (const bf16*)a.v + h * HD;
+  const int qw = tile * BQ + w * WQ;
+  const float c2 = a.scale * LOG2E;
+
+  bf16x8 qf[2][2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int q = qw + 16 * gq + li;
+      qf[gq][s] = q < T ? *reinterpret_cast<const bf16x8*>(Qb + (int64_t)(bT + q) * a.ldq + 32 * s + 8 * g) : bf16x8{};
+    }
+  // Q·Eᵀ table of the wave's 32 queries (E staged over the ring, which is free until tile 0)
+  float* qe = reinterpret_cast<float*>(sm + QE_OFF) + w * WQ * QEW;
+  stage_E(sm, (const bf16*)a.rel_E, nrel, NREL, tid);
+  __syncthreads();
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int jt = 0; jt < NREL / 16; ++jt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sm, jt * 16, s, lane), qf[gq][s], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = jt * 16 + 4 * g + r;
+        if (j < QEW) qe[(16 * gq + li) * QEW + j] = acc[r];
+      }
+    }
+  __syncthreads();
+  float blo[2], bhi[2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    blo[gq] = qe[(16 * gq + li) * QEW] * c2;
+    bhi[gq] = qe[(16 * gq + li) * QEW + nrel - 1] * c2;
+  }
+
+  char* sMask = sm + MASK_OFF;
+  const int nkt = (T + TK - 1) / TK;
+  const bool has_mask = a.key_mask != nullptr;
+  // wave w stages K pieces 2w,2w+1 and V pieces 2w,2w+1 (+ wave 0: the 64 mask words)
+  auto issue = [&](int kt) {
+    char* buf = sm + (kt & 1) * KV;
+    const int kb = kt * TK;
+    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w, lane);
+    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w + 1, lane);
+    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w, lane);
+    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w + 1, lane);
+    if (w == 0 && has_mask) glds_mask(a.key_mask, bT, kb, T, sMask + (kt & 1) * 256, lane);
+  };
+  issue(0);
+  if (nkt > 1) issue(1);
+  if (nkt > 1) {
+    if (w == 0 && has_mask) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  f32x4 o[2][4];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const char* tK = sm + (kt & 1) * KV;
+    const char* tV = tK + TILE;
+    const int* mk = reinterpret_cast<const int*>(sMask + (kt & 1) * 256);
+    const int kb = kt * TK;
+    bf16x8 kf[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) kf[t][ss] = frag_kc(tK, t * 16, ss, lane);
+    const bool lane_in = kb + lane < T;
+    const uint64_t in_bits = __ballot(lane_in);
+    const uint64_t ok_bits = __ballot(lane_in && (!has_mask || mk[lane] != 0));
+    const bool all_valid = ok_bits == ~0ull;
+    f32x4 s[2][4];
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s[gq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) s[gq][t] = mfma16(kf[t][ss], qf[gq][ss], s[gq][t]);
+      }
+    bf16x8 vf[4][2];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) vf[dt][u] = frag_tr_asm(tV, dt * 16, u, lane);
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq) {
+      const int q0g = qw + 16 * gq, myq = q0g + li;
+      const bool all_lo = (kb + TK - 1) - q0g <= -left;
+      const bool all_hi = kb - (q0g + 15) >= right;
+      if (all_lo || all_hi) {
+        const float bc = all_lo ? blo[gq] : bhi[gq];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[gq][t][r] = fmaf(s[gq][t][r], c2, bc);
+      } else {
+        const float* qrow = qe + (16 * gq + li) * QEW + left;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            int d = kb + 16 * t + 4 * g + r - myq;
+            d = d < -left ? -left : (d > right ? right : d);
+            s[gq][t][r] = (s[gq][t][r] + qrow[d]) * c2;
+          }
+      }
+      if (!all_valid) {  // bit kl of the ballots: key kb+kl in range / unmasked
+        const uint64_t inl = in_bits >> (4 * g), okl = ok_bits >> (4 * g);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int bit = 16 * t + r;
+            const float fill = ((inl >> bit) & 1) ? NEG_MASK : -INFINITY;
+            s[gq][t][r] = ((okl >> bit) & 1) ? s[gq][t][r] : fill;
+          }
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[gq][t][r]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(m[gq], tmax);
+      const float alpha = __builtin_amdgcn_exp2f(m[gq] - mnew);
+      float psum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(s[gq][t][r] - mnew);
+          psum += pv;
+          s[gq][t][r] = pv;
+        }
+      psum += __shfl_xor(psum, 16, 64);
+      psum += __shfl_xor(psum, 32, 64);
+      l[gq] = l[gq] * alpha + psum;
+      m[gq] = mnew;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16x8 pb = pack_acc(s[gq][2 * u], s[gq][2 * u + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pb, o[gq][dt]);
+      }
+    if (kt + 1 < nkt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (this wave's pieces)
+      __builtin_amdgcn_s_barrier();                     // ... every wave's, and tile kt fully read
+      if (kt + 2 < nkt) issue(kt + 2);
+    }
+  }
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int myq = qw + 16 * gq + li;
+    if (myq < T) {
+      const float inv_l = 1.0f / l[gq];
+      bf16* O = (bf16*)a.o + (int64_t)(bT + myq) * a.ldo + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) store_bf16x4(O + 16 * dt + 4 * g, o[gq][dt] * inv_l);
+      // natural-log LSE.  A row whose every key is masked (scores all finfo.min, as in the
+      // reference: a uniform distribution over the T keys) is stored as -inf: fp32 cannot
+      // hold finfo.min + log(T), and the v2 backward kernels read -inf as "p = 1/T".
+      if (g == 0)
+        a.lse[(int64_t)(b * H + h) * T + myq] = m[gq] == NEG_MASK ? -INFINITY : (m[gq] + log2f(l[gq])) * LN2;
+    }
+  }
+}
+
+// ====================================== relative-key backward, v2: dQ (+ delta, + bins G)
+// 4 waves x 16 queries, K/V ring as in the forward.  delta = rowsum(dO*O) is computed here
+// from the wave's own dO/O fragments (no separate pass) and written for the dK/dV kernel.
+// Probabilities in the exp2 domain: p = exp2((s + bias)*c2 - lse*log2e); a masked key gets
+// exp(NEG_MASK - lse) (0, or 1/l for a row whose every key is masked).  Distance bins:
+// outside the band a whole tile falls into bin 0 or nrel-1 (register sums); inside, the
+// unique interior bin of each (query, key) is stored to the wave's G table.
+namespace rel2 {
+constexpr int DQ_Q = 64;                         // queries per block
+constexpr int GW = 96;                           // G row stride (3 k-steps of 32 for G·E)
+constexpr int DQ_QE_OFF = MASK_OFF + 512;
+constexpr int DQ_G_OFF = DQ_QE_OFF + 4 * 16 * QEW * 4;
+constexpr int DQ_LDS = DQ_G_OFF + 4 * 16 * GW * 4;
+}  // namespace rel2
+
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel2_kernel(ste_attn_args a) {
+  using namespace rel2;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T = a.T, H = a.H;
+  const int ntile = (T + DQ_Q - 1) / DQ_Q;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = id % ntile, bh = id / ntile, h = bh % H, b = bh / H, bT = b * T;
+  const int left = a.rel_left, right = a.rel_right, nrel = left + right + 1;
+  const bf16* Qb = (const bf16*)a.q + h * HD;
+  const bf16* Kb = (const bf16*)a.k + h * HD;
+  const bf16* Vb = (const bf16*)a.v + h * HD;
+  const bf16* dOb = (const bf16*)a.dout + h * HD;
+  const bf16* Ob = (const bf16*)a.o + h * HD;
+  const int q0 = tile * DQ_Q + w * 16, myq = q0 + li;
+  const bool qvalid = myq < T;
+  const int64_t rowid = (int64_t)(b * H + h) * T + myq;
+  const float c2 = a.scale * LOG2E;
+
+  bf16x8 qf[2], df[2];
+  float dpart = 0.f;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int64_t off = (int64_t)(bT + myq);
+    qf[s] = qvalid ? *reinterpret_cast<const bf16x8*>(Qb + off * a.ldq + 32 * s + 8 * g) : bf16x8{};
+    df[s] = qvalid ? *reinterpret_cast<const bf16x8*>(dOb + off * a.lddo + 32 * s + 8 * g) : bf16x8{};
+    const bf16x8 of = qvalid ? *reinterpret_cast<const bf16x8*>(Ob + off * a.ldo + 32 * s + 8 * g) : bf16x8{};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dpart += (float)df[s][e] * (float)of[e];
+  }
+  dpart += __shfl_xor(dpart, 16, 64);
+  dpart += __shfl_xor(dpart, 32, 64);
+  const float dl = dpart;
+  if (qvalid && g == 0) a.delta[rowid] = dl;
+  const float lse = qvalid ? a.lse[rowid] : 0.f;
+  const float nl2 = -lse * LOG2E;
+  const float pm = lse == -INFINITY ? 1.0f / T : 0.f;   // probability of a masked key in this row
+
+  float* qe = reinterpret_cast<float*>(sm + DQ_QE_OFF) + w * 16 * QEW;
+  float* gt = reinterpret_cast<float*>(sm + DQ_G_OFF) + w * 16 * GW;
+  stage_E(sm, (const bf16*)a.rel_E, nrel, GW, tid);
+  for (int i = lane; i < 16 * GW; i += 64) gt[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int jt = 0; jt < NREL / 16; ++jt) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sm, jt * 16, s, lane), qf[s], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = jt * 16 + 4 * g + r;
+      if (j < QEW) qe[li * QEW + j] = acc[r];
+    }
+  }
+  __syncthreads();
+  const float blo = qe[li * QEW] * c2 + nl2, bhi = qe[li * QEW + nrel - 1] * c2 + nl2;
+  const float* qrow = qe + li * QEW + left;
+  float* grow = gt + li * GW + left;
+
+  char* sMask = sm + MASK_OFF;
+  const int nkt = (T + TK - 1) / TK;
+  const bool has_mask = a.key_mask != nullptr;
+  auto issue = [&](int kt) {
+    char* buf = sm + (kt & 1) * KV;
+    const int kb = kt * TK;
+    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w, lane);
+    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w + 1, lane);
+    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w, lane);
+    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w + 1, lane);
+    if (w == 0 && has_mask) glds_mask(a.key_mask, bT, kb, T, sMask + (kt & 1) * 256, lane);
+  };
+  issue(0);
+  if (nkt > 1) issue(1);
+  if (nkt > 1) {
+    if (w == 0 && has_mask) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  f32x4 dq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float glo = 0.f, ghi = 0.f;
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const char* tK = sm + (kt & 1) * KV;
+    const char* tV = tK + TILE;
+    const int* mk = reinterpret_cast<const int*>(sMask + (kt & 1) * 256);
+    const int kb = kt * TK;
+    f32x4 sc[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[t] = sc[t];
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        sc[t] = mfma16(frag_kc(tK, t * 16, ss, lane), qf[ss], sc[t]);
+        dp[t] = mfma16(frag_kc(tV, t * 16, ss, lane), df[ss], dp[t]);
+      }
+    }
+    bf16x8 ktr[4][2];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) ktr[dt][u] = frag_tr_asm(tK, dt * 16, u, lane);
+    const bool lane_in = kb + lane < T;
+    const uint64_t in_bits = __ballot(lane_in);
+    const uint64_t ok_bits = __ballot(lane_in && (!has_mask || mk[lane] != 0));
+    const bool all_valid = ok_bits == ~0ull;
+    const bool all_lo = (kb + TK - 1) - q0 <= -left;
+    const bool all_hi = kb - (q0 + 15) >= right;
+    const bool band = !(all_lo || all_hi);
+    if (!band) {
+      const float cb = all_lo ? blo : bhi;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[t][r] = __builtin_amdgcn_exp2f(fmaf(sc[t][r], c2, cb));
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int d = kb + 16 * t + 4 * g + r - myq;
+          d = d < -left ? -left : (d > right ? right : d);
+          sc[t][r] = __builtin_amdgcn_exp2f(fmaf(sc[t][r] + qrow[d], c2, nl2));
+        }
+    }
+    if (!all_valid) {
+      const uint64_t inl = in_bits >> (4 * g), okl = ok_bits >> (4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int bit = 16 * t + r;
+          const float fill = ((inl >> bit) & 1) ? pm : 0.f;
+          sc[t][r] = ((okl >> bit) & 1) ? sc[t][r] : fill;
+        }
+    }
+    // dS = P (dP - delta); bins
+    float bsum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ds = sc[t][r] * (dp[t][r] - dl);
+        sc[t][r] = ds;
+        bsum += ds;
+      }
+    if (!band) {
+      if (all_lo) glo += bsum; else ghi += bsum;
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int d = kb + 16 * t + 4 * g + r - myq;
+          if (d <= -left) glo += sc[t][r];
+          else if (d >= right) ghi += sc[t][r];
+          else grow[d] = sc[t][r];
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16x8 pb = pack_acc(sc[2 * u], sc[2 * u + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(ktr[dt][u], pb, dq[dt]);
+    }
+    if (kt + 1 < nkt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < nkt) issue(kt + 2);
+    }
+  }
+  glo += __shfl_xor(glo, 16, 64);
+  glo += __shfl_xor(glo, 32, 64);
+  ghi += __shfl_xor(ghi, 16, 64);
+  ghi += __shfl_xor(ghi, 32, 64);
+  if (g == 0) {
+    gt[li * GW] = glo;
+    gt[li * GW + nrel - 1] = ghi;
+  }
+  __syncthreads();                       // ring free: restage E (96 rows) for dQ += G·E
+  stage_E(sm, (const bf16*)a.rel_E, nrel, GW, tid);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(gt + li * GW + 32 * u + 4 * g);
+    const f32x4 g1 = *reinterpret_cast<const f32x4*>(gt + li * GW + 32 * u + 16 + 4 * g);
+    const bf16x8 pb = pack_acc(g0, g1);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(frag_tr(sm, dt * 16, u, lane), pb, dq[dt]);
+  }
+  if (a.dE && qvalid) {
+    float* G = a.gwork + rowid * NREL;
+#pragma unroll
+    for (int c = 0; c < NREL / 16; ++c) {
+      const int j = c * 16 + 4 * g;
+      *reinterpret_cast<f32x4*>(G + j) = *reinterpret_cast<const f32x4*>(gt + li * GW + j);
+    }
+  }
+  if (qvalid) {
+    bf16* dQ = (bf16*)a.dq + (int64_t)(bT + myq) * a.lddq + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) store_bf16x4(dQ + 16 * dt + 4 * g, dq[dt] * a.scale);
+  }
+}
+
+// ================================================= relative-key backward, v2: dK and dV
+// 4 waves x 32 keys (two 16-key groups sharing every Q/dO fragment read), 128 keys per
+// block, iterating over query tiles of 64 whose Q, dO, lse and delta are staged by
+// global_load_lds into a 2-deep ring.  Per query tile the four waves rebuild that tile's
+// Q·Eᵀ table from the resident E (all 80 bins when the block meets the distance band,
+// else only the two edge bins).
+namespace rel2 {
+constexpr int KB = 128;                          // keys per block
+constexpr int QD = 2 * TILE + 512;               // Q | dO | lse[64] | delta[64]
+constexpr int KV_E_OFF = 2 * QD;
+constexpr int KV_QE_OFF = KV_E_OFF + NREL * 128;
+constexpr int KV_EDGE_OFF = KV_QE_OFF + 64 * QEW * 4;   // elo[64], ehi[64]
+constexpr int DKV_LDS = KV_EDGE_OFF + 512;
+}  // namespace rel2
+
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel2_kernel(ste_attn_args a) {
+  using namespace rel2;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T = a.T, H = a.H;
+  const int ntile = (T + KB - 1) / KB;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = id % ntile, bh = id / ntile, h = bh % H, b = bh / H, bT = b * T;
+  const int left = a.rel_left, right = a.rel_right, nrel = left + right + 1;
+  const bf16* Qb = (const bf16*)a.q + h * HD;
+  const bf16* Kb = (const bf16*)a.k + h * HD;
+  const bf16* Vb = (const bf16*)a.v + h * HD;
+  const bf16* dOb = (const bf16*)a.dout + h * HD;
+  const int kb0 = tile * KB, k0w = kb0 + w * 32;
+  const int64_t rowbase = (int64_t)(b * H + h) * T;
+  const float c2 = a.scale * LOG2E;
+
+  bf16x8 kf[2][2], vf[2][2];
+  bool kmask[2];
+#pragma unroll
+  for (int gk = 0; gk < 2; ++gk) {
+    const int key = k0w + 16 * gk + li;
+    const bool kv = key < T;
+    kmask[gk] = kv && a.key_mask != nullptr && a.key_mask[bT + key] == 0;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      kf[gk][s] = kv ? *reinterpret_cast<const bf16x8*>(Kb + (int64_t)(bT + key) * a.ldk + 32 * s + 8 * g) : bf16x8{};
+      vf[gk][s] = kv ? *reinterpret_cast<const bf16x8*>(Vb + (int64_t)(bT + key) * a.ldv + 32 * s + 8 * g) : bf16x8{};
+    }
+  }
+  const bool any_masked = __ballot(kmask[0] || kmask[1]) != 0;
+  char* sE = sm + KV_E_OFF;
+  float* qet = reinterpret_cast<float*>(sm + KV_QE_OFF);
+  float* elo = reinterpret_cast<float*>(sm + KV_EDGE_OFF);
+  float* ehi = elo + 64;
+  stage_E(sE, (const bf16*)a.rel_E, nrel, NREL, tid);
+
+  const int nqt = (T + TQ - 1) / TQ;
+  // wave w stages Q pieces 2w,2w+1 and dO pieces 2w,2w+1; wave 0 the lse words, wave 1 delta
+  auto issue = [&](int qt) {
+    char* buf = sm + (qt & 1) * QD;
+    const int qb = qt * TQ;
+    glds_tile_piece(Qb, a.ldq, bT, qb, T, buf, 2 * w, lane);
+    glds_tile_piece(Qb, a.ldq, bT, qb, T, buf, 2 * w + 1, lane);
+    glds_tile_piece(dOb, a.lddo, bT, qb, T, buf + TILE, 2 * w, lane);
+    glds_tile_piece(dOb, a.lddo, bT, qb, T, buf + TILE, 2 * w + 1, lane);
+    if (w < 2) {
+      const float* src = (w == 0 ? a.lse : a.delta) + rowbase + min(qb + lane, T - 1);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(buf + 2 * TILE + w * 256), 4, 0, 0);
+    }
+  };
+  issue(0);
+  if (nqt > 1) issue(1);
+  if (nqt > 1) {
+    if (w < 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();   // also publishes sE (plain stores)
+
+  f32x4 dk[2][4], dv[2][4];
+#pragma unroll
+  for (int gk = 0; gk < 2; ++gk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      dk[gk][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[gk][i] = dk[gk][i];
+    }
+
+  for (int qt = 0; qt < nqt; ++qt) {
+    const char* tQ = sm + (qt & 1) * QD;
+    const char* tD = tQ + TILE;
+    const float* sL = reinterpret_cast<const float*>(tQ + 2 * TILE);   // lse[64] | delta[64]
+    const int qb = qt * TQ;
+    // Q·Eᵀ of this query tile: wave w builds rows 16w..16w+15
+    const bool blk_lo = (kb0 + KB - 1) - qb <= -left;
+    const bool blk_hi = kb0 - (qb + TQ - 1) >= right;
+    const bool blk_band = !(blk_lo || blk_hi);
+    {
+      bf16x8 qfr[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) qfr[s] = frag_kc(tQ, 16 * w, s, lane);
+#pragma unroll
+      for (int jt = 0; jt < NREL / 16; ++jt) {
+        if (!blk_band && jt != 0 && jt != (nrel - 1) / 16) continue;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sE, jt * 16, s, lane), qfr[s], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = jt * 16 + 4 * g + r;
+          if (j < QEW) qet[(16 * w + li) * QEW + j] = acc[r];
+          if (j == 0) elo[16 * w + li] = acc[r] * c2;
+          if (j == nrel - 1) ehi[16 * w + li] = acc[r] * c2;
+        }
+      }
+    }
+    __syncthreads();
+    // per-lane query vectors (queries 16n + 4g + r): -lse*log2e, delta, edge biases
+    f32x4 nl2[4], dlt[4], lsev[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      lsev[n] = *reinterpret_cast<const f32x4*>(sL + 16 * n + 4 * g);
+      dlt[n] = *reinterpret_cast<const f32x4*>(sL + 64 + 16 * n + 4 * g);
+      nl2[n] = lsev[n] * -LOG2E;
+    }
+#pragma unroll
+    for (int gk = 0; gk < 2; ++gk) {
+      const int k0g = k0w + 16 * gk, mykey = k0g + li;
+      f32x4 sc[4], dp[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        sc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[n] = sc[n];
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          sc[n] = mfma16(frag_kc(tQ, 16 * n, ss, lane), kf[gk][ss], sc[n]);
+          dp[n] = mfma16(frag_kc(tD, 16 * n, ss, lane), vf[gk][ss], dp[n]);
+        }
+      }
+      const bool all_lo = (k0g + 15) - qb <= -left;
+      const bool all_hi = k0g - (qb + TQ - 1) >= right;
+      if (all_lo || all_hi) {
+        const float* ev = all_lo ? elo : ehi;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const f32x4 eb = *reinterpret_cast<const f32x4*>(ev + 16 * n + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sc[n][r] = __builtin_amdgcn_exp2f(fmaf(sc[n][r], c2, eb[r] + nl2[n][r]));
+        }
+      } else {
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ql = 16 * n + 4 * g + r;
+            int d = mykey - (qb + ql);
+            d = d < -left ? -left : (d > right ? right : d);
+            sc[n][r] = __builtin_amdgcn_exp2f(fmaf(sc[n][r] + qet[ql * QEW + d + left], c2, nl2[n][r]));
+          }
+      }
+      if (any_masked && kmask[gk]) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sc[n][r] = lsev[n][r] == -INFINITY ? 1.0f / T : 0.f;
+      }
+      if (qb + TQ > T) {  // last query tile: rows past T (staged as copies of row T-1) add nothing
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (qb + 16 * n + 4 * g + r >= T) sc[n][r] = 0.f;
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        dp[n] = sc[n] * (dp[n] - dlt[n]) * a.scale;   // dS * scale (for dK)
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16x8 pv = pack_acc(sc[2 * u], sc[2 * u + 1]);
+        const bf16x8 pk = pack_acc(dp[2 * u], dp[2 * u + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          dv[gk][dt] = mfma16(frag_tr(tD, dt * 16, u, lane), pv, dv[gk][dt]);
+          dk[gk][dt] = mfma16(frag_tr(tQ, dt * 16, u, lane), pk, dk[gk][dt]);
+        }
+      }
+    }
+    if (qt + 1 < nqt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (qt + 2 < nqt) issue(qt + 2);
+    }
+  }
+#pragma unroll
+  for (int gk = 0; gk < 2; ++gk) {
+    const int key = k0w + 16 * gk + li;
+    if (key < T) {
+      bf16* dK = (bf16*)a.dk + (int64_t)(bT + key) * a.lddk + h * HD;
+      bf16* dV = (bf16*)a.dv + (int64_t)(bT + key) * a.lddv + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        store_bf16x4(dK + 16 * dt + 4 * g, dk[gk][dt]);
+        store_bf16x4(dV + 16 * dt + 4 * g, dv[gk][dt]);
+      }
+    }
+  }
+}
+
 constexpr int FWD_LDS = 4 * TILE + NREL * 128 + 4 * 16 * NREL * 4 + 2 * 64 * 4;
 constexpr int DQ_LDS = 2 * TILE + 96 * 128 + 4 * 16 * NREL * 4 + 4 * 16 * 96 * 4 + 64 * 4;
 constexpr int DKV_LDS = 4 * TILE + NREL * 128 + 64 * NREL * 4 + 2 * 128 * 4;
 
 template <template <bool, bool> class K>
 struct Dispatch;
+
+// STE_ATTN_V1=1: the original relative-key kernels (A/B comparisons in one process)
+bool rel_v2() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("STE_ATTN_V1");
+    v = (e && e[0] == '1') ? 0 : 1;
+  }
+  return v == 1;
+}
 
 int check(const ste_attn_args* a) {
   if (!a || a->B <= 0 || a->T <= 0 || a->H <= 0) return STE_ERR_ARG;
@@ -635,6 +1318,12 @@ extern "C" int ste_attention_fwd(const ste_attn_args* a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)(((a->T + TQ - 1) / TQ) * a->H * a->B));
   const bool rel = a->rel_E != nullptr, drop = a->drop_p > 0.f;
+  if (rel && !drop && rel_v2()) {
+    dim3 g2((unsigned)(((a->T + rel2::BQ - 1) / rel2::BQ) * a->H * a->B));
+    hipLaunchKernelGGL(attn_fwd_rel2_kernel, g2, dim3(NT), rel2::FWD_LDS, s, *a);
+    STE_CHECK_LAUNCH();
+    return 0;
+  }
   if (rel && drop) hipLaunchKernelGGL((attn_fwd_kernel<true, true>), grid, dim3(NT), FWD_LDS, s, *a);
   else if (rel) hipLaunchKernelGGL((attn_fwd_kernel<true, false>), grid, dim3(NT), FWD_LDS, s, *a);
   else if (drop) hipLaunchKernelGGL((attn_fwd_kernel<false, true>), grid, dim3(NT), FWD_LDS, s, *a);
@@ -650,6 +1339,21 @@ extern "C" int ste_attention_bwd(const ste_attn_args* a, void* stream) {
   if (a->dE && (!a->gwork || !a->rel_E)) return STE_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nrow = (int64_t)a->B * a->T * a->H;
+  if (a->rel_E && a->drop_p == 0.f && rel_v2()) {
+    dim3 gq((unsigned)(((a->T + rel2::DQ_Q - 1) / rel2::DQ_Q) * a->H * a->B));
+    hipLaunchKernelGGL(attn_bwd_dq_rel2_kernel, gq, dim3(NT), rel2::DQ_LDS, s, *a);
+    STE_CHECK_LAUNCH();
+    dim3 gk((unsigned)(((a->T + rel2::KB - 1) / rel2::KB) * a->H * a->B));
+    hipLaunchKernelGGL(attn_bwd_dkv_rel2_kernel, gk, dim3(NT), rel2::DKV_LDS, s, *a);
+    STE_CHECK_LAUNCH();
+    if (a->dE) {
+      const int blocks = 512;
+      int64_t rpb = (nrow + blocks - 1) / blocks;
+      hipLaunchKernelGGL(attn_rel_dE_kernel, dim3(blocks), dim3(256), 0, s, *a, rpb);
+      STE_CHECK_LAUNCH();
+    }
+    return 0;
+  }
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((nrow + 255) / 256)), dim3(256), 0, s, *a);
   STE_CHECK_LAUNCH();
   dim3 grid((unsigned)(((a->T + TQ - 1) / TQ) * a->H * a->B));

@@ -109,4 +109,18 @@ STE_DEV int xcd_remap(int bid, int n) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+
+typedef __attribute__((address_space(3))) void lds_void;
+// ds_read_b64_tr_b16 through inline asm: invisible to hipcc's waitcnt pass, which would
+// otherwise treat the builtin as aliasing every in-flight global_load_lds and drain them
+// with vmcnt(0).  The caller orders the read itself (lgkmcnt(0) + sched_barrier(0) before
+// the consuming MFMAs).
+STE_DEV s16x4 ds_read_tr16_asm(const char* p) {
+  typedef __attribute__((address_space(3))) const char lds_cchar;
+  const uint32_t off = (uint32_t)(uintptr_t)(lds_cchar*)p;
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(off) : "memory");
+  return r;
+}
+
 #define STE_CHECK_LAUNCH() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)

@@ -30,7 +30,6 @@
 
 namespace {
 
-typedef __attribute__((address_space(3))) void lds_void;
 
 STE_DEV int km_chunk_xor(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
 
@@ -680,13 +679,6 @@ STE_DEV void stage_half(const bf16* base, int64_t ld, int row0, int rows, int k0
 // vmcnt(0) before it, which drains the 8-phase pipeline; the asm form is invisible to that
 // pass, so the kernel orders these reads itself (lgkmcnt(0) + sched_barrier before the
 // MFMAs that consume them).
-STE_DEV s16x4 ds_read_tr16_asm(const char* p) {
-  typedef __attribute__((address_space(3))) const char lds_cchar;
-  const uint32_t off = (uint32_t)(uintptr_t)(lds_cchar*)p;
-  s16x4 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(off) : "memory");
-  return r;
-}
 STE_DEV bf16x8 frag_load_km_asm(const char* tile, int rb, int s, int lane) {
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
   const int k = s * 32 + 8 * g + q;

@@ -144,6 +144,8 @@ def _attn_case(ops, B, T, H, rel, masked, drop_p, seed=7):
         m[0, T - T // 3:] = 0
         if B > 1:
             m[1, :5] = 0
+        if masked == "all" and B > 2:
+            m[2, :] = 0          # every key masked: uniform attention, like the reference's finfo.min fill
         mask = m.reshape(-1).contiguous()
     E = (torch.randn(73, D, device=DEV) * 0.5).bfloat16() if rel else None
     o = torch.empty(B * T, W, device=DEV, dtype=torch.bfloat16)
@@ -153,6 +155,19 @@ def _attn_case(ops, B, T, H, rel, masked, drop_p, seed=7):
     Ef = E.float().clone().requires_grad_() if rel else None
     ref = attention_ref(qf, kf, vf, mask.view(B, T) if masked else None, Ef, drop_p=drop_p, seed=seed)
     assert rel_err(o.view(B, T, H, D), ref) < 1e-2
+    with torch.no_grad():  # saved log-sum-exp of the scaled, biased, masked scores
+        qh, kh = qf.permute(0, 2, 1, 3), kf.permute(0, 2, 1, 3)
+        sc = qh @ kh.transpose(-1, -2)
+        if rel:
+            pos = torch.arange(T, device=DEV)
+            dist = (pos.view(1, -1) - pos.view(-1, 1)).clamp(-64, 8) + 64
+            sc = sc + torch.gather(qh @ Ef.t(), 3, dist.view(1, 1, T, T).expand(B, H, T, T))
+        sc = sc / math.sqrt(D)
+        if masked:
+            sc = sc + (1.0 - mask.view(B, T)[:, None, None, :].float()) * torch.finfo(torch.float32).min
+        lse_ref = torch.logsumexp(sc, -1).reshape(-1)
+        fin = lse_ref.abs() < 1e30
+        assert rel_err(lse[fin], lse_ref[fin]) < 1e-3
     do = torch.randn(B * T, W, device=DEV).bfloat16()
     ref.backward(do.float().view(B, T, H, D))
     dqkv = torch.zeros(B * T, 3 * W, device=DEV, dtype=torch.bfloat16)
@@ -171,6 +186,10 @@ def _attn_case(ops, B, T, H, rel, masked, drop_p, seed=7):
 @pytest.mark.parametrize("T", [99, 150, 499])
 def test_attention_relkey(ops, T):
     _attn_case(ops, B=2, T=T, H=2, rel=True, masked=True, drop_p=0.0)
+
+
+def test_attention_relkey_fully_masked_row(ops):
+    _attn_case(ops, B=3, T=130, H=2, rel=True, masked="all", drop_p=0.0)
 
 
 def test_attention_relkey_unmasked_long(ops):
