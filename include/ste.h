@@ -278,6 +278,18 @@ int ste_text_embed_fwd(const int64_t* ids, int B, int L, int D, int pad_idx, con
 int ste_text_embed_bwd(const int64_t* ids, const int32_t* pos_ids, const float* dout, int B, int L, int D,
                        int pad_idx, float* dword, float* dpos, float* dtype0, void* stream);
 
+/* Row-sparse exchange of the word-embedding gradient between data-parallel ranks
+ * (replaces all-reducing the dense 250,002 x 768 table that
+ * ref:training/trainer_unfreeze.py:1084-1117 leaves to a single GPU).
+ * ste_rows_extract: unique non-pad ids of ids[n] -> out_ids[cap] (-1 = empty slot),
+ *   rows[cap, D] = grad[id] and grad[id] = 0.  flags int32 [vocab] must be zero on entry
+ *   and is zero again on exit.  cap >= number of unique ids (e.g. n).
+ * ste_rows_accumulate: grad[ids[s]] += scale * rows[s] for ids[s] >= 0 (unique ids). */
+int ste_rows_extract(const int64_t* ids, int n, int pad_idx, float* grad, int D, int32_t* flags,
+                     int32_t* out_ids, float* rows, int cap, int32_t* count, void* stream);
+int ste_rows_accumulate(float* grad, int D, const int32_t* ids, const float* rows, int cap, float scale,
+                        void* stream);
+
 /* ------------------------------------------------------------- optimizer --
  * torch.nn.utils.clip_grad_norm_ + torch.optim.AdamW.step
  * (ref:training/trainer_unfreeze.py:1108-1110, groups :1487-1511).

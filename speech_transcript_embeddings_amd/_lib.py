@@ -109,6 +109,9 @@ _SIGS = {
     "ste_gemm": (c_int, [C.POINTER(GemmArgs), c_void_p]),
     "ste_gemm_kernel": (c_int, [C.POINTER(GemmArgs)]),
     "ste_gemm_kernel_name": (c_int, [C.POINTER(GemmArgs), c_char_p, c_int]),
+    "ste_rows_extract": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                 c_void_p, c_void_p]),
+    "ste_rows_accumulate": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_float, c_void_p]),
     "ste_layernorm_fwd": (c_int, [C.POINTER(LnFwdArgs), c_void_p]),
     "ste_layernorm_bwd": (c_int, [C.POINTER(LnBwdArgs), c_void_p]),
     "ste_attention_fwd": (c_int, [C.POINTER(AttnArgs), c_void_p]),

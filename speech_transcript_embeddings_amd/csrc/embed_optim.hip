@@ -131,6 +131,85 @@ inline unsigned grid_for(int64_t n) {
 
 }  // namespace
 
+// ---------------------------------------------------------- row-sparse gradient exchange
+// The word-embedding gradient of one rank is non-zero only in the rows of its token ids
+// (SURVEY §8e).  Data-parallel ranks exchange (row id, row) lists instead of all-reducing
+// the 250,002 x 768 table:  claim the rank's unique ids (first arrival wins a slot),
+// extract those rows (zeroing them in place), all-gather the fixed-capacity lists, then
+// add every rank's list in rank order (ids unique within a list, so no atomics and the
+// same summation order on every rank).
+namespace {
+__global__ __launch_bounds__(NT) void rows_reset_kernel(int32_t* out_ids, int cap, int32_t* count) {
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (i < cap) out_ids[i] = -1;
+  if (i == 0) *count = 0;
+}
+__global__ __launch_bounds__(NT) void rows_claim_kernel(const int64_t* ids, int n, int pad, int32_t* flags,
+                                                       int32_t* out_ids, int cap, int32_t* count) {
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  const int64_t id = ids[i];
+  if (id == pad || id < 0) return;
+  if (atomicCAS(flags + id, 0, 1) == 0) {
+    const int slot = atomicAdd(count, 1);
+    if (slot < cap) out_ids[slot] = (int32_t)id;
+  }
+}
+// one block per slot: rows[s] = grad[id] (then grad[id] = 0, flags[id] = 0); empty slot -> 0
+__global__ __launch_bounds__(NT) void rows_extract_kernel(float* grad, int D, const int32_t* out_ids, int32_t* flags,
+                                                         float* rows) {
+  const int sidx = blockIdx.x;
+  const int id = out_ids[sidx];
+  float* dst = rows + (int64_t)sidx * D;
+  if (id < 0) {
+    for (int c = threadIdx.x * 4; c < D; c += NT * 4) *reinterpret_cast<f32x4*>(dst + c) = f32x4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
+  float* src = grad + (int64_t)id * D;
+  for (int c = threadIdx.x * 4; c < D; c += NT * 4) {
+    *reinterpret_cast<f32x4*>(dst + c) = *reinterpret_cast<const f32x4*>(src + c);
+    *reinterpret_cast<f32x4*>(src + c) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (threadIdx.x == 0) flags[id] = 0;
+}
+__global__ __launch_bounds__(NT) void rows_accumulate_kernel(float* grad, int D, const int32_t* ids, const float* rows,
+                                                            float scale) {
+  const int sidx = blockIdx.x;
+  const int id = ids[sidx];
+  if (id < 0) return;
+  float* dst = grad + (int64_t)id * D;
+  const float* src = rows + (int64_t)sidx * D;
+  for (int c = threadIdx.x * 4; c < D; c += NT * 4)
+    *reinterpret_cast<f32x4*>(dst + c) += *reinterpret_cast<const f32x4*>(src + c) * scale;
+}
+}  // namespace
+
+extern "C" int ste_rows_extract(const int64_t* ids, int n, int pad_idx, float* grad, int D, int32_t* flags,
+                                int32_t* out_ids, float* rows, int cap, int32_t* count, void* stream) {
+  if (n < 0 || cap <= 0 || (D & 3) || !grad || !flags || !out_ids || !rows || !count) return STE_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(rows_reset_kernel, dim3((cap + NT - 1) / NT), dim3(NT), 0, s, out_ids, cap, count);
+  STE_CHECK_LAUNCH();
+  if (n > 0) {
+    hipLaunchKernelGGL(rows_claim_kernel, dim3((n + NT - 1) / NT), dim3(NT), 0, s, ids, n, pad_idx, flags, out_ids,
+                       cap, count);
+    STE_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(rows_extract_kernel, dim3(cap), dim3(NT), 0, s, grad, D, out_ids, flags, rows);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_rows_accumulate(float* grad, int D, const int32_t* ids, const float* rows, int cap, float scale,
+                                   void* stream) {
+  if (cap <= 0 || (D & 3) || !grad || !ids || !rows) return STE_ERR_ARG;
+  hipLaunchKernelGGL(rows_accumulate_kernel, dim3(cap), dim3(NT), 0, (hipStream_t)stream, grad, D, ids, rows, scale);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+
+
 extern "C" int ste_text_embed_fwd(const int64_t* ids, int B, int L, int D, int pad_idx, const float* word,
                                   const float* pos, const float* type0, float* out, int32_t* pos_ids, void* stream) {
   if (B <= 0 || L <= 0 || L > 2048 || (D & 3)) return STE_ERR_SHAPE;

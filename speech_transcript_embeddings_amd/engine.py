@@ -649,7 +649,10 @@ class Engine:
         b = batch["input_ids_pos"].shape[0]
         return tf[:b], tf[b:], af, align, ctx
 
-    def backward(self, ctx, d_tp, d_tn, d_af, d_align):
+    def backward(self, ctx, d_tp, d_tn, d_af, d_align, stage_done=None):
+        """Backward of the whole step.  stage_done(name) is called once the gradients of a
+        parameter block are final ("heads", then "audio", then "text"), so a data-parallel
+        caller can start their collective while the rest of the backward runs."""
         nb = ctx["t_nb"]
         d_tf = self._e(nb, self.m.projection_dim)
         _copy_f32(d_tp, d_tf[: nb // 2])
@@ -658,9 +661,15 @@ class Engine:
         dah = self._z(ctx["a_b"] * ctx["a_T"], self.acfg.hidden_size)
         self.heads_backward(d_tf, d_af, d_align, ctx, dth, dah)
         ctx.pop("heads", None)
+        if stage_done:
+            stage_done("heads")
         self.audio_backward(dah, ctx)
         del dah
+        if stage_done:
+            stage_done("audio")
         self.text_backward(dth, ctx)
+        if stage_done:
+            stage_done("text")
         ctx.clear()
 
 

@@ -340,3 +340,16 @@ def colsum(x, out):
     """out[c] += Σ_r x[r, c]."""
     call("ste_colsum", ptr(x), int(x.dtype == BF16), x.shape[0], x.shape[1], _ld(x), ptr(out), _s())
     return out
+
+
+# ------------------------------------------------- row-sparse gradient exchange
+def rows_extract(ids, pad_idx, grad2d, flags, out_ids, rows, count):
+    """Unique non-pad ids -> out_ids (-1 padded), rows = grad2d[ids], grad2d[ids] = 0."""
+    assert ids.dtype == torch.int64 and grad2d.dtype == F32 and rows.shape[0] == out_ids.numel()
+    call("ste_rows_extract", ptr(ids), ids.numel(), int(pad_idx), ptr(grad2d), grad2d.shape[1], ptr(flags),
+         ptr(out_ids), ptr(rows), out_ids.numel(), ptr(count), _s())
+
+
+def rows_accumulate(grad2d, ids, rows, scale):
+    """grad2d[ids[s]] += scale * rows[s] for ids[s] >= 0 (ids unique)."""
+    call("ste_rows_accumulate", ptr(grad2d), grad2d.shape[1], ptr(ids), ptr(rows), ids.numel(), float(scale), _s())
