@@ -111,7 +111,7 @@ STE_DEV void st8(void* p, bool is_bf16, f32x8 v, bool full, int nval) {
 }
 
 STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, int row0, int col0, int col1,
-                           int batch, int lane, Csum& csum) {
+                           int batch, int lane, Csum& csum, int ld = EPI_LD, bool swz16 = false) {
   const int cl = (lane & 7) * 8;  // staged column of this lane's 8
   const int col = cl < 32 ? col0 + cl : col1 + (cl - 32);
   const int nval = p.N - col;     // valid columns from `col`
@@ -125,8 +125,13 @@ STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, 
   for (int lr = lane >> 3; lr < nrows; lr += 8) {
     const int row = row0 + lr;
     if (row >= p.M) break;
-    const float* src = epi + lr * EPI_LD + cl;
-    const f32x4 s0 = *reinterpret_cast<const f32x4*>(src), s1 = *reinterpret_cast<const f32x4*>(src + 4);
+    const float* src = epi + lr * ld + cl;
+    f32x4 s0 = *reinterpret_cast<const f32x4*>(src), s1 = *reinterpret_cast<const f32x4*>(src + 4);
+    if (swz16 && ((lr >> 1) & 1)) {  // the 8-phase slot's chunk swizzle (see epi_store16)
+      const f32x4 t = s0;
+      s0 = s1;
+      s1 = t;
+    }
     f32x8 v = f32x8{s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
     v = (v + bias) * p.alpha;
     if (p.act >= STE_ACT_SWISH && p.act <= STE_ACT_RELU) {
@@ -238,39 +243,63 @@ STE_DEV f32x8 actd8(f32x8 z, int act) {
   return g;
 }
 
-// One 32-row pass of a wave: staged fp32 [32 x 64] at `epi` (row stride EPI_LD); staged
-// columns 0..31 -> col0.., 32..63 -> col1...  Lane: 8 columns x rows lr, lr+8, lr+16, lr+24.
-// FULL: every row < M and every column < N (no bounds work at all).
-// epi_load32 issues the pass's global loads (Z, R, beta*C) one pass AHEAD (before the
-// previous pass's stores), so waiting for them never waits for in-flight stores.
+// One 16-row pass of a wave's 128 x 64 accumulator block, staged fp32 in the wave's
+// private [16][64] LDS slot with 16-B chunks XOR-swizzled by bit 1 of the row
+// (chunk ^ ((row >> 1) & 1): conflict-free ds_read_b128, 2-way ds_write_b32 which is free).
+// Staged columns 0..31 -> col0.., 32..63 -> col1...  Lane: 8 columns of rows lr and lr + 8.
+// FULL: every row < M and every column < N: straight-line code, so the pass issues exactly
+// epi_stores<EF>()/8 global stores (the next tile's first vmcnt waits count them).
+// epi_load16 issues a pass's global loads (Z, R, beta*C) one pass AHEAD, before the
+// previous pass's stores, so waiting for them never waits for in-flight stores.
 struct EpiFlags {
   int act;
   bool fwd_act, f_c2, f_z, f_drop, f_rs, f_cs, f_r, r_bf, f_beta, c_bf, f_c3;
 };
 template <int EF, int ACT>
 STE_DEV EpiFlags epi_flags_dev(const ste_gemm_args& p) {
-  constexpr int F = EF < 0 ? 0 : EF;
   EpiFlags f;
-  f.act = ACT;
-  f.fwd_act = ACT >= STE_ACT_SWISH && ACT <= STE_ACT_RELU;
-  f.f_c2 = (F & EF_C2) != 0;
-  f.f_z = (F & EF_Z) != 0;
-  f.f_drop = (F & EF_DROP) != 0;
-  f.f_rs = (F & EF_RS) != 0;
-  f.f_cs = (F & EF_COLSUM) != 0;
-  f.f_r = (F & EF_R) != 0;
-  f.r_bf = (F & EF_RBF16) != 0;
-  f.f_beta = (F & EF_BETA) != 0;
-  f.c_bf = (F & EF_CBF16) != 0;
-  f.f_c3 = (F & EF_C3) != 0;
+  if constexpr (EF < 0) {  // generic: every feature at run time
+    f.act = p.act;
+    f.fwd_act = p.act >= STE_ACT_SWISH && p.act <= STE_ACT_RELU;
+    f.f_c2 = p.C2 != nullptr && f.fwd_act;
+    f.f_z = p.act >= STE_ACT_SWISH_BWD;
+    f.f_drop = p.drop_p > 0.f;
+    f.f_rs = p.row_scale != nullptr;
+    f.f_cs = p.colsum != nullptr;
+    f.f_r = p.R != nullptr;
+    f.r_bf = p.r_bf16 != 0;
+    f.f_beta = p.beta != 0.f;
+    f.c_bf = p.c_bf16 != 0;
+    f.f_c3 = p.C3 != nullptr;
+  } else {
+    f.act = ACT;
+    f.fwd_act = ACT >= STE_ACT_SWISH && ACT <= STE_ACT_RELU;
+    f.f_c2 = (EF & EF_C2) != 0;
+    f.f_z = (EF & EF_Z) != 0;
+    f.f_drop = (EF & EF_DROP) != 0;
+    f.f_rs = (EF & EF_RS) != 0;
+    f.f_cs = (EF & EF_COLSUM) != 0;
+    f.f_r = (EF & EF_R) != 0;
+    f.r_bf = (EF & EF_RBF16) != 0;
+    f.f_beta = (EF & EF_BETA) != 0;
+    f.c_bf = (EF & EF_CBF16) != 0;
+    f.f_c3 = (EF & EF_C3) != 0;
+  }
   return f;
 }
+// global stores one lane issues over a tile's 8 passes on the FULL path (0 = unknown)
+template <int EF>
+constexpr int epi_stores() {
+  if (EF < 0) return 0;
+  return 16 * (((EF & EF_CBF16) ? 1 : 2) + ((EF & EF_C2) ? 1 : 0) + ((EF & EF_C3) ? 1 : 0));
+}
 struct EpiLoads {
-  f32x8 z[4], r[4], c[4];
+  f32x8 z[2], r[2], c[2];
 };
+constexpr int EPI16_FLOATS = 16 * 64;  // one wave's staging slot
 
 template <int EF, int ACT, bool FULL>
-STE_DEV void epi_load32(const ste_gemm_args& p, int row0, int col0, int col1, int batch, int lane, EpiLoads& L) {
+STE_DEV void epi_load16(const ste_gemm_args& p, int row0, int col0, int col1, int batch, int lane, EpiLoads& L) {
   const EpiFlags f = epi_flags_dev<EF, ACT>(p);
   const int cl = (lane & 7) * 8;
   const int col = cl < 32 ? col0 + cl : col1 + (cl - 32);
@@ -280,7 +309,7 @@ STE_DEV void epi_load32(const ste_gemm_args& p, int row0, int col0, int col1, in
   const int64_t offC = (int64_t)batch * p.strideC;
   const int64_t offR = (int64_t)batch * p.strideR;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 2; ++k) {
     const int64_t row = row0 + lr + 8 * k;
     L.z[k] = f32x8{};
     L.r[k] = f32x8{};
@@ -294,27 +323,30 @@ STE_DEV void epi_load32(const ste_gemm_args& p, int row0, int col0, int col1, in
 }
 
 template <int EF, int ACT, bool FULL>
-STE_DEV void epi_store32(const ste_gemm_args& p, const float* epi, int row0, int col0, int col1, int batch,
+STE_DEV void epi_store16(const ste_gemm_args& p, const float* epi, int row0, int col0, int col1, int batch,
                          int lane, f32x8 bias, const EpiLoads& L, Csum& csum) {
   const EpiFlags f = epi_flags_dev<EF, ACT>(p);
-  const int cl = (lane & 7) * 8;
+  const int cg = lane & 7, cl = cg * 8;
   const int col = cl < 32 ? col0 + cl : col1 + (cl - 32);
   const int nval = FULL ? 8 : p.N - col;
   if (!FULL && nval <= 0) return;
   const bool full = FULL || nval >= 8;
   const int lr = lane >> 3;
   const int64_t offC = (int64_t)batch * p.strideC;
-  f32x8 v[4];
+  f32x8 v[2];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float* src = epi + (lr + 8 * k) * EPI_LD + cl;
+  for (int k = 0; k < 2; ++k) {
+    const int row = lr + 8 * k;
+    const int sw = (row >> 1) & 1;  // chunks 2cg, 2cg+1 sit swapped when set
+    const float* src = epi + row * 64 + cl;
     const f32x4 s0 = *reinterpret_cast<const f32x4*>(src), s1 = *reinterpret_cast<const f32x4*>(src + 4);
-    v[k] = f32x8{s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    const f32x4 lo = sw ? s1 : s0, hi = sw ? s0 : s1;
+    v[k] = f32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   }
   const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
   const float inv_keep = f.f_drop ? 1.0f / (1.0f - p.drop_p) : 1.0f;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 2; ++k) {
     const int64_t row = row0 + lr + 8 * k;
     if (!FULL && row >= p.M) continue;
     f32x8 x = (v[k] + bias) * p.alpha;
@@ -636,7 +668,9 @@ namespace ph8 {
 constexpr int NT = 512;
 constexpr int HALF = 16384;                   // 128 rows x 64 k bf16
 constexpr int BUF = 4 * HALF;                 // A0 | A1 | B0 | B1 of one K-tile
-constexpr int LDS_BYTES = 2 * BUF;            // 128 KiB
+constexpr int RING_BYTES = 2 * BUF;           // 128 KiB operand ring
+constexpr int EPI_OFF = RING_BYTES;            // 8 waves x [16][64] fp32 epilogue slots
+constexpr int LDS_BYTES = EPI_OFF + 8 * 16 * 64 * 4;   // 160 KiB
 
 // physical row pr (0..127) of half-tile h -> row of the 256-row tile.  A (G = 64): each
 // 64-row group (one per wave row wm) holds that wave's h-th 64 rows.  B (G = 128): half h
@@ -711,172 +745,52 @@ STE_DEV bf16x8 frag_a_8ph(const char* tile, int rb, int s, int lane) {
 // reads it through ds_read_b64_tr_b16; everything else is shared.
 //
 // Persistent: a grid of min(tiles, CUs) workgroups loops over virtual tiles
-// vb = blockIdx.x, +gridDim.x, ... (same XCD-aware order as one tile per workgroup), so the
-// next tile's operand stream starts right behind this tile's epilogue instead of behind a
-// new workgroup's dispatch.  EF/ACT: compile-time epilogue (epi_pass32).
-template <bool A_KC, bool B_KC, int EF, int ACT>
-__global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
-  using namespace ph8;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int num_m = (p.M + 255) / 256, num_n = (p.N + 255) / 256;
-  const int total = num_m * num_n * p.batch;
-  for (int vb = blockIdx.x; vb < total; vb += gridDim.x) {
-  int batch, tm, tn;
-  map_tile_bid(xcd_remap(vb, total), num_m, num_n, batch, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
-  const bf16* A = (const bf16*)p.A + (int64_t)batch * p.strideA;
-  const bf16* B = (const bf16*)p.B + (int64_t)batch * p.strideB;
+// vb = blockIdx.x, +gridDim.x, ... (same XCD-aware order as one tile per workgroup).
+// Tile hand-over: the next tile's prologue (K-tile 0 + half of K-tile 1, into the operand
+// ring) is issued right after the main loop, BEFORE this tile's epilogue, which stages
+// through its own 32 KiB LDS slots.  The next tile's first vmcnt waits then allow for the
+// epilogue's global stores still in flight (exactly epi_stores<EF>() of them on a FULL
+// tile; 0 = drain everything otherwise), so those stores drain under the next tile's MFMAs
+// instead of stalling its first operand wait.  EF/ACT: compile-time epilogue.
+// bias of this lane's 8 epilogue columns (fp32; zeros past N)
+STE_DEV f32x8 tile_bias(const ste_gemm_args& p, int n0, int wn, int lane) {
+  const int cl = (lane & 7) * 8;
+  const int col = cl < 32 ? n0 + wn * 32 + cl : n0 + 128 + wn * 32 + (cl - 32);
+  const int nval = p.N - col;
+  return nval > 0 ? ld8(p.bias + col, false, nval >= 8, nval) : f32x8{};
+}
 
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = p.K / 64;
-#define STAGE_A(t, h) stage_half<A_KC, 64>(A, p.lda, m0, p.M, (t) * 64, h, smem + ((t) & 1) * BUF + (h) * HALF, wave, lane)
-#define STAGE_B(t, h) \
-  stage_half<B_KC, 128>(B, p.ldb, n0, p.N, (t) * 64, h, smem + ((t) & 1) * BUF + (2 + (h)) * HALF, wave, lane)
-  // prologue: tile 0 complete, tile 1's A0/B0 (the phases (-1,*) of the steady state)
-  STAGE_A(0, 0); STAGE_B(0, 0); STAGE_B(0, 1); STAGE_A(0, 1);
-  if (nk > 1) {
-    STAGE_A(1, 0); STAGE_B(1, 0);
-    STE_VMCNT(8);
-  } else {
-    STE_VMCNT(0);
-  }
-  STE_BARRIER();
-
-  bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
-  // Ping-pong: waves 4-7 run one barrier behind waves 0-3, so on every SIMD (one wave of
-  // each group) one wave's MFMA cluster overlaps the other's ds_reads + staging.  Buffer
-  // safety holds with the extra barrier of skew (reads stay >= 1 phase after the retiring
-  // wait+barrier of every producer, restaging >= 2 phases after the last read).
-  if (wm == 1) STE_BARRIER();
-  for (int t = 0; t < nk; ++t) {
-    const char* buf = smem + (t & 1) * BUF;
-    const bool tail = t + 2 >= nk;  // fewer stages in flight: drain fully instead of counting
-    // ---- phase 0
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) b0[j][s] = frag_b_8ph<B_KC>(buf + 2 * HALF, wn * 32 + j * 16, s, lane);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) a0[i][s] = frag_a_8ph<A_KC>(buf, wm * 64 + i * 16, s, lane);
-    if (t + 1 < nk) STAGE_B(t + 1, 1);
-    if (tail) STE_VMCNT(0); else STE_VMCNT(8);
-    STE_BARRIER();
-    STE_LDS_SYNC(!A_KC || !B_KC);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(a0[i][s], b0[j][s], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    STE_BARRIER();
-    // ---- phase 1
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) b1[j][s] = frag_b_8ph<B_KC>(buf + 3 * HALF, wn * 32 + j * 16, s, lane);
-    if (t + 1 < nk) STAGE_A(t + 1, 1);
-    if (tail) STE_VMCNT(0); else STE_VMCNT(8);
-    STE_BARRIER();
-    STE_LDS_SYNC(!B_KC);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(a0[i][s], b1[j][s], acc[i][2 + j]);
-    __builtin_amdgcn_s_setprio(0);
-    STE_BARRIER();
-    // ---- phase 2
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) a1[i][s] = frag_a_8ph<A_KC>(buf + HALF, wm * 64 + i * 16, s, lane);
-    if (t + 2 < nk) STAGE_A(t + 2, 0);
-    STE_BARRIER();
-    STE_LDS_SYNC(!A_KC);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(a1[i][s], b1[j][s], acc[4 + i][2 + j]);
-    __builtin_amdgcn_s_setprio(0);
-    STE_BARRIER();
-    // ---- phase 3
-    if (t + 2 < nk) STAGE_B(t + 2, 0);
-    if (tail) STE_VMCNT(0); else STE_VMCNT(8);
-    STE_BARRIER();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(a1[i][s], b0[j][s], acc[4 + i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    STE_BARRIER();
-  }
-#undef STAGE_A
-#undef STAGE_B
-#undef STE_LDS_SYNC
-  if (wm == 0) STE_BARRIER();  // re-align the groups (equal barrier counts) before the LDS epilogue
-
-  // epilogue: acc[i][j] = rows wm*128 + i*16, cols (j >> 1)*128 + wn*32 + (j & 1)*16;
-  // 4 passes of 32 rows x 64 columns per wave through LDS
-  float* epi = reinterpret_cast<float*>(smem) + wave * big::EPI_ROWS * EPI_LD;
+// acc[i][j] = rows wm*128 + i*16, cols (j >> 1)*128 + wn*32 + (j & 1)*16: 8 passes of
+// 16 rows x 64 columns through the wave's own LDS slot; straight-line code per FULL value.
+template <int EF, int ACT, bool FULL>
+STE_DEV void epilogue_8ph(const ste_gemm_args& p, const f32x4 (&acc)[8][4], float* epi, int m0, int n0, int batch,
+                          int wm, int wn, int lane, f32x8 bias) {
   Csum csum = {};
-  const bool full_tile = m0 + 256 <= p.M && n0 + 256 <= p.N;
-  f32x8 bias = f32x8{};
-  if (EF >= 0 && (EF & EF_BIAS) != 0) {
-    const int cl = (lane & 7) * 8;
-    const int col = cl < 32 ? n0 + wn * 32 + cl : n0 + 128 + wn * 32 + (cl - 32);
-    const int nval = p.N - col;
-    if (nval > 0) bias = ld8(p.bias + col, false, nval >= 8, nval);
-  }
-#define STE_EPI_STAGE(PS)                                                                                   \
-  {                                                                                                          \
-    for (int ii = 0; ii < 2; ++ii) {                                                                         \
-      _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                                        \
-        _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                                      \
-          epi[(ii * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[2 * (PS) + ii][j][r];   \
-        }                                                                                                    \
-      }                                                                                                      \
-    }                                                                                                        \
-    __builtin_amdgcn_s_waitcnt(0xc07f);                                                                      \
-    __builtin_amdgcn_wave_barrier();                                                                         \
-  }
-#define STE_EPI_ROW0(PS) (m0 + wm * 128 + (PS) * 32)
-#define STE_EPI_LOAD(PS, L)                                                                                  \
-  if (full_tile) epi_load32<EF, ACT, true>(p, STE_EPI_ROW0(PS), c0, c1, batch, lane, L);                     \
-  else epi_load32<EF, ACT, false>(p, STE_EPI_ROW0(PS), c0, c1, batch, lane, L);
-#define STE_EPI_STORE(PS, L)                                                                                 \
-  if (full_tile) epi_store32<EF, ACT, true>(p, epi, STE_EPI_ROW0(PS), c0, c1, batch, lane, bias, L, csum);  \
-  else epi_store32<EF, ACT, false>(p, epi, STE_EPI_ROW0(PS), c0, c1, batch, lane, bias, L, csum);           \
-  __builtin_amdgcn_s_waitcnt(0xc07f);                                                                        \
-  __builtin_amdgcn_wave_barrier();
   const int c0 = n0 + wn * 32, c1 = n0 + 128 + wn * 32;
+#define STE_EPI_STAGE(PS)                                                                       \
+  {                                                                                             \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                             \
+      _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                           \
+        const int row = (lane >> 4) * 4 + r, chunk = (4 * j + ((lane & 15) >> 2)) ^ ((r >> 1) & 1); \
+        epi[row * 64 + chunk * 4 + (lane & 3)] = acc[PS][j][r];                                 \
+      }                                                                                         \
+    }                                                                                           \
+    __builtin_amdgcn_s_waitcnt(0xc07f);                                                         \
+    __builtin_amdgcn_wave_barrier();                                                            \
+  }
+#define STE_EPI_ROW0(PS) (m0 + wm * 128 + (PS) * 16)
+#define STE_EPI_LOAD(PS, L) epi_load16<EF, ACT, FULL>(p, STE_EPI_ROW0(PS), c0, c1, batch, lane, L);
+#define STE_EPI_STORE(PS, L)                                                                    \
+  epi_store16<EF, ACT, FULL>(p, epi, STE_EPI_ROW0(PS), c0, c1, batch, lane, bias, L, csum);     \
+  __builtin_amdgcn_s_waitcnt(0xc07f);                                                           \
+  __builtin_amdgcn_wave_barrier();
   if constexpr (EF < 0) {
-#define STE_EPI_G(PS)                                                                                        \
-    STE_EPI_STAGE(PS)                                                                                        \
-    epilogue_tile(p, epi, 32, STE_EPI_ROW0(PS), c0, c1, batch, lane, csum);                                  \
-    __builtin_amdgcn_s_waitcnt(0xc07f);                                                                      \
+#define STE_EPI_G(PS)                                                                           \
+    STE_EPI_STAGE(PS)                                                                           \
+    epilogue_tile(p, epi, 16, STE_EPI_ROW0(PS), c0, c1, batch, lane, csum, 64, true);           \
+    __builtin_amdgcn_s_waitcnt(0xc07f);                                                         \
     __builtin_amdgcn_wave_barrier();
-    STE_EPI_G(0) STE_EPI_G(1) STE_EPI_G(2) STE_EPI_G(3)
+    STE_EPI_G(0) STE_EPI_G(1) STE_EPI_G(2) STE_EPI_G(3) STE_EPI_G(4) STE_EPI_G(5) STE_EPI_G(6) STE_EPI_G(7)
 #undef STE_EPI_G
   } else {
     EpiLoads L0, L1;
@@ -884,18 +798,186 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
     STE_EPI_STAGE(0) STE_EPI_LOAD(1, L1) STE_EPI_STORE(0, L0)
     STE_EPI_STAGE(1) STE_EPI_LOAD(2, L0) STE_EPI_STORE(1, L1)
     STE_EPI_STAGE(2) STE_EPI_LOAD(3, L1) STE_EPI_STORE(2, L0)
-    STE_EPI_STAGE(3) STE_EPI_STORE(3, L1)
+    STE_EPI_STAGE(3) STE_EPI_LOAD(4, L0) STE_EPI_STORE(3, L1)
+    STE_EPI_STAGE(4) STE_EPI_LOAD(5, L1) STE_EPI_STORE(4, L0)
+    STE_EPI_STAGE(5) STE_EPI_LOAD(6, L0) STE_EPI_STORE(5, L1)
+    STE_EPI_STAGE(6) STE_EPI_LOAD(7, L1) STE_EPI_STORE(6, L0)
+    STE_EPI_STAGE(7) STE_EPI_STORE(7, L1)
   }
 #undef STE_EPI_STAGE
 #undef STE_EPI_ROW0
 #undef STE_EPI_LOAD
 #undef STE_EPI_STORE
-  if (EF < 0 ? p.colsum != nullptr : (EF & EF_COLSUM) != 0)
-    colsum_flush(p, csum, n0 + wn * 32, n0 + 128 + wn * 32, batch, lane);
-  // every wave's epilogue LDS reads are done (lgkmcnt(0) above) before the next tile's
-  // prologue restages the ring over the staging area
-  STE_BARRIER();
+  if (EF < 0 ? p.colsum != nullptr : (EF & EF_COLSUM) != 0) colsum_flush(p, csum, c0, c1, batch, lane);
+}
+
+template <int E>
+STE_DEV void vm_wait8(int extra) {
+  if (E > 0 && extra) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + E) : "memory");
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+template <bool A_KC, bool B_KC, int EF, int ACT>
+__global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
+  using namespace ph8;
+  constexpr int E_ST = epi_stores<EF>();
+  static_assert(8 + E_ST <= 63, "vmcnt immediate");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int num_m = (p.M + 255) / 256, num_n = (p.N + 255) / 256;
+  const int total = num_m * num_n * p.batch;
+  const int nk = p.K / 64;
+  int vb = blockIdx.x;
+  if (vb >= total) return;
+  int batch, tm, tn;
+  map_tile_bid(xcd_remap(vb, total), num_m, num_n, batch, tm, tn);
+  int m0 = tm * 256, n0 = tn * 256;
+  const bf16* A = (const bf16*)p.A + (int64_t)batch * p.strideA;
+  const bf16* B = (const bf16*)p.B + (int64_t)batch * p.strideB;
+#define STAGE_A(t, h) stage_half<A_KC, 64>(A, p.lda, m0, p.M, (t) * 64, h, smem + ((t) & 1) * BUF + (h) * HALF, wave, lane)
+#define STAGE_B(t, h) \
+  stage_half<B_KC, 128>(B, p.ldb, n0, p.N, (t) * 64, h, smem + ((t) & 1) * BUF + (2 + (h)) * HALF, wave, lane)
+#define STAGE_PROLOGUE()                                        \
+  {                                                             \
+    STAGE_A(0, 0); STAGE_B(0, 0); STAGE_B(0, 1); STAGE_A(0, 1); \
+    if (nk > 1) { STAGE_A(1, 0); STAGE_B(1, 0); }               \
   }
+  // prologue of the first tile: tile 0 complete, tile 1's A0/B0 (phases (-1,*) of the steady state)
+  STAGE_PROLOGUE();
+  int extra = 0;  // stores of the previous tile's epilogue issued after this prologue (FULL tiles)
+  float* epi = reinterpret_cast<float*>(smem + EPI_OFF) + wave * EPI16_FLOATS;
+  constexpr bool EPI_OVL = EF >= 0 && (EF & (EF_Z | EF_R | EF_BETA | EF_COLSUM | EF_RS)) == 0;
+  f32x8 bias = f32x8{};
+  if (EF >= 0 && (EF & EF_BIAS) != 0) bias = tile_bias(p, n0, wn, lane);
+
+  for (;;) {
+    if (nk > 1) vm_wait8<E_ST>(extra);
+    else STE_VMCNT(0);
+    STE_BARRIER();
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
+    // Ping-pong: waves 4-7 run one barrier behind waves 0-3, so on every SIMD (one wave of
+    // each group) one wave's MFMA cluster overlaps the other's ds_reads + staging.  Buffer
+    // safety holds with the extra barrier of skew (reads stay >= 1 phase after the retiring
+    // wait+barrier of every producer, restaging >= 2 phases after the last read).
+    if (wm == 1) STE_BARRIER();
+    for (int t = 0; t < nk; ++t) {
+      const char* buf = smem + (t & 1) * BUF;
+      const bool tail = t + 2 >= nk;  // fewer stages in flight: drain fully instead of counting
+      const int ex = t == 0 ? extra : 0;
+      // ---- phase 0
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) b0[j][s] = frag_b_8ph<B_KC>(buf + 2 * HALF, wn * 32 + j * 16, s, lane);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) a0[i][s] = frag_a_8ph<A_KC>(buf, wm * 64 + i * 16, s, lane);
+      if (t + 1 < nk) STAGE_B(t + 1, 1);
+      if (tail) STE_VMCNT(0); else vm_wait8<E_ST>(ex);
+      STE_BARRIER();
+      STE_LDS_SYNC(!A_KC || !B_KC);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(a0[i][s], b0[j][s], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      STE_BARRIER();
+      // ---- phase 1
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) b1[j][s] = frag_b_8ph<B_KC>(buf + 3 * HALF, wn * 32 + j * 16, s, lane);
+      if (t + 1 < nk) STAGE_A(t + 1, 1);
+      if (tail) STE_VMCNT(0); else vm_wait8<E_ST>(ex);
+      STE_BARRIER();
+      STE_LDS_SYNC(!B_KC);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(a0[i][s], b1[j][s], acc[i][2 + j]);
+      __builtin_amdgcn_s_setprio(0);
+      STE_BARRIER();
+      // ---- phase 2
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) a1[i][s] = frag_a_8ph<A_KC>(buf + HALF, wm * 64 + i * 16, s, lane);
+      if (t + 2 < nk) STAGE_A(t + 2, 0);
+      STE_BARRIER();
+      STE_LDS_SYNC(!A_KC);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(a1[i][s], b1[j][s], acc[4 + i][2 + j]);
+      __builtin_amdgcn_s_setprio(0);
+      STE_BARRIER();
+      // ---- phase 3
+      if (t + 2 < nk) STAGE_B(t + 2, 0);
+      if (tail) STE_VMCNT(0); else vm_wait8<E_ST>(ex);
+      STE_BARRIER();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(a1[i][s], b0[j][s], acc[4 + i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      STE_BARRIER();
+    }
+    if (wm == 0) STE_BARRIER();  // re-align the groups (equal barrier counts): every ring read is done
+
+    // ---- hand-over to the next tile.  Load-free epilogues (EPI_OVL) issue the next tile's
+    // prologue first and let their stores drain under its first K-tile; epilogues that read
+    // Z / R / beta*C run first (their loads must not queue behind the prologue's DMA).
+    const int em0 = m0, en0 = n0, ebatch = batch;
+    const int vb_next = vb + gridDim.x;
+    const bool more = vb_next < total;
+    const bool full_tile = em0 + 256 <= p.M && en0 + 256 <= p.N;
+    asm volatile("" : "+v"(bias));  // bias landed long ago (the main loop drained vmcnt): no waits below
+    auto next_prologue = [&]() {
+      if (more) {
+        map_tile_bid(xcd_remap(vb_next, total), num_m, num_n, batch, tm, tn);
+        m0 = tm * 256;
+        n0 = tn * 256;
+        A = (const bf16*)p.A + (int64_t)batch * p.strideA;
+        B = (const bf16*)p.B + (int64_t)batch * p.strideB;
+        STAGE_PROLOGUE();
+      }
+    };
+    if (EPI_OVL) next_prologue();
+    if (full_tile) epilogue_8ph<EF, ACT, true>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias);
+    else epilogue_8ph<EF, ACT, false>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias);
+    if (!EPI_OVL) next_prologue();
+    if (!more) break;
+    vb = vb_next;
+    extra = (EPI_OVL && full_tile) ? 1 : 0;
+    if (EF >= 0 && (EF & EF_BIAS) != 0) bias = tile_bias(p, n0, wn, lane);
+  }
+#undef STAGE_A
+#undef STAGE_B
+#undef STAGE_PROLOGUE
+#undef STE_LDS_SYNC
 }
 #undef STE_EPI_PASS
 
