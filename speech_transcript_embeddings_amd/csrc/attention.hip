@@ -1285,6 +1285,53 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel2_kernel(ste_attn_args 
   }
 }
 
+// ============================== dE[j][d] += scale * Σ_(b,h,t) G[(b,h,t)][j] · Q[b*T+t][h*64+d]
+// One block per (batch, head): its T rows of G (fp32 [T][80]) and Q (bf16 columns h*64..)
+// are staged 64 rows at a time; 256 threads each own 20 of the 80 x 64 outputs (j = tid/16
+// + 16k, d = 4*(tid%16)..+3) and accumulate in fp32; one atomic add per output per block.
+__global__ __launch_bounds__(256) void attn_rel_dE2_kernel(ste_attn_args a) {
+  __shared__ float sG[64][NREL + 4];
+  __shared__ float sQ[64][HD];
+  const int tid = threadIdx.x;
+  const int bh = blockIdx.x, h = bh % a.H, b = bh / a.H;
+  const int T = a.T;
+  const int nrel = a.rel_left + a.rel_right + 1;
+  const int jr = tid >> 4, d0 = (tid & 15) * 4;
+  f32x4 acc[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* G = a.gwork + (int64_t)bh * T * NREL;
+  const bf16* Q = (const bf16*)a.q + (int64_t)b * T * a.ldq + h * HD;
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int nr = min(64, T - t0);
+    __syncthreads();
+    for (int i = tid; i < 64 * (NREL / 4); i += 256) {
+      const int r = i / (NREL / 4), c = (i % (NREL / 4)) * 4;
+      const f32x4 v = r < nr ? *reinterpret_cast<const f32x4*>(G + (int64_t)(t0 + r) * NREL + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(&sG[r][c]) = v;
+    }
+    for (int i = tid; i < 64 * (HD / 8); i += 256) {
+      const int r = i / (HD / 8), c = (i % (HD / 8)) * 8;
+      const bf16x8 v = r < nr ? *reinterpret_cast<const bf16x8*>(Q + (int64_t)(t0 + r) * a.ldq + c) : bf16x8{};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sQ[r][c + e] = (float)v[e];
+    }
+    __syncthreads();
+    for (int r = 0; r < nr; ++r) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(&sQ[r][d0]);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) acc[k] += q * sG[r][jr + 16 * k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int j = jr + 16 * k;
+    if (j < nrel)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomicAdd(a.dE + j * HD + d0 + e, acc[k][e] * a.scale);
+  }
+}
+
 constexpr int FWD_LDS = 4 * TILE + NREL * 128 + 4 * 16 * NREL * 4 + 2 * 64 * 4;
 constexpr int DQ_LDS = 2 * TILE + 96 * 128 + 4 * 16 * NREL * 4 + 4 * 16 * 96 * 4 + 64 * 4;
 constexpr int DKV_LDS = 4 * TILE + NREL * 128 + 64 * NREL * 4 + 2 * 128 * 4;
@@ -1347,9 +1394,7 @@ extern "C" int ste_attention_bwd(const ste_attn_args* a, void* stream) {
     hipLaunchKernelGGL(attn_bwd_dkv_rel2_kernel, gk, dim3(NT), rel2::DKV_LDS, s, *a);
     STE_CHECK_LAUNCH();
     if (a->dE) {
-      const int blocks = 512;
-      int64_t rpb = (nrow + blocks - 1) / blocks;
-      hipLaunchKernelGGL(attn_rel_dE_kernel, dim3(blocks), dim3(256), 0, s, *a, rpb);
+      hipLaunchKernelGGL(attn_rel_dE2_kernel, dim3((unsigned)(a->B * a->H)), dim3(256), 0, s, *a);
       STE_CHECK_LAUNCH();
     }
     return 0;
