@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--tokens", type=int, default=64)
     ap.add_argument("--unfreeze", type=int, default=3)
     ap.add_argument("--align", action="store_true", help="config 4: word-alignment head")
+    ap.add_argument("--freeze", default="partial", choices=["partial", "none", "full"],
+                    help="freeze_encoders (config 5 = none: every encoder layer trainable)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=1)
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -133,7 +135,8 @@ def main():
     from speech_transcript_embeddings_amd.train import TrainStep, synthetic_batch
 
     model = EnhancedAudioTextModel(use_word_alignment=args.align, text_layers_to_unfreeze=args.unfreeze,
-                                   audio_layers_to_unfreeze=args.unfreeze, device=f"cuda:{local}")
+                                   audio_layers_to_unfreeze=args.unfreeze, freeze_encoders=args.freeze,
+                                   device=f"cuda:{local}")
     model.audio_cfg.layerdrop = 0.0
     step = TrainStep(model, warmup=100, total_steps=100000)
     B, nsamp, L = args.batch, int(args.seconds * 16000), args.tokens
@@ -171,7 +174,14 @@ def main():
     achieved = fl / tm / 1e12
     gemm_time = sum(a[2] for a in agg.values()) / args.steps
     pairs = world * B * args.steps / elapsed
-    gflop = GFLOP_PER_PAIR.get(args.unfreeze, 1370.4)
+    # SURVEY §8(d) algorithmic FLOPs per pair exist for the 10 s / 64-token configs c2/c3 (3
+    # unfrozen layers) and c4 (5 + alignment head); other shapes report no step fraction
+    known = args.seconds == 10.0 and args.tokens == 64 and args.freeze == "partial" and \
+        (args.unfreeze, args.align) in ((3, False), (5, True))
+    gflop = GFLOP_PER_PAIR[args.unfreeze] if known else None
+    cname = {(3, False): "c2" if world == 1 else "c3", (5, True): "c4"}.get((args.unfreeze, args.align), "custom") \
+        if args.seconds == 10.0 and args.freeze == "partial" else ("c5-shape (bf16 GEMMs)" if args.freeze == "none"
+                                                                    else "custom")
     traffic, traffic_src = hbm_traffic(dom)
     out = {
         "metric": "audio–text pairs/sec (whole node), 10s@16kHz + 64-tok, 1/2/4/8 MI355X",
@@ -179,13 +189,14 @@ def main():
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (SURVEY §8d waveforms + token ids), random-init weights",
-        "config": {"workload": f"c2 per GPU: {B} pairs x ({args.seconds:g}s@16kHz audio + {L}-tok clean + {L}-tok "
-                               f"corrupt), w2v-bert-2.0 Conformer 24L + XLM-R-base 12L, {args.unfreeze}+"
-                               f"{args.unfreeze} unfrozen{', alignment head' if args.align else ''}; GPU fbank -> "
+        "config": {"workload": f"{cname} per GPU: {B} pairs x ({args.seconds:g}s@16kHz audio + {L}-tok clean + "
+                               f"{L}-tok corrupt), w2v-bert-2.0 Conformer 24L + XLM-R-base 12L, "
+                               f"{'all layers trainable' if args.freeze == 'none' else f'{args.unfreeze}+{args.unfreeze} unfrozen'}"
+                               f"{', alignment head' if args.align else ''}; GPU fbank -> "
                                f"fwd -> InfoNCE -> bwd -> allreduce -> clip+AdamW",
                    "global_batch": world * B, "local_batch": B, "seq_len_audio_frames": ((1 + (nsamp - 400) // 160) + 1) // 2,
                    "seq_len_text": L, "parallelism": f"dp{world}"},
-        "step_roofline_frac": round(pairs * gflop / (world * BF16_PEAK_TFLOPS * 1e3), 4),
+        "step_roofline_frac": round(pairs * gflop / (world * BF16_PEAK_TFLOPS * 1e3), 4) if gflop else None,
         "roofline": {"bound": "mfma", "kernel": dom, "launches_per_step": n_l // args.steps,
                      "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
