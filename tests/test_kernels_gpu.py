@@ -202,10 +202,10 @@ def test_attention_text(ops, drop_p):
 
 
 # ---------------------------------------------------------------- conv
-@pytest.mark.parametrize("T", [37, 150])
-def test_glu_dwconv(ops, T):
+@pytest.mark.parametrize("T,Cc", [(37, 128), (150, 128), (37, 256), (499, 512), (300, 1024)])
+def test_glu_dwconv(ops, T, Cc):
     torch.manual_seed(T)
-    B, Cc = 2, 128
+    B = 2
     pre = torch.randn(B * T, 2 * Cc, device=DEV).bfloat16()
     w = torch.randn(Cc, 31, device=DEV) * 0.2
     out = torch.empty(B * T, Cc, device=DEV, dtype=torch.bfloat16)
