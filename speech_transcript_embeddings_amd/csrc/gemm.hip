@@ -706,6 +706,15 @@ STE_DEV void stage_half(const bf16* base, int64_t ld, int row0, int rows, int k0
 }  // namespace ph8
 
 #define STE_BARRIER() asm volatile("s_barrier" ::: "memory")
+// MFMA-cluster priority: default raises it around every cluster; STE_PRIO_STATIC (experiment
+// builds) instead gives the second-dispatched wave group (waves 4-7) a static priority of 1
+#ifdef STE_PRIO_STATIC
+#define STE_PRIO_HI()
+#define STE_PRIO_LO()
+#else
+#define STE_PRIO_HI() __builtin_amdgcn_s_setprio(1)
+#define STE_PRIO_LO() __builtin_amdgcn_s_setprio(0)
+#endif
 #define STE_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
 // KM fragment through inline-asm ds_read_b64_tr_b16.  The builtin form makes hipcc's
@@ -869,6 +878,9 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
     // safety holds with the extra barrier of skew (reads stay >= 1 phase after the retiring
     // wait+barrier of every producer, restaging >= 2 phases after the last read).
     if (wm == 1) STE_BARRIER();
+#ifdef STE_PRIO_STATIC
+    if (wm == 1) __builtin_amdgcn_s_setprio(1);
+#endif
     for (int t = 0; t < nk; ++t) {
       const char* buf = smem + (t & 1) * BUF;
       const bool tail = t + 2 >= nk;  // fewer stages in flight: drain fully instead of counting
@@ -887,14 +899,14 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
       if (tail) STE_VMCNT(0); else vm_wait8<E_ST>(ex);
       STE_BARRIER();
       STE_LDS_SYNC(!A_KC || !B_KC);
-      __builtin_amdgcn_s_setprio(1);
+      STE_PRIO_HI();
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(a0[i][s], b0[j][s], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
+      STE_PRIO_LO();
       STE_BARRIER();
       // ---- phase 1
 #pragma unroll
@@ -905,14 +917,14 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
       if (tail) STE_VMCNT(0); else vm_wait8<E_ST>(ex);
       STE_BARRIER();
       STE_LDS_SYNC(!B_KC);
-      __builtin_amdgcn_s_setprio(1);
+      STE_PRIO_HI();
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(a0[i][s], b1[j][s], acc[i][2 + j]);
-      __builtin_amdgcn_s_setprio(0);
+      STE_PRIO_LO();
       STE_BARRIER();
       // ---- phase 2
 #pragma unroll
@@ -922,27 +934,27 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
       if (t + 2 < nk) STAGE_A(t + 2, 0);
       STE_BARRIER();
       STE_LDS_SYNC(!A_KC);
-      __builtin_amdgcn_s_setprio(1);
+      STE_PRIO_HI();
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(a1[i][s], b1[j][s], acc[4 + i][2 + j]);
-      __builtin_amdgcn_s_setprio(0);
+      STE_PRIO_LO();
       STE_BARRIER();
       // ---- phase 3
       if (t + 2 < nk) STAGE_B(t + 2, 0);
       if (tail) STE_VMCNT(0); else vm_wait8<E_ST>(ex);
       STE_BARRIER();
-      __builtin_amdgcn_s_setprio(1);
+      STE_PRIO_HI();
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(a1[i][s], b0[j][s], acc[4 + i][j]);
-      __builtin_amdgcn_s_setprio(0);
+      STE_PRIO_LO();
       STE_BARRIER();
     }
     if (wm == 0) STE_BARRIER();  // re-align the groups (equal barrier counts): every ring read is done
