@@ -190,7 +190,9 @@ class Engine:
                             out_bf16=True, colsum=s.g(pre + "ffn2.intermediate_dense.bias"))
         if tr:
             self._dw(dx4b, sv["h2"], pre + "ffn2.output_dense.weight")
-        da5 = ops.linear_dx(dz2, s.w(pre + "ffn2.intermediate_dense.weight"))
+        # dX GEMMs feeding an LN backward leave bf16 (as under the reference's bf16 autocast, whose
+        # Linear backward returns a bf16 input gradient); the residual-stream gradient stays fp32
+        da5 = ops.linear_dx(dz2, s.w(pre + "ffn2.intermediate_dense.weight"), out_bf16=True)
         if tr:
             self._dw(dz2, sv["a5"], pre + "ffn2.intermediate_dense.weight")
         del dz2
@@ -200,7 +202,7 @@ class Engine:
                      drop_p=sv["p_conv"], seed=_site_seed(sv["seed"], 1))
         del da5, dx4, dx4b
         # conv module
-        dsw = ops.linear_dx(dx3b, s.w(pre + "conv_module.pointwise_conv2.weight"))
+        dsw = ops.linear_dx(dx3b, s.w(pre + "conv_module.pointwise_conv2.weight"), out_bf16=True)
         if tr:
             self._dw(dx3b, sv["sw"], pre + "conv_module.pointwise_conv2.weight")
         dcv = self._e(M, D, dtype=BF16)
@@ -211,7 +213,7 @@ class Engine:
         ops.glu_dwconv_bwd(sv["pw1"], s.p(pre + "conv_module.depthwise_conv.weight").view(D, -1), dcv, dpw1,
                            None if gdw is None else gdw.view(D, -1), b, T)
         del dcv
-        da3 = ops.linear_dx(dpw1, s.w(pre + "conv_module.pointwise_conv1.weight"))
+        da3 = ops.linear_dx(dpw1, s.w(pre + "conv_module.pointwise_conv1.weight"), out_bf16=True)
         if tr:
             self._dw(dpw1, sv["a3"], pre + "conv_module.pointwise_conv1.weight")
         del dpw1
@@ -236,7 +238,7 @@ class Engine:
                           rel_left=c.left_max_position_embeddings, rel_right=c.right_max_position_embeddings,
                           scale=1.0 / math.sqrt(D // H), dE=gE, gwork=gwork)
         del do, delta, gwork
-        da2 = ops.linear_dx(dqkv, s.fused(pre + "self_attn.linear_q.weight", 3, "w"))
+        da2 = ops.linear_dx(dqkv, s.fused(pre + "self_attn.linear_q.weight", 3, "w"), out_bf16=True)
         if tr:
             self._dw(dqkv, sv["a2"], pre + "self_attn.linear_q.weight", fused=3)
             self._db(dqkv, pre + "self_attn.linear_q.bias", fused=3)
@@ -251,7 +253,7 @@ class Engine:
                             out_bf16=True, colsum=s.g(pre + "ffn1.intermediate_dense.bias"))
         if tr:
             self._dw(dx1b, sv["h1"], pre + "ffn1.output_dense.weight")
-        da1 = ops.linear_dx(dz1, s.w(pre + "ffn1.intermediate_dense.weight"))
+        da1 = ops.linear_dx(dz1, s.w(pre + "ffn1.intermediate_dense.weight"), out_bf16=True)
         if tr:
             self._dw(dz1, sv["a1"], pre + "ffn1.intermediate_dense.weight")
         del dz1
