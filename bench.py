@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 BF16_PEAK_TFLOPS = 2516.6          # MI355X dense bf16 MFMA (256 CU x 4096 FLOP/clk x 2.4 GHz)
 GFLOP_PER_PAIR = {3: 1370.4, 5: 1429.5}   # SURVEY §8(d) algorithmic fwd+bwd FLOPs per pair (c2/c3, c4)
+GFLOP_FWD_PER_PAIR = 641.8                 # SURVEY §8(d) forward only: 615.1 audio + 21.7 text + ≈5 heads
 
 
 def parse():
@@ -47,6 +48,9 @@ def parse():
     ap.add_argument("--align", action="store_true", help="config 4: word-alignment head")
     ap.add_argument("--freeze", default="partial", choices=["partial", "none", "full"],
                     help="freeze_encoders (config 5 = none: every encoder layer trainable)")
+    ap.add_argument("--eval", action="store_true",
+                    help="time the forward-only evaluation step (SURVEY §8f rank 1, ref evaluate() :1165-1284): "
+                         "GPU fbank -> forward without saved activations -> similarity + InfoNCE value")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=1)
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -74,6 +78,9 @@ def cpu_baseline(args):
     v = {n: torch.zeros_like(t) for n, t in p.items() if t.requires_grad}
 
     def one_step(step):
+        if args.eval:
+            with torch.no_grad():
+                return forward_only()
         feats = [fbank_ref.extract(fbank_ref.synth_wave(1000 + i, N))[0] for i in range(B)]
         f, am = fbank_ref.collate(feats)
         ids = torch.randint(5, 250000, (B, L))
@@ -97,15 +104,26 @@ def cpu_baseline(args):
                 t.copy_(t2)
                 t.grad = None
 
+    def forward_only():
+        feats = [fbank_ref.extract(fbank_ref.synth_wave(1000 + i, N))[0] for i in range(B)]
+        f, am = fbank_ref.collate(feats)
+        ids = torch.randint(5, 250000, (B, L))
+        mask = torch.ones(B, L, dtype=torch.long)
+        batch = {"input_ids_pos": ids, "attention_mask_pos": mask, "input_ids_neg": ids.clone(),
+                 "attention_mask_neg": mask, "input_values": torch.from_numpy(f), "attention_mask_audio": torch.from_numpy(am)}
+        R.step_loss(p, batch, cfg)
+
     one_step(1)
     t0 = time.perf_counter()
     for s in range(args.cpu_steps):
         one_step(2 + s)
     dt = (time.perf_counter() - t0) / args.cpu_steps
+    what = "forward-only evaluation step (numpy fbank + forward + loss, no_grad)" if args.eval else \
+        "full train step incl. numpy fbank + AdamW"
     return {"value": round(B / dt, 4), "unit": "audio-text pairs/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ (CPU fp32 torch restatement pinned to the reference) full train step incl. numpy "
-                      f"fbank + AdamW, {args.seconds:g} s clips + {L}-token transcripts, {args.unfreeze} unfrozen "
-                      f"layers, batch {B}, {args.cpu_steps} timed steps after 1 warmup, {dt:.2f} s/step"}
+            "sample": f"oracle/ (CPU fp32 torch restatement pinned to the reference) {what}, {args.seconds:g} s clips "
+                      f"+ {L}-token transcripts, {args.unfreeze} unfrozen layers, batch {B}, {args.cpu_steps} timed "
+                      f"steps after 1 warmup, {dt:.2f} s/step"}
 
 
 def hbm_traffic(kernel):
@@ -141,16 +159,31 @@ def main():
     step = TrainStep(model, warmup=100, total_steps=100000)
     B, nsamp, L = args.batch, int(args.seconds * 16000), args.tokens
     data = synthetic_batch(B, nsamp, L, device=f"cuda:{local}", rank=rank)
+    if args.eval:
+        from speech_transcript_embeddings_amd.evaluate import EvalStep
+        model.eval()
+        ev = EvalStep(model, 0.1, 0.5)
+        wav, lens, ids_p, m_p, ids_n, m_n = data
+
+        def eval_step(*_):
+            feats, amask = step.features(wav, lens)
+            sp, sn, lo = ev({"input_ids_pos": ids_p, "attention_mask_pos": m_p, "input_ids_neg": ids_n,
+                             "attention_mask_neg": m_n, "input_values": feats, "attention_mask_audio": amask})
+            step.last = {"loss": lo, "s_pos": sp, "s_neg": sn}
+            return lo
+        run = eval_step
+    else:
+        run = step
 
     for _ in range(args.warmup):
-        step(*data)
+        run(*data)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     ops.GEMM_TRACE = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(*data)
+        run(*data)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -178,13 +211,14 @@ def main():
     # unfrozen layers) and c4 (5 + alignment head); other shapes report no step fraction
     known = args.seconds == 10.0 and args.tokens == 64 and args.freeze == "partial" and \
         (args.unfreeze, args.align) in ((3, False), (5, True))
-    gflop = GFLOP_PER_PAIR[args.unfreeze] if known else None
+    gflop = (GFLOP_FWD_PER_PAIR if args.eval else GFLOP_PER_PAIR[args.unfreeze]) if known else None
     cname = {(3, False): "c2" if world == 1 else "c3", (5, True): "c4"}.get((args.unfreeze, args.align), "custom") \
         if args.seconds == 10.0 and args.freeze == "partial" else ("c5-shape (bf16 GEMMs)" if args.freeze == "none"
                                                                     else "custom")
     traffic, traffic_src = hbm_traffic(dom)
     out = {
-        "metric": "audio–text pairs/sec (whole node), 10s@16kHz + 64-tok, 1/2/4/8 MI355X",
+        "metric": ("evaluated audio–text pairs/sec, forward only (whole node), 10s@16kHz + 64-tok" if args.eval else
+                   "audio–text pairs/sec (whole node), 10s@16kHz + 64-tok, 1/2/4/8 MI355X"),
         "value": round(pairs, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16",
@@ -193,7 +227,8 @@ def main():
                                f"{L}-tok corrupt), w2v-bert-2.0 Conformer 24L + XLM-R-base 12L, "
                                f"{'all layers trainable' if args.freeze == 'none' else f'{args.unfreeze}+{args.unfreeze} unfrozen'}"
                                f"{', alignment head' if args.align else ''}; GPU fbank -> "
-                               f"fwd -> InfoNCE -> bwd -> allreduce -> clip+AdamW",
+                               + ("fwd (no saved activations, eval mode) -> similarity + InfoNCE value" if args.eval
+                                  else "fwd -> InfoNCE -> bwd -> allreduce -> clip+AdamW"),
                    "global_batch": world * B, "local_batch": B, "seq_len_audio_frames": ((1 + (nsamp - 400) // 160) + 1) // 2,
                    "seq_len_text": L, "parallelism": f"dp{world}"},
         "step_roofline_frac": round(pairs * gflop / (world * BF16_PEAK_TFLOPS * 1e3), 4) if gflop else None,

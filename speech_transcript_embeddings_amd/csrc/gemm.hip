@@ -1009,6 +1009,8 @@ int num_cus() {
 #define STE_EPI_SPECS(X)                                                              \
   X(true, true, EF_BIAS | EF_C2 | EF_CBF16, STE_ACT_SWISH)   /* FFN intermediate   */ \
   X(true, true, EF_BIAS | EF_C2 | EF_CBF16, STE_ACT_GELU)    /* XLM-R intermediate */ \
+  X(true, true, EF_BIAS | EF_CBF16, STE_ACT_SWISH)           /* FFN in, no backward */ \
+  X(true, true, EF_BIAS | EF_CBF16, STE_ACT_GELU)                                     \
   X(true, true, EF_BIAS | EF_R, STE_ACT_NONE)                /* FFN out, O-proj    */ \
   X(true, true, EF_BIAS | EF_CBF16, STE_ACT_NONE)            /* QKV                */ \
   X(true, true, EF_CBF16, STE_ACT_NONE)                      /* pointwise conv 1   */ \

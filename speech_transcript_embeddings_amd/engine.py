@@ -86,7 +86,7 @@ class Engine:
                                  dgamma=g, dbeta=self.s.g(name + ".bias"), **kw)
 
     # ================================================================ audio
-    def audio_forward(self, feats, mask_i64, train, base_seed, ctx):
+    def audio_forward(self, feats, mask_i64, train, base_seed, ctx, save=True):
         c = self.acfg
         b, T, fin = feats.shape
         M = b * T
@@ -109,14 +109,15 @@ class Engine:
                 layers.append(None)
                 continue
             last = i == nl - 1
-            x, xb, sv = self._conformer_fwd(i, x, b, T, maskf, mask32, train, _site_seed(base_seed, 100 + i), last)
-            layers.append(sv)
-        if xb is None or layers[-1] is None:
+            x, xb, sv = self._conformer_fwd(i, x, b, T, maskf, mask32, train, _site_seed(base_seed, 100 + i), last,
+                                            save)
+            layers.append(sv if save else None)
+        if xb is None:  # the last layer was dropped (only the last layer writes the bf16 copy)
             xb = ops.cast_bf16(x, self._e(M, D, dtype=BF16))
         ctx["a_layers"] = layers
         return x, xb
 
-    def _conformer_fwd(self, i, x, b, T, maskf, mask32, train, seed, want_bf16):
+    def _conformer_fwd(self, i, x, b, T, maskf, mask32, train, seed, want_bf16, save=True):
         c = self.acfg
         s = self.s
         pre = f"audio_encoder.encoder.layers.{i}."
@@ -128,7 +129,7 @@ class Engine:
         # -- FFN1 (half-step)
         a1 = self._e(M, D, dtype=BF16)
         sv["st1"] = self._ln(x, pre + "ffn1_layer_norm", eps, yb=a1)
-        z1 = self._e(M, F_, dtype=BF16)
+        z1 = self._e(M, F_, dtype=BF16) if save else None  # swish pre-activation, for backward only
         h1 = ops.linear(a1, s.w(pre + "ffn1.intermediate_dense.weight"), s.p(pre + "ffn1.intermediate_dense.bias"),
                         act=ACT_SWISH, pre_out=z1, out_bf16=True)
         x1 = ops.linear(h1, s.w(pre + "ffn1.output_dense.weight"), s.p(pre + "ffn1.output_dense.bias"), alpha=0.5,
@@ -160,7 +161,7 @@ class Engine:
         # -- FFN2 (half-step) + final LN
         a5 = self._e(M, D, dtype=BF16)
         sv["st5"] = self._ln(x3, pre + "ffn2_layer_norm", eps, yb=a5)
-        z2 = self._e(M, F_, dtype=BF16)
+        z2 = self._e(M, F_, dtype=BF16) if save else None
         h2 = ops.linear(a5, s.w(pre + "ffn2.intermediate_dense.weight"), s.p(pre + "ffn2.intermediate_dense.bias"),
                         act=ACT_SWISH, pre_out=z2, out_bf16=True)
         x4 = ops.linear(h2, s.w(pre + "ffn2.output_dense.weight"), s.p(pre + "ffn2.output_dense.bias"), alpha=0.5,
@@ -288,7 +289,7 @@ class Engine:
                 self._ln_bwd(da0, ctx["a_xin"], ctx["a_st0"], "audio_encoder.feature_projection.layer_norm")
 
     # ================================================================= text
-    def text_forward(self, ids, mask_i64, train, base_seed, ctx):
+    def text_forward(self, ids, mask_i64, train, base_seed, ctx, save=True):
         c = self.tcfg
         s = self.s
         nb, L = ids.shape
@@ -310,12 +311,12 @@ class Engine:
                    t_seed=base_seed)
         layers = []
         for i in range(c.num_hidden_layers):
-            x, xb, sv = self._xlmr_fwd(i, x, xb, nb, L, mask32, hp, ap, _site_seed(base_seed, 10 + i))
-            layers.append(sv)
+            x, xb, sv = self._xlmr_fwd(i, x, xb, nb, L, mask32, hp, ap, _site_seed(base_seed, 10 + i), save)
+            layers.append(sv if save else None)
         ctx["t_layers"] = layers
         return x, xb
 
-    def _xlmr_fwd(self, i, x, xb, nb, L, mask32, hp, ap, seed):
+    def _xlmr_fwd(self, i, x, xb, nb, L, mask32, hp, ap, seed, save=True):
         c = self.tcfg
         s = self.s
         pre = f"text_encoder.encoder.layer.{i}."
@@ -335,7 +336,7 @@ class Engine:
         x1 = self._e(M, D)
         x1b = self._e(M, D, dtype=BF16)
         sv["st1"] = self._ln(y1, pre + "attention.output.LayerNorm", eps, y=x1, yb=x1b)
-        zt = self._e(M, F_, dtype=BF16)
+        zt = self._e(M, F_, dtype=BF16) if save else None  # GELU pre-activation, for backward only
         h = ops.linear(x1b, s.w(pre + "intermediate.dense.weight"), s.p(pre + "intermediate.dense.bias"),
                        act=ACT_GELU, pre_out=zt, out_bf16=True)
         y2 = ops.linear(h, s.w(pre + "output.dense.weight"), s.p(pre + "output.dense.bias"), residual=x1, drop_p=hp,
@@ -636,16 +637,19 @@ class Engine:
         align_backward(self, d_align, hs, ctx, dth, dah)
 
     # ============================================================== full step
-    def forward(self, batch, train: bool):
-        """compute_pos_neg_embeddings (ref:502-565) -> (tp_fused, tn_fused, a_fused, align, ctx)."""
+    def forward(self, batch, train: bool, save: bool = True):
+        """compute_pos_neg_embeddings (ref:502-565) -> (tp_fused, tn_fused, a_fused, align, ctx).
+        save=False (forward-only evaluation, ref:1165-1284 under no_grad): no encoder layer keeps
+        its activations, so each layer's buffers return to the allocator as the next one runs, and
+        the FFN GEMMs skip the pre-activation copies only backward reads."""
         ctx = Ctx()
         base_seed = int(torch.randint(0, 2**62, (1,)).item()) if train else 0
         ids = torch.cat([batch["input_ids_pos"], batch["input_ids_neg"]], 0)
         tmask = torch.cat([batch["attention_mask_pos"], batch["attention_mask_neg"]], 0).contiguous()
         ctx["_tmask_i64"] = tmask  # rows [0, b) = positive transcripts (alignment head's text mask)
-        th, thb = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx)
+        th, thb = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx, save)
         ah, ahb = self.audio_forward(batch["input_values"].contiguous(), batch["attention_mask_audio"].contiguous(),
-                                     train, _site_seed(base_seed, 3), ctx)
+                                     train, _site_seed(base_seed, 3), ctx, save)
         ctx["_thb"], ctx["_ahb"] = thb, ahb
         tf, af, align = self.heads_forward(th, thb, ah, ahb, train, _site_seed(base_seed, 4), ctx)
         b = batch["input_ids_pos"].shape[0]

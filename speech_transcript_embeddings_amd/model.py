@@ -182,8 +182,15 @@ class EnhancedAudioTextModel(nn.Module):
             if batch[k].device.type != "cuda":
                 raise RuntimeError(f"batch[{k!r}] must be on the GPU (libste.so has no CPU path)")
         self.store.sync_shadow()
+        if not torch.is_grad_enabled():
+            # forward only (the reference's evaluate() under torch.no_grad, ref:1188-1198): no
+            # autograd node, no saved activations
+            tf_p, tf_n, af, align, _ = self.engine.forward(batch, self.training, save=False)
+            tpn, tnn, an = _l2_normalise(tf_p, tf_n, af)[0]
+            self.last_alignment_scores = align if self.use_word_alignment else None
+            return tpn, tnn, an
         dummy = self.store.master[:1]
-        outs = _ModelFn.apply(self, batch, dummy.detach().requires_grad_(torch.is_grad_enabled()))
+        outs = _ModelFn.apply(self, batch, dummy.detach().requires_grad_(True))
         tpn, tnn, an = outs[:3]
         self.last_alignment_scores = outs[3] if self.use_word_alignment else None
         return tpn, tnn, an
@@ -217,16 +224,22 @@ class EnhancedAudioTextModel(nn.Module):
         return proj, h.view(B, T, -1)
 
 
+def _l2_normalise(tf_p, tf_n, af):
+    """F.normalize(dim=-1) of the three embeddings (ref:561-563) -> ((tpn, tnn, an), norms)."""
+    outs = tuple(torch.empty_like(t) for t in (tf_p, tf_n, af))
+    norms = [torch.empty(t.shape[0], device=t.device) for t in (tf_p, tf_n, af)]
+    for x, y, nrm in zip((tf_p, tf_n, af), outs, norms):
+        ops.l2norm_fwd(x.contiguous(), y, nrm)
+    return outs, norms
+
+
 class _ModelFn(torch.autograd.Function):
     """The whole model forward as one autograd node (backward = engine.backward)."""
 
     @staticmethod
     def forward(fctx, model, batch, dummy):
         tf_p, tf_n, af, align, ctx = model.engine.forward(batch, model.training)
-        tpn, tnn, an = (torch.empty_like(t) for t in (tf_p, tf_n, af))
-        norms = [torch.empty(t.shape[0], device=t.device) for t in (tf_p, tf_n, af)]
-        for x, y, nrm in zip((tf_p, tf_n, af), (tpn, tnn, an), norms):
-            ops.l2norm_fwd(x.contiguous(), y, nrm)
+        (tpn, tnn, an), norms = _l2_normalise(tf_p, tf_n, af)
         fctx.model, fctx.ctx = model, ctx
         fctx.saved = (tpn, tnn, an, norms)
         outs = (tpn, tnn, an)
