@@ -92,6 +92,10 @@ class EnhancedAudioTextModel(nn.Module):
         self.dropout = dropout
         self.xattn_heads = 8
         self.spec_augment = spec_augment
+        # constructor arguments the reference's checkpoint dict records (ref:1617-1633)
+        self.freeze_encoders = freeze_encoders
+        self.text_layers_to_unfreeze = text_layers_to_unfreeze
+        self.audio_layers_to_unfreeze = audio_layers_to_unfreeze
         self._apply_freezing(freeze_encoders, text_layers_to_unfreeze, audio_layers_to_unfreeze)
         self.text_projection = EnhancedProjection(text_embedding_dim, projection_dim, dropout=dropout)
         self.audio_projection = EnhancedProjection(audio_embedding_dim, projection_dim, dropout=dropout)

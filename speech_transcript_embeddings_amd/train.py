@@ -44,26 +44,120 @@ class LinearWarmupSchedule:
 
 
 class FusedAdamW:
-    """torch.optim.AdamW over the two reference param groups (encoder lr/50, heads lr,
-    weight_decay 0.01, betas (0.9, 0.999), eps 1e-8; ref:1487-1511) with
-    clip_grad_norm_(max_norm) (ref:1108) folded in: one Σg² pass, then one AdamW pass per
-    group that reads the clip coefficient on device (no host sync)."""
+    """torch.optim.AdamW over the reference's param groups with clip_grad_norm_(max_norm)
+    (ref:1108) folded in: one Σg² pass, then one AdamW pass per group that reads the clip
+    coefficient on device (no host sync).  Groups (ref:1486-1519): freeze_encoders="partial"
+    -> encoder params at lr/50 and the rest at lr; any other mode -> one group at lr.
+    weight_decay 0.01, betas (0.9, 0.999), eps 1e-8.
+
+    state_dict() / load_state_dict() use torch.optim.AdamW's format with the reference's
+    parameter numbering, so optimizer states move between this optimizer and a reference
+    AdamW in either direction (checkpoint parity)."""
 
     def __init__(self, model: EnhancedAudioTextModel, lr=2.1e-3, encoder_lr_div=50.0, weight_decay=0.01,
                  betas=(0.9, 0.999), eps=1e-8, max_norm=1.0):
         st = model.store
+        self.model = model
         self.store = st
-        self.groups = [{"range": st.seg_range["enc"], "lr": lr / encoder_lr_div},
+        self.partial = getattr(model, "freeze_encoders", "partial") == "partial"
+        div = encoder_lr_div if self.partial else 1.0
+        self.groups = [{"range": st.seg_range["enc"], "lr": lr / div},
                        {"range": st.seg_range["head"], "lr": lr}]
         self.wd, self.betas, self.eps, self.max_norm = weight_decay, betas, eps, max_norm
         self.exp_avg = torch.zeros(st.n_grad, device=st.device, dtype=F32)
         self.exp_avg_sq = torch.zeros(st.n_grad, device=st.device, dtype=F32)
         self.sumsq = torch.zeros(1, device=st.device, dtype=torch.float64)
         self.t = 0
+        self.last_factor = 1.0
+
+    # ------------------------------------------------------- torch.optim format
+    def _ref_groups(self):
+        """The reference's param groups as lists of parameter names (ref:1494-1519)."""
+        named = [(n, p) for n, p in self.model.named_parameters() if p.requires_grad]
+        if not self.partial:
+            return [[n for n, _ in named]]
+        enc = [n for n, _ in named if "text_encoder" in n or "audio_encoder" in n]
+        rest = [n for n, _ in named if not ("text_encoder" in n or "audio_encoder" in n)]
+        return [enc, rest]
+
+    def _group_hparams(self, gi):
+        base = self.groups[0]["lr"] if (self.partial and gi == 0) else self.groups[1]["lr"]
+        return {"lr": base * self.last_factor, "weight_decay": self.wd, "betas": tuple(self.betas), "eps": self.eps,
+                "amsgrad": False, "maximize": False, "foreach": None, "capturable": False, "differentiable": False,
+                "fused": None, "decoupled_weight_decay": True, "initial_lr": base}
+
+    def state_dict(self, lr_factor: float | None = None):
+        """torch.optim.AdamW.state_dict() layout: per-parameter {"step", "exp_avg", "exp_avg_sq"}
+        for every parameter that has received a gradient step (none before the first step),
+        keyed by the reference's parameter index; param_groups carry lr = initial_lr x
+        lr_factor (default: the factor of the last step; LambdaLR leaves the NEXT step's factor
+        there, which TrainStep.optimizer_state_dict() passes) and initial_lr."""
+        if lr_factor is not None:
+            saved, self.last_factor = self.last_factor, lr_factor
+            try:
+                return self.state_dict()
+            finally:
+                self.last_factor = saved
+        st = self.store
+        state, groups, idx = {}, [], 0
+        for gi, names in enumerate(self._ref_groups()):
+            ids = []
+            for n in names:
+                s = st.slots[n]
+                if self.t > 0 and s.segment in ("enc", "head"):
+                    sl = slice(s.offset, s.offset + s.numel)
+                    state[idx] = {"step": torch.tensor(float(self.t), dtype=F32),
+                                  "exp_avg": self.exp_avg[sl].view(s.shape).clone(),
+                                  "exp_avg_sq": self.exp_avg_sq[sl].view(s.shape).clone()}
+                ids.append(idx)
+                idx += 1
+            groups.append({**self._group_hparams(gi), "params": ids})
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, sd):
+        """Inverse of state_dict(); accepts a reference AdamW state_dict of the same model
+        configuration (same parameter numbering).  Restores the moments, the step count, the
+        base learning rates (initial_lr, or lr without a scheduler) and the shared
+        betas / eps / weight decay."""
+        st = self.store
+        ref = self._ref_groups()
+        pgs = sd["param_groups"]
+        if len(pgs) != len(ref) or any(len(g["params"]) != len(r) for g, r in zip(pgs, ref)):
+            raise ValueError("optimizer state_dict does not match this model's parameter groups "
+                             f"({[len(g['params']) for g in pgs]} vs {[len(r) for r in ref]})")
+        steps = set()
+        self.exp_avg.zero_()
+        self.exp_avg_sq.zero_()
+        for g, names in zip(pgs, ref):
+            for i, n in zip(g["params"], names):
+                ps = sd["state"].get(i)
+                if ps is None:
+                    continue
+                s = st.slots[n]
+                if s.segment not in ("enc", "head"):
+                    continue  # a parameter the HIP backward never produces a gradient for
+                sl = slice(s.offset, s.offset + s.numel)
+                self.exp_avg[sl].copy_(ps["exp_avg"].reshape(-1).to(self.exp_avg.device, F32))
+                self.exp_avg_sq[sl].copy_(ps["exp_avg_sq"].reshape(-1).to(self.exp_avg_sq.device, F32))
+                steps.add(int(float(ps["step"])))
+        if len(steps) > 1:
+            raise ValueError(f"parameters at different step counts {sorted(steps)}: not supported by the fused "
+                             "optimizer (one shared step)")
+        self.t = steps.pop() if steps else 0
+        bases = [g.get("initial_lr", g["lr"]) for g in pgs]
+        if self.partial:
+            self.groups[0]["lr"], self.groups[1]["lr"] = bases[0], bases[1]
+            self.last_factor = pgs[1]["lr"] / bases[1] if bases[1] else 1.0
+        else:
+            self.groups[0]["lr"] = self.groups[1]["lr"] = bases[0]
+            self.last_factor = pgs[0]["lr"] / bases[0] if bases[0] else 1.0
+        g0 = pgs[0]
+        self.wd, self.betas, self.eps = float(g0["weight_decay"]), tuple(g0["betas"]), float(g0["eps"])
 
     def step(self, lr_factor: float = 1.0):
         st = self.store
         self.t += 1
+        self.last_factor = lr_factor
         self.sumsq.zero_()
         if self.max_norm is not None:
             ops.sumsq(st.grad[: st.n_grad], self.sumsq)
@@ -248,6 +342,16 @@ class TrainStep:
         self.sched.step()
         self.last = {"loss": loss, "s_pos": sp, "s_neg": sn}
         return loss
+
+    def optimizer_state_dict(self):
+        """The optimizer state as the reference's training loop would save it after this many
+        optimizer.step(); scheduler.step() pairs (group lr = the next step's scheduled lr)."""
+        return self.opt.state_dict(lr_factor=self.sched.factor())
+
+    def load_optimizer_state_dict(self, sd):
+        """Restore moments + step count and put the warmup schedule at the same step."""
+        self.opt.load_state_dict(sd)
+        self.sched.step_count = self.opt.t
 
     def _gather_metrics(self, an, tn_all):
         ws = dist.get_world_size()
