@@ -308,6 +308,11 @@ int ste_axpby2d(float* y, int64_t ldy, const float* x, int64_t ldx, int64_t rows
 /* strided 2-D copy of 2- or 4-byte elements (concatenations feeding fusion GEMMs). */
 int ste_copy2d(void* y, int64_t ldy, const void* x, int64_t ldx, int64_t rows, int cols, int elem_bytes,
                void* stream);
+/* y[c, r] = x[r, c] for 2-byte elements (row strides ldx >= cols, ldy >= rows, in elements).
+ * Builds the k-contiguous copies Wᵀ [in, out] of the nn.Linear weights that the input-gradient
+ * GEMMs dX = dY·W read as their KC operand (replaces reading W k-major in the backward of
+ * every encoder Linear: tf:…wav2vec2_bert…:119-226, tf:…xlm_roberta…:186-398). */
+int ste_transpose16(void* y, int64_t ldy, const void* x, int64_t ldx, int64_t rows, int cols, void* stream);
 /* out[c] += Σ_r x[r, c] over a row-major [rows, cols] fp32/bf16 matrix (bias gradients). */
 int ste_colsum(const void* x, int is_bf16, int64_t rows, int cols, int64_t ld, float* out, void* stream);
 /* y[r, c] = x[r, c] * scale[r]  (fp32, row stride ld) */

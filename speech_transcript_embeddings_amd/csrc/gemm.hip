@@ -1018,10 +1018,10 @@ int num_cus() {
   X(true, true, EF_R, STE_ACT_NONE)                                                   \
   X(true, false, EF_CBF16, STE_ACT_NONE)                     /* dX, bf16 out       */ \
   X(true, false, 0, STE_ACT_NONE)                            /* dX, fp32 out       */ \
-  X(true, false, EF_Z | EF_COLSUM | EF_CBF16, STE_ACT_SWISH_BWD)                      \
-  X(true, false, EF_Z | EF_COLSUM | EF_CBF16, STE_ACT_GELU_BWD)                       \
-  X(true, false, EF_Z | EF_CBF16, STE_ACT_SWISH_BWD)         /* frozen layer: no db */ \
-  X(true, false, EF_Z | EF_CBF16, STE_ACT_GELU_BWD)                                   \
+  X(true, true, EF_Z | EF_COLSUM | EF_CBF16, STE_ACT_SWISH_BWD) /* dz = dh·W ⊙ act'(z), Wᵀ copy */ \
+  X(true, true, EF_Z | EF_COLSUM | EF_CBF16, STE_ACT_GELU_BWD)                        \
+  X(true, true, EF_Z | EF_CBF16, STE_ACT_SWISH_BWD)          /* frozen layer: no db */ \
+  X(true, true, EF_Z | EF_CBF16, STE_ACT_GELU_BWD)                                    \
   X(false, false, 0, STE_ACT_NONE)                           /* dW split-K slabs   */
 
 template <bool A_KC, bool B_KC>

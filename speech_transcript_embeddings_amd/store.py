@@ -121,6 +121,8 @@ class ParamStore:
             params[n] = newp
         self.params = params
         self._versions = {}
+        self._wt = {}          # (name, count) -> (Wᵀ bf16, param versions, opt_epoch) (see wt())
+        self.opt_epoch = 0     # fused optimizer steps so far (each refreshes the shadow of every trained weight)
         self.sync_shadow(force=True)
 
     # ------------------------------------------------------------------ views
@@ -154,6 +156,29 @@ class ParamStore:
         base = self.grad[s.offset:s.offset + n]
         return base.view(s.shape[0] * count, *s.shape[1:]) if len(s.shape) > 1 else base
 
+    def wt(self, name: str, count: int = 1):
+        """Wᵀ as a contiguous bf16 [in, out] matrix (the KC operand of dX = dY·W; `count` > 1:
+        the adjacent fused group starting at `name`, e.g. Q|K|V -> [in, 3·out]).  Built from the
+        bf16 shadow by the transpose kernel and cached; rebuilt when the shadow changed: after
+        a fused optimizer step for weights that receive gradients, or when a parameter was
+        written outside the optimizer (its _version moved)."""
+        key = (name, count)
+        s = self.slots[name]
+        names = [name] if count == 1 else None
+        if names is None:
+            first = s.offset
+            names = [n for n, t in self.slots.items() if first <= t.offset < first + s.numel * count]
+        versions = tuple(self.params[n]._version for n in names)
+        trained = s.segment in ("enc", "head")
+        ent = self._wt.get(key)
+        if ent is not None and ent[1] == versions and (not trained or ent[2] == self.opt_epoch):
+            return ent[0]
+        src = self.fused(name, count, "w") if count > 1 else self.w(name)
+        dst = ent[0] if ent is not None else None
+        dst = ops.transpose16(src, dst)
+        self._wt[key] = (dst, versions, self.opt_epoch)
+        return dst
+
     def trainable_layer(self, name: str) -> bool:
         return self.slots[name].segment in ("enc", "head")
 
@@ -171,8 +196,10 @@ class ParamStore:
                 self._versions[n] = self.params[n]._version
 
     def mark_synced(self):
+        """The fused optimizer refreshed the shadow of every trained parameter."""
         for n in self.slots:
             self._versions[n] = self.params[n]._version
+        self.opt_epoch += 1
 
     # ------------------------------------------------------------------ grads
     def attach_grads(self):

@@ -40,6 +40,49 @@ def test_gemm_layouts(ops, M, N, K):
     assert rel_err(ops.linear_dw(dy, x), dy.float().t() @ x.float()) < 1e-5
 
 
+@pytest.mark.parametrize("rows,cols", [(1024, 4096), (3072, 1024), (130, 77), (64, 1), (1000, 4100)])
+def test_transpose16(ops, rows, cols):
+    x = torch.randn(rows, cols, device=DEV).bfloat16()
+    assert torch.equal(ops.transpose16(x), x.t().contiguous())
+    big = torch.randn(rows, cols + 8, device=DEV).bfloat16()[:, 3:3 + cols]  # strided source view
+    assert torch.equal(ops.transpose16(big), big.t().contiguous())
+
+
+def test_dx_through_cached_transpose():
+    """dX = dY·W on the KC kernel with ParamStore.wt equals the k-major kernel bit for bit, and
+    the cached Wᵀ follows optimizer steps (trained weights) but is reused for frozen ones."""
+    import json
+    from conftest import GOLDEN
+    from test_model_gpu import mini_model
+    from speech_transcript_embeddings_amd import ops
+    from speech_transcript_embeddings_amd.train import TrainStep, synthetic_batch
+    meta = json.loads((GOLDEN / "model_golden_noalign.json").read_text())
+    model = mini_model(meta)
+    st = model.store
+    trained = "audio_encoder.encoder.layers.1.ffn1.intermediate_dense.weight"
+    frozen = "audio_encoder.encoder.layers.0.ffn1.intermediate_dense.weight"
+    assert st.slots[trained].segment == "enc" and st.slots[frozen].segment == "frozen"
+    dy = torch.randn(300, st.slots[trained].shape[0], device=DEV).bfloat16()
+    for n in (trained, frozen):
+        a = ops.linear_dx(dy, st.w(n), out_bf16=True)
+        b = ops.linear(dy, st.wt(n), out_bf16=True)
+        assert torch.equal(a, b)
+    q = "audio_encoder.encoder.layers.1.self_attn.linear_q.weight"
+    assert torch.equal(st.wt(q, 3), st.fused(q, 3, "w").t())
+    t_frozen, t_trained = st.wt(frozen), st.wt(trained).clone()
+    step = TrainStep(model, lr=1e-2, warmup=1, total_steps=10)
+    data = synthetic_batch(2, 16000, 12, vocab=meta["mini"]["text"]["vocab_size"], seed=1)
+    step(*data)
+    step(*data)
+    assert st.wt(frozen) is t_frozen  # frozen: built once
+    assert not torch.equal(st.wt(trained), t_trained)  # trained: follows the optimizer
+    assert torch.equal(st.wt(trained), st.w(trained).t())
+    with torch.no_grad():  # a write outside the optimizer (e.g. load_state_dict) invalidates it
+        model.get_parameter(frozen).mul_(2.0)
+    st.sync_shadow()
+    assert torch.equal(st.wt(frozen), st.w(frozen).t())
+
+
 @pytest.mark.parametrize("M,N,K,ws_mb", [(4096, 1024, 31936, 80),   # c2 FFN intermediate dW: S=4, K tail 3 tiles
                                          (1024, 1024, 15968, 80),   # c3 (b=32) O-proj dW: S=16, ragged 32-row tail
                                          (3072, 768, 8192, 80),     # text QKV dW over 2bL rows
