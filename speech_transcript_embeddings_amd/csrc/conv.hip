@@ -5,49 +5,85 @@
 // emits d(pre) for both GLU halves directly.
 //
 // Block = (batch b, 64 time rows, 64 channels), 256 threads; the time window with its
-// K-1 halo is staged in LDS as fp32; each thread owns one channel and 16 consecutive
-// rows (the taps held in registers).
+// K-1 halo is staged in LDS as fp32 (16-B global loads of 8 channels); each thread owns one
+// channel and 16 consecutive rows: its 31 taps (staged through LDS, coalesced) and its
+// 16 + 30 window rows sit in registers, so the tap loop reads LDS once per row, not per tap.
+// Results leave row-contiguous through the freed staging rows (16-B stores of 8 channels).
 #include "common.h"
 #include "../../include/ste.h"
 
 namespace {
 
 constexpr int TT = 64, CC = 64, NT = 256, KMAX = 31;
+constexpr int RPT = TT / (NT / CC);  // rows per thread (16)
 
 template <int K>
 __global__ __launch_bounds__(NT) void glu_dwconv_fwd_kernel(const bf16* __restrict__ pre, const float* __restrict__ w,
                                                           bf16* __restrict__ out, int T, int C) {
   __shared__ float sg[TT + K - 1][CC];
+  __shared__ float sw[CC * K];  // the block's taps, staged coalesced (a lane's taps are 124 B apart in w)
   const int b = blockIdx.z, t0 = blockIdx.x * TT, c0 = blockIdx.y * CC;
   const int tid = threadIdx.x;
-  // stage g = a * sigmoid(gate) for rows t0-(K-1) .. t0+TT-1
-  for (int i = tid; i < (TT + K - 1) * (CC / 4); i += NT) {
-    const int r = i / (CC / 4), c4 = (i % (CC / 4)) * 4;
+  for (int i = tid; i < CC * K; i += NT) sw[i] = w[c0 * K + i];
+  // stage g = a * sigmoid(gate) for rows t0-(K-1) .. t0+TT-1: 16-B loads of 8 channels of
+  // each GLU half, every load of the thread issued before the first use
+  constexpr int ITEMS = (TT + K - 1) * (CC / 8), PER = (ITEMS + NT - 1) / NT;
+  bf16x8 av[PER], gv[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = tid + u * NT, r = i / (CC / 8), c8 = (i % (CC / 8)) * 8;
     const int t = t0 - (K - 1) + r;
-    f32x4 g = {0.f, 0.f, 0.f, 0.f};
-    if (t >= 0 && t < T) {
-      const bf16* p = pre + (int64_t)(b * T + t) * (2 * C) + c0 + c4;
-      f32x4 av = load_bf16x4(p), gv = load_bf16x4(p + C);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) g[e] = av[e] * sigmoidf_(gv[e]);
+    av[u] = bf16x8{};
+    gv[u] = bf16x8{};
+    if (i < ITEMS && t >= 0 && t < T) {
+      const bf16* p = pre + (int64_t)(b * T + t) * (2 * C) + c0 + c8;
+      av[u] = *reinterpret_cast<const bf16x8*>(p);
+      gv[u] = *reinterpret_cast<const bf16x8*>(p + C);
     }
+  }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) sg[r][c4 + e] = g[e];
+  for (int u = 0; u < PER; ++u) {
+    const int i = tid + u * NT, r = i / (CC / 8), c8 = (i % (CC / 8)) * 8;
+    if (i >= ITEMS) continue;
+    f32x4 lo, hi;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      lo[e] = (float)av[u][e] * sigmoidf_((float)gv[u][e]);
+      hi[e] = (float)av[u][4 + e] * sigmoidf_((float)gv[u][4 + e]);
+    }
+    *reinterpret_cast<f32x4*>(&sg[r][c8]) = lo;
+    *reinterpret_cast<f32x4*>(&sg[r][c8 + 4]) = hi;
   }
   __syncthreads();
-  const int c = tid & (CC - 1), rg = tid >> 6;  // 4 row groups of 16
+  const int c = tid & (CC - 1), rg = tid >> 6;  // 4 row groups of RPT
   float wk[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) wk[k] = w[(c0 + c) * K + k];
-  const int rbeg = rg * 16;
-#pragma unroll 2
-  for (int i = 0; i < 16; ++i) {
-    const int r = rbeg + i;  // output row t0 + r uses sg[r .. r+K-1]
-    float acc = 0.f;
+  for (int k = 0; k < K; ++k) wk[k] = sw[c * K + k];  // stride 31 words: conflict-free
+  const int rbeg = rg * RPT;
+  // the thread's RPT + K - 1 input rows in registers: one LDS read per row instead of one per tap
+  float win[RPT + K - 1];
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc += wk[k] * sg[r + k][c];
+  for (int j = 0; j < RPT + K - 1; ++j) win[j] = sg[rbeg + j][c];
+  float acc[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) acc[i] += wk[k] * win[i + k];  // output row t0+rbeg+i: rows i..i+K-1
+  // outputs leave row-contiguous: through the (now free) staging rows, 8 channels per 16-B store
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) sg[rbeg + i][c] = acc[i];
+  __syncthreads();
+  for (int i = tid; i < TT * (CC / 8); i += NT) {
+    const int r = i / (CC / 8), c8 = (i % (CC / 8)) * 8;
     const int t = t0 + r;
-    if (t < T) out[(int64_t)(b * T + t) * C + c0 + c] = (bf16)acc;
+    if (t >= T) continue;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)sg[r][c8 + e];
+    *reinterpret_cast<bf16x8*>(out + (int64_t)(b * T + t) * C + c0 + c8) = o;
   }
 }
 
@@ -60,60 +96,83 @@ __global__ __launch_bounds__(NT) void glu_dwconv_bwd_kernel(const bf16* __restri
                                                           float* __restrict__ dw, int T, int C) {
   constexpr int ROWS = TT + K - 1;
   __shared__ float lds[(DW ? 2 : 1) * ROWS * CC];
+  __shared__ float sw[CC * K];
   float (*sd)[CC] = reinterpret_cast<float (*)[CC]>(lds);              // dout rows t0 .. t0+TT+K-2
   float (*sg)[CC] = reinterpret_cast<float (*)[CC]>(lds + ROWS * CC);  // g rows t0-(K-1) .. t0+TT-1 (DW only)
   const int b = blockIdx.z, t0 = blockIdx.x * TT, c0 = blockIdx.y * CC;
   const int tid = threadIdx.x;
-  for (int i = tid; i < ROWS * (CC / 4); i += NT) {
-    const int r = i / (CC / 4), c4 = (i % (CC / 4)) * 4;
+  for (int i = tid; i < CC * K; i += NT) sw[i] = w[c0 * K + i];
+  for (int i = tid; i < ROWS * (CC / 8); i += NT) {  // 16-B loads of 8 channels
+    const int r = i / (CC / 8), c8 = (i % (CC / 8)) * 8;
     const int td = t0 + r;
-    f32x4 dv = {0.f, 0.f, 0.f, 0.f};
-    if (td < T) dv = load_bf16x4(dout + (int64_t)(b * T + td) * C + c0 + c4);
+    bf16x8 dv = bf16x8{};
+    if (td < T) dv = *reinterpret_cast<const bf16x8*>(dout + (int64_t)(b * T + td) * C + c0 + c8);
+    bf16x8 av = bf16x8{}, gv = bf16x8{};
+    const int tg = t0 - (K - 1) + r;
+    if (DW && tg >= 0 && tg < T) {
+      const bf16* p = pre + (int64_t)(b * T + tg) * (2 * C) + c0 + c8;
+      av = *reinterpret_cast<const bf16x8*>(p);
+      gv = *reinterpret_cast<const bf16x8*>(p + C);
+    }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) sd[r][c4 + e] = dv[e];
+    for (int e = 0; e < 8; ++e) sd[r][c8 + e] = (float)dv[e];
     if (DW) {
-      const int tg = t0 - (K - 1) + r;
-      f32x4 g = {0.f, 0.f, 0.f, 0.f};
-      if (tg >= 0 && tg < T) {
-        const bf16* p = pre + (int64_t)(b * T + tg) * (2 * C) + c0 + c4;
-        f32x4 av = load_bf16x4(p), gv = load_bf16x4(p + C);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) g[e] = av[e] * sigmoidf_(gv[e]);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) sg[r][c4 + e] = g[e];
+      for (int e = 0; e < 8; ++e) sg[r][c8 + e] = (tg >= 0 && tg < T) ? (float)av[e] * sigmoidf_((float)gv[e]) : 0.f;
     }
   }
   __syncthreads();
   const int c = tid & (CC - 1), rg = tid >> 6;
   float wk[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) wk[k] = w[(c0 + c) * K + k];
+  for (int k = 0; k < K; ++k) wk[k] = sw[c * K + k];
   float dwp[DW ? K : 1];
 #pragma unroll
   for (int k = 0; k < (DW ? K : 1); ++k) dwp[k] = 0.f;
-  const int rbeg = rg * 16;
-  for (int i = 0; i < 16; ++i) {
-    const int r = rbeg + i;
-    const int t = t0 + r;
-    // dg[t] = Σ_k w[k] * dout[t + (K-1) - k]  -> sd[r + K-1-k]
-    float dg = 0.f;
+  const int rbeg = rg * RPT;
+  // register windows of the thread's RPT + K - 1 staged rows (one LDS read per row)
+  float dwin[RPT + K - 1], gwin[DW ? RPT + K - 1 : 1];
 #pragma unroll
-    for (int k = 0; k < K; ++k) dg += wk[k] * sd[r + (K - 1) - k][c];
+  for (int j = 0; j < RPT + K - 1; ++j) dwin[j] = sd[rbeg + j][c];
+  if (DW) {
+#pragma unroll
+    for (int j = 0; j < RPT + K - 1; ++j) gwin[j] = sg[rbeg + j][c];
+  }
+  float dg[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    // dg[t] = Σ_k w[k] * dout[t + (K-1) - k]  -> dwin[i + K-1-k]
+    dg[i] = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) dg[i] += wk[k] * dwin[i + (K - 1) - k];
     if (DW) {
-      // dW[k] += dout[t] * g[t - (K-1) + k] -> sd[r] * sg[r + k]
-      const float d0 = sd[r][c];
+      // dW[k] += dout[t] * g[t - (K-1) + k] -> dwin[i] * gwin[i + k]
+      const float d0 = dwin[i];
 #pragma unroll
-      for (int k = 0; k < K; ++k) dwp[k] += d0 * sg[r + k][c];
+      for (int k = 0; k < K; ++k) dwp[k] += d0 * gwin[i + k];
     }
-    if (t < T) {
-      const int64_t row = (int64_t)(b * T + t);
-      const float av = (float)pre[row * 2 * C + c0 + c];
-      const float gv = (float)pre[row * 2 * C + C + c0 + c];
-      const float sgm = sigmoidf_(gv);
-      dpre[row * 2 * C + c0 + c] = (bf16)(dg * sgm);
-      dpre[row * 2 * C + C + c0 + c] = (bf16)(dg * av * sgm * (1.f - sgm));
+  }
+  // GLU backward row-contiguous: dg through the (now free) dout rows, 8 channels per 16-B access
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) sd[rbeg + i][c] = dg[i];
+  __syncthreads();
+  for (int i = tid; i < TT * (CC / 8); i += NT) {
+    const int r = i / (CC / 8), c8 = (i % (CC / 8)) * 8;
+    const int t = t0 + r;
+    if (t >= T) continue;
+    const int64_t row = (int64_t)(b * T + t);
+    const bf16x8 av = *reinterpret_cast<const bf16x8*>(pre + row * 2 * C + c0 + c8);
+    const bf16x8 gv = *reinterpret_cast<const bf16x8*>(pre + row * 2 * C + C + c0 + c8);
+    bf16x8 da, dgate;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = sd[r][c8 + e], sgm = sigmoidf_((float)gv[e]);
+      da[e] = (bf16)(d * sgm);
+      dgate[e] = (bf16)(d * (float)av[e] * sgm * (1.f - sgm));
     }
+    *reinterpret_cast<bf16x8*>(dpre + row * 2 * C + c0 + c8) = da;
+    *reinterpret_cast<bf16x8*>(dpre + row * 2 * C + C + c0 + c8) = dgate;
   }
   if (!DW) return;
   // reduce the 4 row groups' partials through the (now free) staging LDS: [rg][c][K+1]
