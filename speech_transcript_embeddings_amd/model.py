@@ -207,7 +207,7 @@ class EnhancedAudioTextModel(nn.Module):
         ctx = {}
         if attention_mask is None:
             attention_mask = torch.ones_like(input_ids)
-        h, hb = e.text_forward(input_ids.contiguous(), attention_mask.contiguous(), False, 0, ctx)
+        h, hb = e.text_forward(input_ids.contiguous(), attention_mask.contiguous(), False, 0, ctx, save=False)
         sv = {}
         B, L = input_ids.shape
         _, pb = e._pool_fwd("text_pooling", hb, ctx["t_mask32"], B, L, sv)
@@ -222,7 +222,7 @@ class EnhancedAudioTextModel(nn.Module):
         B, T, _ = input_values.shape
         if attention_mask is None:
             attention_mask = torch.ones(B, T, dtype=torch.int64, device=input_values.device)
-        h, hb = e.audio_forward(input_values.contiguous(), attention_mask.contiguous(), False, 0, ctx)
+        h, hb = e.audio_forward(input_values.contiguous(), attention_mask.contiguous(), False, 0, ctx, save=False)
         _, pb = e._pool_fwd("audio_pooling", hb, ctx["a_mask32"], B, T, {})
         proj = e._proj_fwd("audio_projection", pb, B, False, 0, {})
         return proj, h.view(B, T, -1)

@@ -135,3 +135,39 @@ def test_optimizer_oracle_matches_reference(tag):
         assert np.all(np.abs(z[f"pnew::{n}"][noise] - decayed[noise]) <= lr * 1.001 + 1e-7), n
         np.testing.assert_allclose(pn.reshape(-1).numpy()[idx][~noise], z[f"pnew::{n}"][~noise], atol=1e-6,
                                    rtol=1e-5, err_msg=n)
+
+
+def _infer_golden():
+    meta = json.loads((GOLDEN / "infer_golden.json").read_text())
+    z = np.load(GOLDEN / "infer_golden.npz")
+    return meta, z
+
+
+def infer_cfgs(meta):
+    """(TextCfg, AudioCfg) of the inference-variant golden (RoBERTa / w2v-bert at mini dims)."""
+    tx, au = meta["text"], meta["audio"]
+    t = R.TextCfg(hidden=tx["hidden_size"], layers=tx["num_hidden_layers"], heads=tx["num_attention_heads"],
+                  inter=tx["intermediate_size"], vocab=tx["vocab_size"], max_pos=tx["max_position_embeddings"],
+                  pad_id=tx["pad_token_id"])
+    a = R.AudioCfg(hidden=au["hidden_size"], layers=au["num_hidden_layers"], heads=au["num_attention_heads"],
+                   inter=au["intermediate_size"], feat_in=au["feature_projection_input_dim"],
+                   left=au["left_max_position_embeddings"], right=au["right_max_position_embeddings"],
+                   conv_k=au["conv_depthwise_kernel_size"])
+    return t, a
+
+
+def test_infer_oracle_matches_golden():
+    """oracle/ref_infer.py (model.py:131-329 restated) against the real model.py's outputs."""
+    from oracle import ref_infer
+    meta, z = _infer_golden()
+    vals = det_init.state_dict_values([(n, tuple(s)) for n, s in meta["shapes"].items()])
+    p = {n: torch.from_numpy(v) for n, v in vals.items()}
+    batch = {k: torch.from_numpy(z[k]) for k in ("input_ids", "attention_mask", "input_features",
+                                                 "attention_mask_audio")}
+    t, a = infer_cfgs(meta)
+    te, ae = ref_infer.forward(p, batch, t, a)
+    np.testing.assert_allclose(te.numpy(), z["text_emb"], atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(ae.numpy(), z["audio_emb"], atol=2e-6, rtol=1e-5)
+    tp, th = ref_infer.encode_text(p, batch["input_ids"], batch["attention_mask"], t)
+    np.testing.assert_allclose(th.numpy(), z["text_hidden"], atol=2e-5, rtol=1e-5)
+    np.testing.assert_allclose(tp.numpy(), z["text_proj"], atol=2e-5, rtol=1e-5)
