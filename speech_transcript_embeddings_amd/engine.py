@@ -19,6 +19,7 @@ store.py (beta=1 accumulation), so micro-batch accumulation needs no extra pass.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -47,15 +48,30 @@ class Engine:
         self.s = model.store
         self.acfg = model.audio_cfg
         self.tcfg = model.text_cfg
-        self._ws = None
+        self._ws = {}
+        self._side = None
+        # the text encoder (forward and backward) runs on a second HIP stream, concurrently with
+        # the audio encoder: its GEMMs are too small to fill 256 CUs (8,192 rows) and overlap the
+        # audio side's bandwidth-bound kernels.  STE_TEXT_STREAM=0: one stream (A/B runs).
+        self.overlap = os.environ.get("STE_TEXT_STREAM", "1") != "0"
 
     WS_BYTES = 80 << 20   # split-K slabs of the weight-gradient GEMMs (largest: 7 x 3072 x 768 fp32)
 
     @property
     def ws(self):
-        if self._ws is None:
-            self._ws = torch.empty(self.WS_BYTES // 4, device=self.s.device, dtype=F32)
-        return self._ws
+        """Split-K workspace of the CURRENT stream (the text and audio backward run concurrently)."""
+        key = torch.cuda.current_stream(self.s.device).cuda_stream if self.s.device.type == "cuda" else 0
+        w = self._ws.get(key)
+        if w is None:
+            w = self._ws[key] = torch.empty(self.WS_BYTES // 4, device=self.s.device, dtype=F32)
+        return w
+
+    def _side_stream(self):
+        if not (self.overlap and self.s.device.type == "cuda"):
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.s.device)
+        return self._side
 
     # ------------------------------------------------------------- helpers
     def _e(self, *shape, dtype=F32):
@@ -653,9 +669,18 @@ class Engine:
         ids = torch.cat([batch["input_ids_pos"], batch["input_ids_neg"]], 0)
         tmask = torch.cat([batch["attention_mask_pos"], batch["attention_mask_neg"]], 0).contiguous()
         ctx["_tmask_i64"] = tmask  # rows [0, b) = positive transcripts (alignment head's text mask)
-        th, thb = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx, save)
+        side = self._side_stream()
+        if side is not None:  # text encoder on the side stream, audio encoder on the main stream
+            main = torch.cuda.current_stream(self.s.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                th, thb = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx, save)
+        else:
+            th, thb = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx, save)
         ah, ahb = self.audio_forward(batch["input_values"].contiguous(), batch["attention_mask_audio"].contiguous(),
                                      train, _site_seed(base_seed, 3), ctx, save)
+        if side is not None:
+            main.wait_stream(side)
         ctx["_thb"], ctx["_ahb"] = thb, ahb
         tf, af, align = self.heads_forward(th, thb, ah, ahb, train, _site_seed(base_seed, 4), ctx)
         b = batch["input_ids_pos"].shape[0]
@@ -675,13 +700,26 @@ class Engine:
         ctx.pop("heads", None)
         if stage_done:
             stage_done("heads")
-        self.audio_backward(dah, ctx)
-        del dah
-        if stage_done:
-            stage_done("audio")
-        self.text_backward(dth, ctx)
-        if stage_done:
-            stage_done("text")
+        side = self._side_stream()
+        if side is not None:  # text backward on the side stream, concurrent with the audio backward
+            main = torch.cuda.current_stream(self.s.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self.text_backward(dth, ctx)
+            self.audio_backward(dah, ctx)
+            main.wait_stream(side)
+            del dah
+            if stage_done:
+                stage_done("audio")
+                stage_done("text")
+        else:
+            self.audio_backward(dah, ctx)
+            del dah
+            if stage_done:
+                stage_done("audio")
+            self.text_backward(dth, ctx)
+            if stage_done:
+                stage_done("text")
         ctx.clear()
 
 
