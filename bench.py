@@ -154,7 +154,7 @@ def main():
 
     model = EnhancedAudioTextModel(use_word_alignment=args.align, text_layers_to_unfreeze=args.unfreeze,
                                    audio_layers_to_unfreeze=args.unfreeze, freeze_encoders=args.freeze,
-                                   device=f"cuda:{local}")
+                                   device=f"cuda:{local}", spec_augment=False)  # timed without SpecAugment
     model.audio_cfg.layerdrop = 0.0
     step = TrainStep(model, warmup=100, total_steps=100000)
     B, nsamp, L = args.batch, int(args.seconds * 16000), args.tokens

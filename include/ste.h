@@ -308,6 +308,14 @@ int ste_axpby2d(float* y, int64_t ldy, const float* x, int64_t ldx, int64_t rows
 /* strided 2-D copy of 2- or 4-byte elements (concatenations feeding fusion GEMMs). */
 int ste_copy2d(void* y, int64_t ldy, const void* x, int64_t ldx, int64_t rows, int cols, int elem_bytes,
                void* stream);
+/* SpecAugment time masking of the audio encoder input (tf:…wav2vec2_bert…:944-988, training mode):
+ * forward x[r,:] = embed for rows with spec[r] != 0 and valid[r] != 0 (x fp32 [rows, cols], row
+ * stride ld; spec int32 [rows]; valid = the frame mask as float); backward dembed += Σ dx[r,:]
+ * over the same rows (fp32 atomics; dembed may be NULL) and dx[r,:] = 0. */
+int ste_spec_mask_fwd(float* x, int64_t ld, const int32_t* spec, const float* valid, const float* embed,
+                      int64_t rows, int cols, void* stream);
+int ste_spec_mask_bwd(float* dx, int64_t ld, const int32_t* spec, const float* valid, float* dembed,
+                      int64_t rows, int cols, void* stream);
 /* y[c, r] = x[r, c] for 2-byte elements (row strides ldx >= cols, ldy >= rows, in elements).
  * Builds the k-contiguous copies Wᵀ [in, out] of the nn.Linear weights that the input-gradient
  * GEMMs dX = dY·W read as their KC operand (replaces reading W k-major in the backward of

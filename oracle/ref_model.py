@@ -123,10 +123,14 @@ def conformer_ffn(p, pre, h):
     return _lin(p, pre + "output_dense", F.silu(_lin(p, pre + "intermediate_dense", h)))
 
 
-def audio_encoder(p, feats, mask, cfg: AudioCfg, prefix="audio_encoder."):
-    """w2v:991-1042 (Wav2Vec2BertModel.forward, eval: no SpecAugment) + encoder w2v:480-548."""
+def audio_encoder(p, feats, mask, cfg: AudioCfg, prefix="audio_encoder.", spec_mask=None):
+    """w2v:991-1042 (Wav2Vec2BertModel.forward) + encoder w2v:480-548.  spec_mask (bool [B,T],
+    training mode): SpecAugment rows replaced by masked_spec_embed (w2v:944-988) before the
+    encoder zeroes the padded frames."""
     x = _ln(p, prefix + "feature_projection.layer_norm", feats, cfg.eps)
     h = _lin(p, prefix + "feature_projection.projection", x)
+    if spec_mask is not None:
+        h = torch.where(spec_mask.unsqueeze(-1), p[prefix + "masked_spec_embed"].expand_as(h), h)
     add_mask = None
     if mask is not None:
         h = h.masked_fill(~mask.bool().unsqueeze(-1), 0.0)
@@ -243,9 +247,9 @@ def encode_text(p, ids, mask, cfg: ModelCfg):
     return enhanced_projection(p, "text_projection.", pooled), h
 
 
-def encode_audio(p, feats, mask, cfg: ModelCfg):
+def encode_audio(p, feats, mask, cfg: ModelCfg, spec_mask=None):
     """ref:587-641."""
-    h = audio_encoder(p, feats, mask, cfg.audio)
+    h = audio_encoder(p, feats, mask, cfg.audio, spec_mask=spec_mask)
     if cfg.use_attentive_pooling:
         pooled = attentive_pooling(p, "audio_pooling.", h, mask)
     else:
@@ -267,11 +271,12 @@ def apply_cross_modal(p, tproj, th, tmask, aproj, ah, amask, cfg: ModelCfg):
     return tf_, af_
 
 
-def compute_pos_neg_embeddings(p, batch, cfg: ModelCfg):
-    """ref:502-565.  Returns (txt_pos_norm, txt_neg_norm, aud_norm, alignment_scores|None)."""
+def compute_pos_neg_embeddings(p, batch, cfg: ModelCfg, spec_mask=None):
+    """ref:502-565.  Returns (txt_pos_norm, txt_neg_norm, aud_norm, alignment_scores|None).
+    spec_mask: the training-mode SpecAugment rows of the audio encoder (None: eval / off)."""
     tp, th = encode_text(p, batch["input_ids_pos"], batch["attention_mask_pos"], cfg)
     tn, thn = encode_text(p, batch["input_ids_neg"], batch["attention_mask_neg"], cfg)
-    ap, ah = encode_audio(p, batch["input_values"], batch["attention_mask_audio"], cfg)
+    ap, ah = encode_audio(p, batch["input_values"], batch["attention_mask_audio"], cfg, spec_mask=spec_mask)
     if cfg.use_cross_modal:
         tpf, af = apply_cross_modal(p, tp, th, batch["attention_mask_pos"], ap, ah, batch["attention_mask_audio"], cfg)
         tnf, _ = apply_cross_modal(p, tn, thn, batch["attention_mask_neg"], ap, ah, batch["attention_mask_audio"], cfg)

@@ -157,6 +157,8 @@ _SIGS = {
     "ste_axpby2d": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_float, c_float, c_void_p]),
     "ste_copy2d": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_int, c_void_p]),
     "ste_transpose16": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p]),
+    "ste_spec_mask_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "ste_spec_mask_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "ste_scale_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int64, c_void_p]),
     "ste_mask_i64_to_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "ste_version": (C.c_char_p, []),

@@ -113,7 +113,56 @@ __global__ __launch_bounds__(256) void transpose16_kernel(uint16_t* __restrict__
     if (r0 + rr < rows && c0 + cc < cols) y[(int64_t)(c0 + cc) * ldy + r0 + rr] = t[rr][cc];
   }
 }
+// SpecAugment rows (spec[r] != 0 and valid[r] != 0): forward x[r,:] = embed; backward
+// dembed += Σ dx[r,:] over those rows (block partials + one atomic per column per block) and
+// dx[r,:] = 0 (the replaced projection output gets no gradient)
+__global__ __launch_bounds__(256) void spec_mask_fwd_kernel(float* x, int64_t ld, const int32_t* spec,
+                                                            const float* valid, const float* embed, int64_t rows,
+                                                            int cols) {
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    if (!spec[r] || valid[r] == 0.f) continue;
+    for (int c = threadIdx.x; c < cols; c += blockDim.x) x[r * ld + c] = embed[c];
+  }
+}
+__global__ __launch_bounds__(256) void spec_mask_bwd_kernel(float* dx, int64_t ld, const int32_t* spec,
+                                                            const float* valid, float* dembed, int64_t rows,
+                                                            int cols) {
+  for (int c0 = 0; c0 < cols; c0 += blockDim.x) {
+    const int c = c0 + threadIdx.x;
+    float acc = 0.f;
+    for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+      if (!spec[r] || valid[r] == 0.f) continue;
+      if (c < cols) {
+        acc += dx[r * ld + c];
+        dx[r * ld + c] = 0.f;
+      }
+    }
+    if (dembed && c < cols && acc != 0.f) atomicAdd(dembed + c, acc);
+  }
+}
 }  // namespace
+
+extern "C" int ste_spec_mask_fwd(float* x, int64_t ld, const int32_t* spec, const float* valid, const float* embed,
+                                 int64_t rows, int cols, void* stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (!x || !spec || !valid || !embed) return STE_ERR_ARG;
+  const int blocks = (int)(rows < 2048 ? rows : 2048);
+  hipLaunchKernelGGL(spec_mask_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, ld, spec, valid, embed,
+                     rows, cols);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_spec_mask_bwd(float* dx, int64_t ld, const int32_t* spec, const float* valid, float* dembed,
+                                 int64_t rows, int cols, void* stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (!dx || !spec || !valid) return STE_ERR_ARG;
+  const int blocks = (int)(rows < 512 ? rows : 512);
+  hipLaunchKernelGGL(spec_mask_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dx, ld, spec, valid,
+                     dembed, rows, cols);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int ste_transpose16(void* y, int64_t ldy, const void* x, int64_t ldx, int64_t rows, int cols,
                                void* stream) {

@@ -122,7 +122,16 @@ class Engine:
         st0 = self._ln(xin, "audio_encoder.feature_projection.layer_norm", c.layer_norm_eps, yb=a0)
         x = ops.linear(a0, self.s.w("audio_encoder.feature_projection.projection.weight"),
                        self.s.p("audio_encoder.feature_projection.projection.bias"), row_scale=maskf)
-        ctx.update(a_b=b, a_T=T, a_maskf=maskf, a_mask32=mask32, a_xin=xin, a_a0=a0, a_st0=st0)
+        spec = None
+        if train and getattr(self.m, "spec_augment", False) and c.mask_time_prob > 0:
+            # SpecAugment (w2v:944-988): spans drawn on the host with numpy's global RNG exactly as
+            # transformers does (the frame counts cost one host sync, as in the reference)
+            from .specaug import compute_mask_indices
+            sm = compute_mask_indices((b, T), c.mask_time_prob, c.mask_time_length, mask_i64.sum(-1).tolist(),
+                                      c.mask_time_min_masks)
+            spec = torch.from_numpy(sm.astype("int32").reshape(-1)).to(self.s.device)
+            ops.spec_mask_fwd(x, spec, maskf, self.s.p("audio_encoder.masked_spec_embed"))
+        ctx.update(a_b=b, a_T=T, a_maskf=maskf, a_mask32=mask32, a_xin=xin, a_a0=a0, a_st0=st0, a_spec=spec)
         layers = []
         xb = None
         nl = c.num_hidden_layers
@@ -295,8 +304,10 @@ class Engine:
                 continue
             dx = self._conformer_bwd(i, sv, dx, b, T, maskf, mask32)
             ctx["a_layers"][i] = None
-        # feature projection: x = mask * (LN(feats) W^T + b)
         s = self.s
+        if ctx.get("a_spec") is not None:  # SpecAugment rows: gradient to masked_spec_embed, not the projection
+            ops.spec_mask_bwd(dx, ctx["a_spec"], maskf, s.g("audio_encoder.masked_spec_embed"))
+        # feature projection: x = mask * (LN(feats) W^T + b)
         gW = s.g("audio_encoder.feature_projection.projection.weight")
         if gW is not None:
             M = dx.shape[0]

@@ -46,18 +46,18 @@ def _resolve(name_or_cfg, table, default_cls):
 
 class EnhancedAudioTextModel(nn.Module):
     """ref:315-697.  Encoders are built from architecture configs (there is no
-    network: weights are random-initialised or loaded with load_state_dict)."""
+    network: weights are random-initialised or loaded with load_state_dict).
+    spec_augment (default on, like the reference's w2v-bert config): SpecAugment time masking of
+    the audio encoder input in training mode (specaug.py)."""
 
     def __init__(self, text_model_name="sentence-transformers/paraphrase-multilingual-mpnet-base-v2",
                  audio_model_name="facebook/w2v-bert-2.0", projection_dim=768, text_embedding_dim=768,
                  audio_embedding_dim=1024, dropout=0.1, use_cross_modal=True, use_attentive_pooling=True,
                  use_word_alignment=False, freeze_encoders="partial", text_layers_to_unfreeze=5,
-                 audio_layers_to_unfreeze=5, device="cuda", spec_augment=False):
+                 audio_layers_to_unfreeze=5, device="cuda", spec_augment=True):
         super().__init__()
         if not use_attentive_pooling:
             raise NotImplementedError("use_attentive_pooling=False (CLS / mean pooling) is not built yet")
-        if spec_augment:
-            raise NotImplementedError("SpecAugment time masking (tf:…wav2vec2_bert…:944-988) is not built yet")
         self.text_cfg = _resolve(text_model_name, _TEXT_CONFIGS, TextConfig)
         self.audio_cfg = _resolve(audio_model_name, _AUDIO_CONFIGS, AudioConfig)
         with torch.device("meta"):  # no host-side weights: values are initialised in the HBM store

@@ -336,6 +336,16 @@ def copy2d(dst, src):
     return dst
 
 
+def spec_mask_fwd(x, spec, valid, embed):
+    """x[r] = embed where spec[r] and valid[r] (x fp32 [rows, cols]; spec int32 [rows])."""
+    call("ste_spec_mask_fwd", ptr(x), _ld(x), ptr(spec), ptr(valid), ptr(embed), x.shape[0], x.shape[1], _s())
+
+
+def spec_mask_bwd(dx, spec, valid, dembed=None):
+    """dembed += Σ dx[r] over the SpecAugment rows, and dx[r] = 0 there."""
+    call("ste_spec_mask_bwd", ptr(dx), _ld(dx), ptr(spec), ptr(valid), ptr(dembed), dx.shape[0], dx.shape[1], _s())
+
+
 def transpose16(src, dst=None):
     """dst [cols, rows] = srcᵀ for a 2-D bf16 (2-byte) matrix with unit column stride."""
     assert src.dim() == 2 and src.stride(1) == 1 and src.element_size() == 2

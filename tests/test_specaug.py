@@ -1,0 +1,134 @@
+"""SpecAugment time masking in training mode (w2v-bert, tf:…wav2vec2_bert…:800-988), which the
+reference applies whenever it trains (mask_time_prob 0.05 in w2v-bert-2.0).  Golden vectors:
+tests/golden/make_specaug_golden.py runs the REAL reference model in train mode with every
+dropout at 0, so SpecAugment's numpy draws are the only randomness.
+
+CPU: our span sampler reproduces transformers' mask from the same numpy seed; the oracle with
+that mask reproduces the reference's embeddings, loss and masked_spec_embed gradient.
+GPU: the HIP path in train mode, seeded the same way, matches them (bf16 bound)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import det_init, ref_model as R
+
+
+def _golden():
+    return json.loads((GOLDEN / "specaug_golden.json").read_text()), np.load(GOLDEN / "specaug_golden.npz")
+
+
+def _batch(z, dev="cpu"):
+    keys = ["input_ids_pos", "attention_mask_pos", "input_ids_neg", "attention_mask_neg", "input_values",
+            "attention_mask_audio"]
+    return {k: torch.from_numpy(z[k]).to(dev) for k in keys}
+
+
+def _cfg(meta):
+    a, t, m = meta["audio"], meta["text"], meta["mini"]
+    return R.ModelCfg(
+        audio=R.AudioCfg(hidden=a["hidden_size"], layers=a["num_hidden_layers"], heads=a["num_attention_heads"],
+                         inter=a["intermediate_size"], feat_in=a["feature_projection_input_dim"],
+                         left=a["left_max_position_embeddings"], right=a["right_max_position_embeddings"],
+                         conv_k=a["conv_depthwise_kernel_size"]),
+        text=R.TextCfg(hidden=t["hidden_size"], layers=t["num_hidden_layers"], heads=t["num_attention_heads"],
+                       inter=t["intermediate_size"], vocab=t["vocab_size"], max_pos=t["max_position_embeddings"],
+                       pad_id=t["pad_token_id"]),
+        projection_dim=m["projection_dim"], use_word_alignment=False, text_layers_to_unfreeze=m["unfreeze"],
+        audio_layers_to_unfreeze=m["unfreeze"])
+
+
+def test_span_sampler_matches_transformers():
+    from speech_transcript_embeddings_amd.specaug import compute_mask_indices
+    meta, z = _golden()
+    a = meta["audio"]
+    am = z["attention_mask_audio"]
+    np.random.seed(meta["seed"])
+    m = compute_mask_indices(am.shape, a["mask_time_prob"], a["mask_time_length"], am.sum(-1).tolist(),
+                             a["mask_time_min_masks"])
+    assert m.dtype == bool and np.array_equal(m, z["spec_mask"])
+    assert m.sum() > 0 and not m[1, am[1].sum():].any()  # spans stay inside each clip's frames
+    np.random.seed(7)
+    assert not compute_mask_indices((2, 40), 0.0, 4, None, 0).any()
+    with pytest.raises(ValueError):
+        compute_mask_indices((1, 3), 0.5, 4)
+
+
+def test_oracle_with_spec_mask_matches_reference():
+    meta, z = _golden()
+    cfg = _cfg(meta)
+    names = meta["names"]
+    shapes = dict(R.param_shapes(cfg, spec_augment=True))
+    vals = det_init.state_dict_values([(n, shapes[n]) for n in names if n in shapes])
+    with_grad = set(meta["with_grad"])
+    p = {n: torch.from_numpy(v).requires_grad_(n in with_grad) for n, v in vals.items()}
+    spec = torch.from_numpy(z["spec_mask"])
+    tpn, tnn, an, _ = R.compute_pos_neg_embeddings(p, _batch(z), cfg, spec_mask=spec)
+    np.testing.assert_allclose(an.detach().numpy(), z["aud"], atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(tpn.detach().numpy(), z["txt_pos"], atol=2e-6, rtol=1e-5)
+    loss = R.alignment_aware_infonce((an * tpn).sum(1), (an * tnn).sum(1))
+    np.testing.assert_allclose(loss.item(), float(z["loss"]), rtol=1e-5)
+    loss.backward()
+    g = p["audio_encoder.masked_spec_embed"].grad.numpy()
+    ref = z["g::audio_encoder.masked_spec_embed"]  # summed over 24 rows in another order: compare by norm
+    assert np.linalg.norm(g - ref) <= 1e-4 * np.linalg.norm(ref)
+
+
+@pytest.mark.gpu
+def test_hip_specaug_train_step_matches_reference():
+    from speech_transcript_embeddings_amd.model import AlignmentAwareInfoNCE, EnhancedAudioTextModel
+    from speech_transcript_embeddings_amd.modules import AudioConfig, TextConfig
+    meta, z = _golden()
+    a, t, m = meta["audio"], meta["text"], meta["mini"]
+    acfg = AudioConfig(hidden_size=a["hidden_size"], num_hidden_layers=a["num_hidden_layers"],
+                       num_attention_heads=a["num_attention_heads"], intermediate_size=a["intermediate_size"],
+                       mask_time_prob=a["mask_time_prob"], mask_time_length=a["mask_time_length"],
+                       mask_time_min_masks=a["mask_time_min_masks"], layerdrop=0.0, conformer_conv_dropout=0.0)
+    tcfg = TextConfig(vocab_size=t["vocab_size"], hidden_size=t["hidden_size"], num_hidden_layers=t["num_hidden_layers"],
+                      num_attention_heads=t["num_attention_heads"], intermediate_size=t["intermediate_size"],
+                      hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    model = EnhancedAudioTextModel(text_model_name=tcfg, audio_model_name=acfg, projection_dim=m["projection_dim"],
+                                   text_embedding_dim=t["hidden_size"], audio_embedding_dim=a["hidden_size"],
+                                   dropout=0.0, text_layers_to_unfreeze=m["unfreeze"],
+                                   audio_layers_to_unfreeze=m["unfreeze"])
+    sd = model.state_dict()
+    vals = det_init.state_dict_values([(n, v.shape) for n, v in sd.items()])
+    model.load_state_dict({n: torch.from_numpy(v) for n, v in vals.items()})
+    model.train()
+    batch = _batch(z, "cuda")
+    np.random.seed(meta["seed"])
+    tpn, tnn, an = EnhancedAudioTextModel.compute_pos_neg_embeddings(model, batch)
+
+    def rel(x, y):
+        x, y = torch.as_tensor(x).double().cpu(), torch.as_tensor(y).double().cpu()
+        return ((x - y).norm() / y.norm()).item()
+
+    assert rel(an, z["aud"]) < 2e-2 and rel(tpn, z["txt_pos"]) < 2e-2
+    loss = AlignmentAwareInfoNCE(0.1, 0.5)((an * tpn).sum(1), (an * tnn).sum(1))
+    assert rel(loss.item(), float(z["loss"])) < 2e-2
+    # backward with random cotangents against the oracle under the same span mask (the
+    # loss-derived cotangent is a near-cancelling difference of embeddings, see
+    # test_model_gpu.py::test_backward_random_cotangents)
+    gen = torch.Generator().manual_seed(3)
+    cots = [torch.randn(o.shape, generator=gen) for o in (tpn, tnn, an)]
+    torch.autograd.backward([tpn, tnn, an], [c.cuda() for c in cots])
+    cfg = _cfg(meta)
+    shapes = dict(R.param_shapes(cfg, spec_augment=True))
+    ovals = det_init.state_dict_values([(n, shapes[n]) for n in meta["names"] if n in shapes])
+    p = {n: torch.from_numpy(v).requires_grad_(n in set(meta["with_grad"])) for n, v in ovals.items()}
+    ro = R.compute_pos_neg_embeddings(p, _batch(z), cfg, spec_mask=torch.from_numpy(z["spec_mask"]))[:3]
+    torch.autograd.backward(list(ro), cots)
+    errs = {n: rel(model.get_parameter(n).grad, p[n].grad)
+            for n in ("audio_encoder.masked_spec_embed", "audio_encoder.feature_projection.projection.weight",
+                      "audio_encoder.feature_projection.layer_norm.weight")}
+    print("grad rel errors vs oracle (same spec mask):", errs)
+    for n, e in errs.items():
+        assert e < 2e-2, (n, e)
+    # eval mode draws nothing and masks nothing
+    model.eval()
+    st = np.random.get_state()
+    with torch.no_grad():
+        EnhancedAudioTextModel.compute_pos_neg_embeddings(model, batch)
+    assert np.array_equal(np.random.get_state()[1], st[1])
