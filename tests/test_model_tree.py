@@ -34,8 +34,13 @@ def test_full_size_tree_matches_reference(counts, key, align, k):
     assert all("text_encoder" in n or "audio_encoder" in n for n in enc)
     assert not any("text_encoder" in n or "audio_encoder" in n for n in head)
     nograd = {n for n, s in st.slots.items() if s.segment == "nograd"}
-    assert nograd == {"text_encoder.pooler.dense.weight", "text_encoder.pooler.dense.bias",
-                      "audio_encoder.masked_spec_embed"}
+    # the pooler output is unused (no gradient); masked_spec_embed receives SpecAugment's
+    # gradient in training mode (spec_augment=True, the default) and none without it
+    assert nograd == {"text_encoder.pooler.dense.weight", "text_encoder.pooler.dense.bias"}
+    assert st.slots["audio_encoder.masked_spec_embed"].segment == "enc"
+    off = EnhancedAudioTextModel(use_word_alignment=align, text_layers_to_unfreeze=k, audio_layers_to_unfreeze=k,
+                                 device="meta", spec_augment=False).store
+    assert off.slots["audio_encoder.masked_spec_embed"].segment == "nograd"
     # fused q/k/v adjacency
     for i in range(24):
         pre = f"audio_encoder.encoder.layers.{i}.self_attn."
