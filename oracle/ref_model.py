@@ -440,4 +440,5 @@ def mini_cfg(golden_json: dict) -> ModelCfg:
                      inter=tx["intermediate_size"], vocab=tx["vocab_size"], max_pos=tx["max_position_embeddings"],
                      pad_id=tx["pad_token_id"]),
         projection_dim=m["projection_dim"], use_word_alignment=golden_json["use_word_alignment"],
+        use_attentive_pooling=golden_json.get("use_attentive_pooling", True),
         text_layers_to_unfreeze=m["unfreeze"], audio_layers_to_unfreeze=m["unfreeze"])

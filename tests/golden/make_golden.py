@@ -134,14 +134,14 @@ def synth_batch(T, B=2, L=12, vocab=1000):
     return T.custom_collate_fn(items)
 
 
-def model_fixture(T, use_align: bool):
+def model_fixture(T, use_align: bool, attentive: bool = True):
     T.AutoModel = make_automodel_shim(MINI)
     torch.manual_seed(0)
     model = T.EnhancedAudioTextModel(
         text_model_name="xlmr-mini", audio_model_name="w2v-bert-mini",
         projection_dim=MINI["projection_dim"], text_embedding_dim=MINI["text"]["hidden_size"],
         audio_embedding_dim=MINI["audio"]["hidden_size"], dropout=0.1, use_cross_modal=True,
-        use_attentive_pooling=True, use_word_alignment=use_align, freeze_encoders="partial",
+        use_attentive_pooling=attentive, use_word_alignment=use_align, freeze_encoders="partial",
         text_layers_to_unfreeze=MINI["unfreeze"], audio_layers_to_unfreeze=MINI["unfreeze"])
     sd = model.state_dict()
     vals = det_init.state_dict_values([(n, t.shape) for n, t in sd.items() if t.is_floating_point()])
@@ -193,11 +193,11 @@ def model_fixture(T, use_align: bool):
             continue
         idx = det_init.sample_indices(n, p.numel())
         out[f"pnew::{n}"] = p.detach().reshape(-1).numpy()[idx]
-    cfg = {"mini": MINI, "use_word_alignment": use_align, "names": names, "trainable": trainable,
+    cfg = {"mini": MINI, "use_word_alignment": use_align, "use_attentive_pooling": attentive, "names": names, "trainable": trainable,
            "with_grad": with_grad, "lr": lr, "warmup": 2, "total_steps": 10, "sched_step": 1,
            "param_count": sum(p.numel() for p in model.parameters()),
            "trainable_count": sum(p.numel() for p in model.parameters() if p.requires_grad)}
-    tag = "align" if use_align else "noalign"
+    tag = ("align" if use_align else "noalign") if attentive else "nopool"
     np.savez_compressed(HERE / f"model_golden_{tag}.npz", **out)
     (HERE / f"model_golden_{tag}.json").write_text(json.dumps(cfg, indent=1))
     print(f"model_golden_{tag}.npz loss={loss.item():.6f} trainable={cfg['trainable_count']}")
@@ -232,5 +232,6 @@ if __name__ == "__main__":
     fbank_fixture(T)
     model_fixture(T, use_align=False)
     model_fixture(T, use_align=True)
+    model_fixture(T, use_align=False, attentive=False)  # CLS text / masked-mean audio (ref:578-580,621-636)
     if "--counts" in sys.argv:
         param_count_fixture(T)
