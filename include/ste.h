@@ -217,6 +217,16 @@ int ste_attn_pool_fwd(const void* t, const float* w2, const float* b2, const voi
 int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float* weights, const float* dpooled,
                       int B, int L, int Hh, int H, float* dh, void* dt, float* dw2, float* db2, void* stream);
 
+/* Pooling without the scorer, use_attentive_pooling=False
+ * (ref:training/trainer_unfreeze.py:578-580 text `last_hidden_state[:, 0, :]`, :621-636 audio
+ * masked mean `sum(h*m)/clamp(sum(m), 1e-9)`): h bf16 [B*L, H]; mask int32 [B*L] (NULL = all
+ * valid); cls != 0 selects row 0 of each sample. Outputs: weights fp32 [B*L] (the pooling
+ * weights, read by the backward), pooled fp32 [B,H] and bf16 [B,H] (optional). */
+int ste_mean_pool_fwd(const void* h, const int32_t* mask, int B, int L, int H, int cls, float* weights, float* pooled,
+                      void* pooled_bf16, void* stream);
+/* Backward of any fixed-weight pooling: dh fp32 [B*L,H] += weights[b,l] * dpooled fp32 [B,H]. */
+int ste_weighted_pool_bwd(const float* weights, const float* dpooled, int B, int L, int H, float* dh, void* stream);
+
 /* CrossModalAttention with a single query vector per sample
  * (ref:training/trainer_unfreeze.py:125-168 called with x.unsqueeze(1) at :653-667):
  * q fp32 [B,P]; k,v bf16 [B*S, P] (row stride ldkv); mask int32 [B*S] (NULL = all);

@@ -125,6 +125,9 @@ _SIGS = {
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     "ste_attn_pool_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ste_mean_pool_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                  c_void_p]),
+    "ste_weighted_pool_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "ste_xattn1_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                c_float, c_uint64, c_void_p, c_void_p, c_void_p]),
     "ste_xattn1_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

@@ -1,5 +1,5 @@
 // Head-side kernels of EnhancedAudioTextModel (ref = /root/reference/training/trainer_unfreeze.py):
-//   AttentivePooling core (ref:171-211) fwd/bwd
+//   AttentivePooling core (ref:171-211) fwd/bwd; CLS / masked-mean pooling (ref:578-580, 621-636)
 //   single-query CrossModalAttention core (ref:125-168, called with x.unsqueeze(1) at :653-667)
 //   F.normalize (ref:561-563), batch similarity matrix on the fp32 MFMA (ref:1073-1074),
 //   AlignmentAwareInfoNCE (ref:702-742) fwd/bwd.
@@ -121,6 +121,49 @@ __global__ __launch_bounds__(NT) void pool_bwd_kernel(const bf16* t, const float
     if (dw2) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) atomicAdd(dw2 + k + e, g2[e]);
+    }
+  }
+}
+
+// ------------------------------------------- CLS / masked-mean pooling (no scorer)
+// use_attentive_pooling=False (ref:578-580 text CLS, :621-636 audio masked mean).
+// weights[b][l] = CLS: [l == 0];  mean: mask[l] / max(sum(mask), 1e-9) (all-masked rows pool to 0).
+__global__ __launch_bounds__(NT) void mean_pool_fwd_kernel(const bf16* h, const int32_t* mask, int L, int H, int cls,
+                                                         float* weights, float* pooled, bf16* pooled_bf16) {
+  extern __shared__ float sc[];  // L weights
+  __shared__ float red[8];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  float cnt = 0.f;
+  for (int l = tid; l < L; l += NT) {
+    const float m = cls ? (l == 0 ? 1.f : 0.f) : (mask ? (mask[b * L + l] != 0 ? 1.f : 0.f) : 1.f);
+    sc[l] = m;
+    cnt += m;
+  }
+  cnt = block_sum(cnt, red);  // contains a barrier: sc is complete
+  const float inv = cls ? 1.f : 1.f / fmaxf(cnt, 1e-9f);
+  for (int l = tid; l < L; l += NT) weights[b * L + l] = sc[l] * inv;
+  const int Lr = cls ? 1 : L;  // CLS reads one row
+  for (int c = tid * 4; c < H; c += NT * 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int l = 0; l < Lr; ++l)
+      if (sc[l] != 0.f) acc += load_bf16x4(h + (int64_t)(b * L + l) * H + c);
+    acc *= inv;
+    *reinterpret_cast<f32x4*>(pooled + (int64_t)b * H + c) = acc;
+    if (pooled_bf16) store_bf16x4(pooled_bf16 + (int64_t)b * H + c, acc);
+  }
+}
+
+// dh[b][l][:] += weights[b][l] * dpooled[b][:]; grid (B, ceil(L/16)), rows with weight 0 untouched.
+__global__ __launch_bounds__(NT) void weighted_pool_bwd_kernel(const float* weights, const float* dpooled, int L,
+                                                             int H, float* dh) {
+  const int b = blockIdx.x, l0 = blockIdx.y * 16;
+  const float* dp = dpooled + (int64_t)b * H;
+  for (int l = l0; l < min(l0 + 16, L); ++l) {
+    const float wt = weights[b * L + l];
+    if (wt == 0.f) continue;
+    for (int c = threadIdx.x * 4; c < H; c += NT * 4) {
+      f32x4* o = reinterpret_cast<f32x4*>(dh + (int64_t)(b * L + l) * H + c);
+      *o = *o + *reinterpret_cast<const f32x4*>(dp + c) * wt;
     }
   }
 }
@@ -385,6 +428,24 @@ extern "C" int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, 
   if (B <= 0 || L <= 0 || (Hh & 3) || (H & 3) || L > 8192) return STE_ERR_SHAPE;
   hipLaunchKernelGGL(pool_bwd_kernel, dim3(B), dim3(NT), L * sizeof(float), (hipStream_t)stream, (const bf16*)t, w2,
                      (const bf16*)h, weights, dpooled, L, Hh, H, dh, (bf16*)dt, dw2, db2);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_mean_pool_fwd(const void* h, const int32_t* mask, int B, int L, int H, int cls, float* weights,
+                                 float* pooled, void* pooled_bf16, void* stream) {
+  if (B <= 0 || L <= 0 || (H & 3) || L > 16384) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(mean_pool_fwd_kernel, dim3(B), dim3(NT), L * sizeof(float), (hipStream_t)stream, (const bf16*)h,
+                     mask, L, H, cls, weights, pooled, (bf16*)pooled_bf16);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_weighted_pool_bwd(const float* weights, const float* dpooled, int B, int L, int H, float* dh,
+                                     void* stream) {
+  if (B <= 0 || L <= 0 || (H & 3)) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(weighted_pool_bwd_kernel, dim3(B, (L + 15) / 16), dim3(NT), 0, (hipStream_t)stream, weights,
+                     dpooled, L, H, dh);
   STE_CHECK_LAUNCH();
   return 0;
 }

@@ -473,9 +473,17 @@ class Engine:
         self._dw(dz, sv["xb"], name + ".projection.0.weight")
 
     def _pool_fwd(self, name, hb, mask32, nb, L, sv):
-        """AttentivePooling ref:171-211 -> pooled fp32 [nb, H] and bf16 copy."""
+        """AttentivePooling ref:171-211 -> pooled fp32 [nb, H] and bf16 copy.  With
+        use_attentive_pooling=False: text CLS row (ref:578-580) / audio masked mean (ref:621-636)."""
         s = self.s
         H = hb.shape[1]
+        if not self.m.use_attentive_pooling:
+            w = self._e(nb * L)
+            pooled = self._e(nb, H)
+            pooledb = self._e(nb, H, dtype=BF16)
+            ops.mean_pool_fwd(hb, mask32, nb, L, name == "text_pooling", w, pooled, pooledb)
+            sv.update(w=w)
+            return pooled, pooledb
         t = ops.linear(hb, s.w(name + ".attention.0.weight"), s.p(name + ".attention.0.bias"), act=ACT_TANH,
                        out_bf16=True)
         w = self._e(nb * L)
@@ -488,6 +496,9 @@ class Engine:
 
     def _pool_bwd(self, name, sv, dpooled, dh, nb, L):
         s = self.s
+        if not self.m.use_attentive_pooling:
+            ops.weighted_pool_bwd(sv["w"], dpooled, nb, L, dh)
+            return
         t = sv["t"]
         dz = self._e(*t.shape, dtype=BF16)
         gw2 = s.g(name + ".attention.2.weight")

@@ -56,8 +56,6 @@ class EnhancedAudioTextModel(nn.Module):
                  use_word_alignment=False, freeze_encoders="partial", text_layers_to_unfreeze=5,
                  audio_layers_to_unfreeze=5, device="cuda", spec_augment=True):
         super().__init__()
-        if not use_attentive_pooling:
-            raise NotImplementedError("use_attentive_pooling=False (CLS / mean pooling) is not built yet")
         self.text_cfg = _resolve(text_model_name, _TEXT_CONFIGS, TextConfig)
         self.audio_cfg = _resolve(audio_model_name, _AUDIO_CONFIGS, AudioConfig)
         with torch.device("meta"):  # no host-side weights: values are initialised in the HBM store
@@ -108,8 +106,9 @@ class EnhancedAudioTextModel(nn.Module):
                                              nn.LayerNorm(projection_dim))
             self.audio_fusion = nn.Sequential(nn.Linear(2 * projection_dim, projection_dim),
                                               nn.LayerNorm(projection_dim))
-        self.text_pooling = AttentivePooling(text_embedding_dim)
-        self.audio_pooling = AttentivePooling(audio_embedding_dim)
+        if use_attentive_pooling:  # else CLS text / masked-mean audio, no parameters (ref:480-482)
+            self.text_pooling = AttentivePooling(text_embedding_dim)
+            self.audio_pooling = AttentivePooling(audio_embedding_dim)
         if use_word_alignment:
             self.word_level_alignment = WordLevelAlignmentModule(self.text_hidden_dim, self.audio_hidden_dim,
                                                                  projection_dim, dropout=dropout)

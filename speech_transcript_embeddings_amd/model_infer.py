@@ -49,8 +49,6 @@ class EnhancedAudioTextModel(nn.Module):
                  audio_embedding_dim=1024, dropout=0.1, use_cross_modal=True, use_attentive_pooling=True,
                  freeze_encoders=True, device="cuda"):
         super().__init__()
-        if not use_attentive_pooling:
-            raise NotImplementedError("use_attentive_pooling=False (CLS / mean pooling) is not built yet")
         self.text_cfg = _resolve(text_model_name, _TEXT_CONFIGS, TextConfig)
         self.audio_cfg = _resolve(audio_model_name, _AUDIO_CONFIGS, AudioConfig)
         if use_cross_modal and not (self.text_cfg.hidden_size == self.audio_cfg.hidden_size == projection_dim):
@@ -76,8 +74,9 @@ class EnhancedAudioTextModel(nn.Module):
                                                  nn.LayerNorm(projection_dim))
                 self.audio_fusion = nn.Sequential(nn.Linear(2 * projection_dim, projection_dim),
                                                   nn.LayerNorm(projection_dim))
-            self.text_pooling = AttentivePooling(text_embedding_dim)
-            self.audio_pooling = AttentivePooling(audio_embedding_dim)
+            if use_attentive_pooling:  # else CLS text / masked-mean audio (ref model.py:214-216, 255-270)
+                self.text_pooling = AttentivePooling(text_embedding_dim)
+                self.audio_pooling = AttentivePooling(audio_embedding_dim)
         self.store = ParamStore(self, device, has_grad=set())  # forward only: no gradient buffer
         _TrainModel._init_params(self)
         self.store.sync_shadow(force=True)

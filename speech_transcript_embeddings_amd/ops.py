@@ -234,6 +234,15 @@ def attn_pool_bwd(t, w2, h, weights, dpooled, B, L, dh, dz, dw2=None, db2=None):
          ptr(dh), ptr(dz), ptr(dw2), ptr(db2), _s())
 
 
+def mean_pool_fwd(h, mask, B, L, cls, weights, pooled, pooled_bf16=None):
+    call("ste_mean_pool_fwd", ptr(h), ptr(mask), B, L, h.shape[-1], int(bool(cls)), ptr(weights), ptr(pooled),
+         ptr(pooled_bf16), _s())
+
+
+def weighted_pool_bwd(weights, dpooled, B, L, dh):
+    call("ste_weighted_pool_bwd", ptr(weights), ptr(dpooled), B, L, dh.shape[-1], ptr(dh), _s())
+
+
 def xattn1_fwd(q, k, v, mask, B, S, nh, probs, out, drop_p=0.0, seed=0):
     P = q.shape[-1]
     call("ste_xattn1_fwd", ptr(q), ptr(k), ptr(v), _ld(k), ptr(mask), B, S, P, nh, float((P // nh) ** -0.5),

@@ -353,6 +353,37 @@ def test_attn_pool(ops):
     assert abs(db2.item() - b2r.grad.item()) < 1e-4
 
 
+@pytest.mark.parametrize("cls", [False, True])
+def test_mean_pool(ops, cls):
+    """use_attentive_pooling=False: text CLS row (ref:578-580), audio masked mean with
+    clamp(sum(mask), 1e-9) (ref:621-636): a ragged row and an all-masked row (pools to 0)."""
+    torch.manual_seed(5)
+    B, L, H = 4, 37, 1024
+    h = torch.randn(B * L, H, device=DEV).bfloat16()
+    mask = torch.ones(B, L, dtype=torch.int32, device=DEV)
+    mask[1, 20:] = 0
+    mask[2] = 0
+    weights = torch.empty(B * L, device=DEV)
+    pooled = torch.empty(B, H, device=DEV)
+    pooledb = torch.empty(B, H, device=DEV, dtype=torch.bfloat16)
+    ops.mean_pool_fwd(h, mask, B, L, cls, weights, pooled, pooledb)
+    hr = h.float().view(B, L, H).clone().requires_grad_()
+    if cls:
+        pref = hr[:, 0, :]
+    else:
+        m = mask.view(B, L, 1).expand(B, L, H).long()
+        pref = (hr * m).sum(1) / torch.clamp(m.sum(1), min=1e-9)
+    assert rel_err(pooled, pref) < 1e-6
+    assert (pooledb.float() - pooled).abs().max().item() <= pooled.abs().max().item() * 2 ** -8
+    if not cls:
+        assert pooled[2].abs().max().item() == 0.0
+    dp = torch.randn(B, H, device=DEV)
+    pref.backward(dp)
+    dh = torch.ones(B * L, H, device=DEV)  # += semantics
+    ops.weighted_pool_bwd(weights, dp, B, L, dh)
+    assert rel_err(dh - 1.0, hr.grad.view(B * L, H)) < 1e-6
+
+
 @pytest.mark.parametrize("drop_p", [0.0, 0.1])
 def test_xattn1(ops, drop_p):
     torch.manual_seed(4)

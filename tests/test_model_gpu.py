@@ -29,7 +29,8 @@ def mini_model(meta, **kw):
     model = EnhancedAudioTextModel(text_model_name=tcfg, audio_model_name=acfg, projection_dim=m["projection_dim"],
                                    text_embedding_dim=tx["hidden_size"], audio_embedding_dim=au["hidden_size"],
                                    use_word_alignment=meta["use_word_alignment"], text_layers_to_unfreeze=m["unfreeze"],
-                                   audio_layers_to_unfreeze=m["unfreeze"], **kw)
+                                   audio_layers_to_unfreeze=m["unfreeze"],
+                                   use_attentive_pooling=meta.get("use_attentive_pooling", True), **kw)
     sd = model.state_dict()
     vals = det_init.state_dict_values([(n, t.shape) for n, t in sd.items()])
     model.load_state_dict({n: torch.from_numpy(v) for n, v in vals.items()})
@@ -77,7 +78,7 @@ def _grad_errors(model, meta, batch_cpu):
     return sorted(out, reverse=True), lo.item()
 
 
-@pytest.mark.parametrize("tag", ["noalign", "align"])
+@pytest.mark.parametrize("tag", ["noalign", "align", "nopool"])
 def test_backward_random_cotangents(tag):
     """Backward of the whole model for random output cotangents vs the oracle's autograd.
 
@@ -158,7 +159,7 @@ def test_backward_random_cotangents(tag):
         assert e < 3e-2, (n, e)
 
 
-@pytest.mark.parametrize("tag", ["noalign", "align"])
+@pytest.mark.parametrize("tag", ["noalign", "align", "nopool"])
 def test_forward_backward_matches_golden_and_oracle(tag):
     meta, z = load(tag)
     model = mini_model(meta)

@@ -60,3 +60,28 @@ def test_forward_requires_gpu_tensors():
         EnhancedAudioTextModel.compute_pos_neg_embeddings(m, batch)
     with pytest.raises(ValueError):
         m({"input_values": batch["input_values"]})
+
+
+@pytest.mark.parametrize("tag", ["noalign", "align", "nopool"])
+def test_mini_tree_matches_reference(tag):
+    """Mini-dim trees (incl. use_attentive_pooling=False: no *_pooling modules, ref:480-482)
+    have the reference's state_dict keys and trainable set (model_golden_<tag>.json)."""
+    from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
+    from speech_transcript_embeddings_amd.modules import AudioConfig, TextConfig
+    meta = json.loads((GOLDEN / f"model_golden_{tag}.json").read_text())
+    mm = meta["mini"]
+    au, tx = mm["audio"], mm["text"]
+    acfg = AudioConfig(hidden_size=au["hidden_size"], num_hidden_layers=au["num_hidden_layers"],
+                       num_attention_heads=au["num_attention_heads"], intermediate_size=au["intermediate_size"],
+                       mask_time_prob=0.0, layerdrop=0.0)
+    tcfg = TextConfig(vocab_size=tx["vocab_size"], hidden_size=tx["hidden_size"],
+                      num_hidden_layers=tx["num_hidden_layers"], num_attention_heads=tx["num_attention_heads"],
+                      intermediate_size=tx["intermediate_size"])
+    m = EnhancedAudioTextModel(text_model_name=tcfg, audio_model_name=acfg, projection_dim=mm["projection_dim"],
+                               text_embedding_dim=tx["hidden_size"], audio_embedding_dim=au["hidden_size"],
+                               use_word_alignment=meta["use_word_alignment"],
+                               use_attentive_pooling=meta.get("use_attentive_pooling", True),
+                               text_layers_to_unfreeze=mm["unfreeze"], audio_layers_to_unfreeze=mm["unfreeze"],
+                               device="meta")
+    assert list(m.state_dict().keys()) == meta["names"]
+    assert sorted(n for n, p in m.named_parameters() if p.requires_grad) == sorted(meta["trainable"])
