@@ -96,6 +96,21 @@ int ste_gemm_kernel(const ste_gemm_args* args);
  * into buf[len]; bench.py keys its HIP-event timings and PMC traffic by it. */
 int ste_gemm_kernel_name(const ste_gemm_args* args, char* buf, int len);
 
+/* MX-fp8 forward GEMM (BASELINE config 5, "fp8 MFMA GEMMs"): the nn.Linear forwards of the
+ * Conformer layers (tf:…wav2vec2_bert…:134-154 FFN, :229-337 q/k/v/o, :157-226 pointwise convs)
+ * with both operands in OCP e4m3 and one E8M0 scale per 32 consecutive k of a row (OCP MX
+ * block scaling), on v_mfma_scale_f32_16x16x128_f8f6f4.  args as for ste_gemm with a_kc =
+ * b_kc = 1 and A/B pointing at e4m3 bytes (lda/ldb in bytes, multiples of 16, K % 128 == 0,
+ * batch 1, no split-K); a_scales [M][K/32], b_scales [N][K/32] bytes.  Every epilogue option
+ * of ste_gemm applies to the fp32 accumulators unchanged.  q_out/q_scales (optional, N % 128
+ * == 0): the final values also leave MX-fp8 quantised ([M][N] e4m3, [M][N/32] E8M0), the input
+ * of the next MX-fp8 GEMM; args->C may then be NULL (no bf16/fp32 copy). */
+int ste_gemm_mx8(const ste_gemm_args* args, const void* a_scales, const void* b_scales, void* q_out, void* q_scales,
+                 void* stream);
+/* bf16 x [rows][K] (row stride ldx) -> e4m3 q [rows][K] and E8M0 scales [rows][K/32]:
+ * scale 2^e, e = ceil(log2(amax/448)) per 32-element block (no saturation; zero blocks 2^-127). */
+int ste_mx8_quant(const void* x, int64_t ldx, int rows, int K, void* q, void* scales, void* stream);
+
 /* ------------------------------------------------------------- LayerNorm --
  * Replaces nn.LayerNorm forward/backward (every LN of both encoders and the
  * heads: tf:…wav2vec2_bert…:122,169,181,381-394; tf:…xlm_roberta…:64,333,389;

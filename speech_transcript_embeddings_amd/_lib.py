@@ -121,6 +121,8 @@ _SIGS = {
                                    c_void_p]),
     "ste_fbank": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p,
                           c_void_p]),
+    "ste_gemm_mx8": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ste_mx8_quant": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "ste_attn_pool_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     "ste_attn_pool_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

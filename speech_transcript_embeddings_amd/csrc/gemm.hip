@@ -110,8 +110,43 @@ STE_DEV void st8(void* p, bool is_bf16, f32x8 v, bool full, int nval) {
   else store_f32x8((float*)p, v);
 }
 
+// MX-fp8 block quantisation of 8 values held by each of 4 consecutive lanes (one 32-element
+// block): scale 2^e with e = ceil(log2(amax/448)) (no saturation; zero blocks 2^-127), OCP e4m3
+// values to q[0..7], the E8M0 byte to *s from the block's first lane.  Used by ste_mx8_quant and
+// by the GEMM epilogue's fp8 output (the FFN intermediate feeding the next MX-fp8 GEMM).
+STE_DEV void mx8_block_store(f32x8 v, uint8_t* q, uint8_t* s, int lane) {
+  float amax = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+  amax = fmaxf(amax, __shfl_xor(amax, 1));
+  amax = fmaxf(amax, __shfl_xor(amax, 2));
+  int ex = -127;
+  if (amax > 0.f) {
+    int e2;
+    const float m = frexpf(amax * (1.0f / 448.0f), &e2);  // amax/448 = m·2^e2, m in [0.5, 1)
+    ex = max(-127, min(127, (m == 0.5f) ? e2 - 1 : e2));   // ceil(log2(amax/448))
+  }
+  const float inv = ldexpf(1.0f, -ex);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = fminf(fmaxf(v[e] * inv, -448.f), 448.f);
+  uint32_t lo = 0, hi = 0;
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], lo, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], lo, true);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], hi, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6], v[7], hi, true);
+  *reinterpret_cast<uint2*>(q) = make_uint2(lo, hi);
+  if ((lane & 3) == 0) *s = (uint8_t)(ex + 127);
+}
+
+struct Q8Out {  // optional MX-fp8 copy of a GEMM output: q [M][ldq] e4m3, s [M][ldq/32] E8M0
+  uint8_t* q;
+  uint8_t* s;
+  int64_t ldq;
+};
+
 STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, int row0, int col0, int col1,
-                           int batch, int lane, Csum& csum, int ld = EPI_LD, bool swz16 = false) {
+                           int batch, int lane, Csum& csum, int ld = EPI_LD, bool swz16 = false,
+                           const Q8Out* q8 = nullptr) {
   const int cl = (lane & 7) * 8;  // staged column of this lane's 8
   const int col = cl < 32 ? col0 + cl : col1 + (cl - 32);
   const int nval = p.N - col;     // valid columns from `col`
@@ -163,7 +198,9 @@ STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, 
     }
     char* cp = (char*)p.C + (offC + (int64_t)row * p.ldc + col) * (p.c_bf16 ? 2 : 4);
     if (p.beta != 0.f) v += ld8(cp, p.c_bf16, full, nval) * p.beta;
-    st8(cp, p.c_bf16, v, full, nval);
+    if (q8) mx8_block_store(v, q8->q + (int64_t)row * q8->ldq + col, q8->s + (int64_t)row * (q8->ldq >> 5) + (col >> 5),
+                            lane);
+    if (p.C) st8(cp, p.c_bf16, v, full, nval);
     if (p.C3) st8((bf16*)p.C3 + offC + (int64_t)row * p.ldc3 + col, true, v, full, nval);
   }
 }
@@ -1361,4 +1398,193 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
   if (a.a_kc && !a.b_kc) return launch_small<true, false>(a, s);
   if (!a.a_kc && !a.b_kc) return launch_small<false, false>(a, s);
   return launch_small<false, true>(a, s);
+}
+
+// ============================================================ MX-fp8 GEMM (config 5)
+// Y = X·Wᵀ with both operands OCP e4m3 (KC, k contiguous) and E8M0 block scales, one per 32
+// consecutive k of a row ([rows][K/32] bytes): v_mfma_scale_f32_16x16x128_f8f6f4, which runs at
+// twice the bf16 MFMA rate (MI355X_MICROARCH.md, matrix cores).  Same 256x256 tile, 8 waves
+// (2(M) x 4(N), 128x64 each), 2-deep global_load_lds ring and general epilogue as gemm_big;
+// a K-tile is 128 fp8 = 128 B per row, so the LDS image and its swizzle are gemm_big's.
+// Operand lane map of the 16x16x128 form (probed on the box with exact integer data,
+// scratch/mx8_probe.hip): lane l holds row l&15, bytes 0-15 = k 16g..16g+15 and bytes 16-31 =
+// k 64+16g..+15 (g = l>>4); the scale of row r's k-block kb is read from lane r + 16·kb.  So
+// lane l supplies the scale of its own row and k-block g.
+namespace mx8 {
+constexpr int BM = 256, BN = 256, BK = 128, NT = 512;
+constexpr int TILE_BYTES = BM * BK;             // 32 KiB per operand per stage
+constexpr int SC_BYTES = BM * 4;                // 4 scale bytes per row per K-tile
+constexpr int STAGE_BYTES = 2 * TILE_BYTES + 2 * SC_BYTES;
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;      // 132 KiB
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+
+STE_DEV void issue_tile(const uint8_t* base, int64_t ld, int row0, int rows, int k0, char* tile, int wave,
+                        int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave * 4 + i;
+    const int r = piece * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ (lane >> 3);
+    const int gr = min(row0 + r, rows - 1);
+    const uint8_t* src = base + (int64_t)gr * ld + k0 + ch * 16;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(tile + piece * 1024), 16, 0, 0);
+  }
+}
+// waves 0-3: A scales of rows 64w..64w+63; waves 4-7: B scales.  One dword (4 k-blocks) per row.
+STE_DEV void issue_scales(const uint8_t* sa, const uint8_t* sb, int64_t lds_a, int64_t lds_b, int m0, int M, int n0,
+                          int N, int k0, char* stage, int wave, int lane) {
+  const bool isb = wave >= 4;
+  const int r = (wave & 3) * 64 + lane;
+  const uint8_t* src = isb ? sb + (int64_t)min(n0 + r, N - 1) * lds_b + (k0 >> 5)
+                           : sa + (int64_t)min(m0 + r, M - 1) * lds_a + (k0 >> 5);
+  char* dst = stage + 2 * TILE_BYTES + (isb ? SC_BYTES : 0) + (wave & 3) * 256;
+  __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 4, 0, 0);
+}
+STE_DEV i32x8 frag(const char* tile, int rb, int lane) {
+  const int r = rb + (lane & 15), g = lane >> 4;
+  const i32x4v lo = *reinterpret_cast<const i32x4v*>(tile + r * 128 + ((g ^ (r & 7)) << 4));
+  const i32x4v hi = *reinterpret_cast<const i32x4v*>(tile + r * 128 + (((g + 4) ^ (r & 7)) << 4));
+  return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+STE_DEV int scale(const char* sc, int rb, int lane) {
+  return *reinterpret_cast<const int*>(sc + (rb + (lane & 15)) * 4) >> (8 * (lane >> 4));
+}
+}  // namespace mx8
+
+__global__ __launch_bounds__(mx8::NT, 1) void gemm_mx8_kernel(ste_gemm_args p, const uint8_t* sa, const uint8_t* sb,
+                                                              Q8Out q8o) {
+  using namespace mx8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int num_m = (p.M + BM - 1) / BM, num_n = (p.N + BN - 1) / BN;
+  int batch, tm, tn;
+  map_tile(gridDim.x, num_m, num_n, batch, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const uint8_t* A = (const uint8_t*)p.A;
+  const uint8_t* B = (const uint8_t*)p.B;
+  const int64_t lsa = p.K >> 5, lsb = p.K >> 5;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / BK;
+  issue_tile(A, p.lda, m0, p.M, 0, smem, wave, lane);
+  issue_tile(B, p.ldb, n0, p.N, 0, smem + TILE_BYTES, wave, lane);
+  issue_scales(sa, sb, lsa, lsb, m0, p.M, n0, p.N, 0, smem, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      char* nxt = smem + (cur ^ 1) * STAGE_BYTES;
+      issue_tile(A, p.lda, m0, p.M, (kt + 1) * BK, nxt, wave, lane);
+      issue_tile(B, p.ldb, n0, p.N, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+      issue_scales(sa, sb, lsa, lsb, m0, p.M, n0, p.N, (kt + 1) * BK, nxt, wave, lane);
+    }
+    const char* ta = smem + cur * STAGE_BYTES;
+    const char* tb = ta + TILE_BYTES;
+    const char* sca = ta + 2 * TILE_BYTES;
+    const char* scb = sca + SC_BYTES;
+    i32x8 fb[4];
+    int sbv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      fb[j] = frag(tb, wn * 64 + j * 16, lane);
+      sbv[j] = scale(scb, wn * 64 + j * 16, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const i32x8 fa = frag(ta, wm * 128 + i * 16, lane);
+      const int sav = scale(sca, wm * 128 + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa, fb[j], acc[i][j], 0, 0, 0, sav, 0, sbv[j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  float* epi = reinterpret_cast<float*>(smem) + wave * big::EPI_ROWS * EPI_LD;
+  Csum csum = {};
+  constexpr bool EPI_SKIP = false;
+#define EPI_COL0 (n0 + wn * 64)
+#define EPI_COL1 (n0 + wn * 64 + 32)
+#define STE_EPI_PASS(PS)                                                                                     \
+  {                                                                                                          \
+    for (int ii = 0; ii < 2; ++ii) {                                                                         \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                                        \
+        _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                                      \
+          epi[(ii * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[2 * (PS) + ii][j][r];   \
+        }                                                                                                    \
+      }                                                                                                      \
+    }                                                                                                        \
+    __builtin_amdgcn_s_waitcnt(0xc07f);                                                                      \
+    __builtin_amdgcn_wave_barrier();                                                                         \
+    for (int hh = 0; hh < big::EPI_ROWS; hh += 16) {                                                         \
+      if (!EPI_SKIP) epilogue_tile(p, epi + hh * EPI_LD, 16, m0 + wm * 128 + (PS) * big::EPI_ROWS + hh,     \
+                                   EPI_COL0, EPI_COL1, batch, lane, csum, EPI_LD, false, q8o.q ? &q8o : nullptr);                                   \
+    }                                                                                                        \
+    __builtin_amdgcn_s_waitcnt(0xc07f);                                                                      \
+    __builtin_amdgcn_wave_barrier();                                                                         \
+  }
+  STE_EPI_PASS(0) STE_EPI_PASS(1) STE_EPI_PASS(2) STE_EPI_PASS(3)
+#undef STE_EPI_PASS
+#undef EPI_COL0
+#undef EPI_COL1
+  if (p.colsum) colsum_flush(p, csum, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane);
+}
+
+// bf16 [rows][K] (row stride ld) -> e4m3 [rows][K] + E8M0 [rows][K/32].  Block scale 2^e with
+// e = ceil(log2(amax/448)): the largest element maps to <= 448 (no saturation), zero blocks
+// get 2^-127.  4 lanes (8 elements each) per 32-element block.
+__global__ __launch_bounds__(256) void mx8_quant_kernel(const bf16* x, int64_t ld, int rows, int K, uint8_t* q,
+                                                        uint8_t* sc) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int per_row = K >> 3;
+  const int64_t r = t / per_row;  // K % 128 == 0: a 4-lane block never straddles rows
+  const int c = (int)(t - r * per_row) * 8;
+  if (r >= rows) return;
+  mx8_block_store(load_bf16x8(x + r * ld + c), q + r * K + c, sc + r * (K >> 5) + (c >> 5), threadIdx.x);
+}
+
+extern "C" int ste_mx8_quant(const void* x, int64_t ldx, int rows, int K, void* q, void* scales, void* stream) {
+  if (rows <= 0 || K <= 0 || (K & 127) || ldx < K || (ldx & 7)) return STE_ERR_SHAPE;
+  const int64_t threads = (int64_t)rows * (K >> 3);
+  hipLaunchKernelGGL(mx8_quant_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)x, ldx, rows, K, (uint8_t*)q, (uint8_t*)scales);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_gemm_mx8(const ste_gemm_args* args, const void* a_scales, const void* b_scales, void* q_out,
+                            void* q_scales, void* stream) {
+  if (!args || !a_scales || !b_scales || (!args->C && !q_out) || (!q_out != !q_scales)) return STE_ERR_ARG;
+  if (q_out && ((args->N & 127) || (((uintptr_t)q_out) & 7) || args->colsum)) return STE_ERR_SHAPE;
+  ste_gemm_args a = *args;
+  a.batch = 1;
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0) return STE_ERR_ARG;
+  if (!a.a_kc || !a.b_kc || (a.K & 127) || (a.lda & 15) || (a.ldb & 15) || a.lda < a.K || a.ldb < a.K || a.ws)
+    return STE_ERR_SHAPE;
+  if (a.drop_ld == 0) a.drop_ld = a.N;
+  auto misaligned = [&a](const void* ptr, int64_t ld, int esz) {
+    return a.N >= 8 && ptr && ((((uintptr_t)ptr) & 15) || ((ld * esz) & 15));
+  };
+  if (misaligned(a.C, a.ldc, a.c_bf16 ? 2 : 4) || misaligned(a.C2, a.ldc2, 2) || misaligned(a.C3, a.ldc3, 2) ||
+      misaligned(a.R, a.ldr, a.r_bf16 ? 2 : 4) || misaligned(a.Z, a.ldz, 2) || misaligned(a.bias, 0, 4) ||
+      (((uintptr_t)a.A) & 15) || (((uintptr_t)a.B) & 15) || (((uintptr_t)a_scales) & 3) ||
+      (((uintptr_t)b_scales) & 3))
+    return STE_ERR_SHAPE;
+  const int nb = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  const Q8Out q8o = {(uint8_t*)q_out, (uint8_t*)q_scales, a.N};
+  hipLaunchKernelGGL(gemm_mx8_kernel, dim3(nb), dim3(mx8::NT), mx8::LDS_BYTES, (hipStream_t)stream, a,
+                     (const uint8_t*)a_scales, (const uint8_t*)b_scales, q8o);
+  STE_CHECK_LAUNCH();
+  return 0;
 }

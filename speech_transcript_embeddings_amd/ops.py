@@ -31,12 +31,15 @@ def _ld(t: torch.Tensor) -> int:
 def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf16=False, bias=None,
          act=_lib.ACT_NONE, pre_out=None, z=None, residual=None, alpha=1.0, beta=0.0, colsum=None,
          row_scale=None, drop_p=0.0, seed=0, out_bf16_copy=None, batch=1, stride_a=0, stride_b=0, stride_c=0,
-         stride_r=0, drop_ld=0, ws=None):
+         stride_r=0, drop_ld=0, ws=None, mx8=None):
     """out[M,N] = epilogue(alpha * A·B).  See include/ste.h for the epilogue order.
 
     a_kc: A is [M,K] row-major (else [K,M]);  b_kc: B is [N,K] row-major (else [K,N]).
     """
-    assert a.dtype == BF16 and b.dtype == BF16, "GEMM operands are bf16"
+    if mx8 is not None:  # (a_scales, b_scales): e4m3 operands with E8M0 block scales (ste_gemm_mx8)
+        assert a.dtype == torch.uint8 and b.dtype == torch.uint8 and a_kc and b_kc, "MX-fp8 GEMM operands"
+    else:
+        assert a.dtype == BF16 and b.dtype == BF16, "GEMM operands are bf16"
     if M is None:
         M = a.shape[-2] if a_kc else a.shape[-1]
     if K is None:
@@ -45,12 +48,17 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
         N = b.shape[-2] if b_kc else b.shape[-1]
     if out is None:
         out = torch.empty((M, N), device=a.device, dtype=BF16 if out_bf16 else F32)
+    elif out is False:
+        assert mx8 is not None and len(mx8) > 2, "out=False: MX-fp8 GEMM with an fp8 output only"
     args = GemmArgs()
     args.M, args.N, args.K, args.batch = M, N, K, batch
     args.A, args.lda, args.a_kc = ptr(a), _ld(a), int(a_kc)
     args.B, args.ldb, args.b_kc = ptr(b), _ld(b), int(b_kc)
     args.strideA, args.strideB, args.strideC, args.strideR = stride_a, stride_b, stride_c, stride_r
-    args.C, args.ldc, args.c_bf16 = ptr(out), _ld(out), int(out.dtype == BF16)
+    if out is not False:
+        args.C, args.ldc, args.c_bf16 = ptr(out), _ld(out), int(out.dtype == BF16)
+    else:
+        args.ldc, args.c_bf16 = N, int(out_bf16)
     if pre_out is not None:
         args.C2, args.ldc2 = ptr(pre_out), _ld(pre_out)
     if out_bf16_copy is not None:
@@ -72,6 +80,12 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
     if ws is not None:  # split-K workspace (weight gradients), see include/ste.h
         assert ws.dtype == F32 and ws.is_contiguous()
         args.ws, args.ws_bytes = ptr(ws), ws.numel() * 4
+    if mx8 is not None:
+        q8 = mx8[2] if len(mx8) > 2 else (None, None)
+        if out is False:  # fp8 copy only
+            args.C = None
+        call("ste_gemm_mx8", C.byref(args), ptr(mx8[0]), ptr(mx8[1]), ptr(q8[0]), ptr(q8[1]), _s())
+        return q8 if out is False else out
     if GEMM_TRACE is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -97,6 +111,24 @@ def gemm_kernel_name(args: GemmArgs) -> str:
 def linear(x, w, bias=None, **kw):
     """y = x·wᵀ (+bias) with x [M,K] bf16, w [N,K] bf16 (nn.Linear layout)."""
     return gemm(x, w, a_kc=True, b_kc=True, bias=bias, **kw)
+
+
+def mx8_quant(x, q=None, scales=None):
+    """bf16 [rows, K] -> (e4m3 bytes [rows, K], E8M0 scales [rows, K/32]) (ste_mx8_quant)."""
+    rows, K = x.shape
+    if q is None:
+        q = torch.empty((rows, K), device=x.device, dtype=torch.uint8)
+    if scales is None:
+        scales = torch.empty((rows, K // 32), device=x.device, dtype=torch.uint8)
+    call("ste_mx8_quant", ptr(x), _ld(x), rows, K, ptr(q), ptr(scales), _s())
+    return q, scales
+
+
+def linear_mx8(xq, wq, bias=None, q_out=None, **kw):
+    """y = x·wᵀ (+bias) on the MX-fp8 GEMM: xq = (e4m3 [M,K], scales), wq = (e4m3 [N,K], scales).
+    q_out = (e4m3 [M,N], scales [M,N/32]): also write y MX-fp8 quantised; with out=False only that."""
+    mx8 = (xq[1], wq[1]) if q_out is None else (xq[1], wq[1], q_out)
+    return gemm(xq[0], wq[0], a_kc=True, b_kc=True, bias=bias, mx8=mx8, **kw)
 
 
 def linear_dx(dy, w, **kw):

@@ -106,6 +106,55 @@ def test_gemm_dw_splitk(ops, M, N, K, ws_mb):
     assert (kern >= 12) == (K >= 16 * 64), kern
 
 
+def _mx8_dequant(q, sc):
+    """e4m3 bytes + E8M0 block scales -> fp64 (torch's float8_e4m3fn is the OCP encoding)."""
+    v = q.view(torch.float8_e4m3fn).double()
+    e = sc.long().repeat_interleave(32, dim=1) - 127
+    return v * torch.pow(2.0, e.double())
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 768, 1024), (4000, 3072, 1024), (2000, 1024, 4096), (300, 2048, 128)])
+def test_gemm_mx8(ops, M, N, K):
+    """MX-fp8 GEMM (config 5): exact on the dequantised operands (fp32 accumulation), quantiser
+    bit-exact against torch's e4m3 cast with the same block scale, and a few % from bf16."""
+    torch.manual_seed(8)
+    x = (torch.randn(M, K, device=DEV) * torch.rand(M, 1, device=DEV) * 4).bfloat16()
+    x[3, 64:96] = 0  # a zero block
+    w = (torch.randn(N, K, device=DEV) * 0.03).bfloat16()
+    xq = ops.mx8_quant(x)
+    wq = ops.mx8_quant(w)
+    # quantiser: e = ceil(log2(amax/448)) per 32-block, q = e4m3(x / 2^e)
+    xb = x.float().view(M, K // 32, 32)
+    amax = xb.abs().amax(-1)
+    e = torch.where(amax > 0, torch.ceil(torch.log2(amax / 448.0)), torch.full_like(amax, -127.0)).clamp(-127, 127)
+    assert torch.equal(xq[1].long() - 127, e.long())
+    qref = (xb / torch.pow(2.0, e).unsqueeze(-1)).view(M, K).to(torch.float8_e4m3fn).view(torch.uint8)
+    assert (xq[0] != qref).float().mean().item() < 1e-4
+    ref = _mx8_dequant(*xq) @ _mx8_dequant(*wq).T
+    y = ops.linear_mx8(xq, wq)
+    assert rel_err(y.double(), ref) < 1e-4  # fp32 accumulation order (1.5e-5 measured at K=1024)
+    ybf = x.double() @ w.double().T
+    assert rel_err(y.double(), ybf) < 5e-2
+    # epilogue options ride on the fp32 accumulators unchanged: bias + swish + pre-activation
+    bias = torch.randn(N, device=DEV)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    yb = ops.linear_mx8(xq, wq, bias, act=1, out_bf16=True, pre_out=pre)
+    z = ref + bias.double()
+    assert rel_err(pre.double(), z) < 1e-2
+    assert rel_err(yb.double(), z * torch.sigmoid(z)) < 1e-2
+    # fp8 output of the epilogue (the FFN intermediate feeding the next MX-fp8 GEMM) equals the
+    # quantiser applied to the fp32 output; out=False writes only the fp8 copy
+    yf = torch.empty(M, N, device=DEV)
+    q = (torch.empty(M, N, device=DEV, dtype=torch.uint8), torch.empty(M, N // 32, device=DEV, dtype=torch.uint8))
+    ops.linear_mx8(xq, wq, bias, act=1, out=yf, q_out=q)
+    qr = ops.mx8_quant(yf.bfloat16())  # reference quantiser (bf16 input: compare dequantised values)
+    assert rel_err(_mx8_dequant(*q), yf.double()) < 4e-2
+    assert (q[1].long() - qr[1].long()).abs().max().item() <= 1
+    q2 = (torch.zeros_like(q[0]), torch.zeros_like(q[1]))
+    assert ops.linear_mx8(xq, wq, bias, act=1, out=False, q_out=q2) is q2
+    assert torch.equal(q2[0], q[0]) and torch.equal(q2[1], q[1])
+
+
 def test_gemm_epilogues(ops):
     from speech_transcript_embeddings_amd import _lib
     torch.manual_seed(1)
