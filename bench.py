@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BF16_PEAK_TFLOPS = 2516.6          # MI355X dense bf16 MFMA (256 CU x 4096 FLOP/clk x 2.4 GHz)
+FP8_PEAK_TFLOPS = 5033.2           # dense MX-fp8 (scaled 16x16x128 f8f6f4: 2x the bf16 rate)
 GFLOP_PER_PAIR = {3: 1370.4, 5: 1429.5}   # SURVEY §8(d) algorithmic fwd+bwd FLOPs per pair (c2/c3, c4)
 GFLOP_FWD_PER_PAIR = 641.8                 # SURVEY §8(d) forward only: 615.1 audio + 21.7 text + ≈5 heads
 
@@ -48,6 +49,8 @@ def parse():
     ap.add_argument("--align", action="store_true", help="config 4: word-alignment head")
     ap.add_argument("--freeze", default="partial", choices=["partial", "none", "full"],
                     help="freeze_encoders (config 5 = none: every encoder layer trainable)")
+    ap.add_argument("--fp8", action="store_true",
+                    help="config 5's fp8 MFMA GEMMs: the Conformer forward GEMMs on MX-fp8 (e4m3, 32-k block scales)")
     ap.add_argument("--eval", action="store_true",
                     help="time the forward-only evaluation step (SURVEY §8f rank 1, ref evaluate() :1165-1284): "
                          "GPU fbank -> forward without saved activations -> similarity + InfoNCE value")
@@ -154,7 +157,8 @@ def main():
 
     model = EnhancedAudioTextModel(use_word_alignment=args.align, text_layers_to_unfreeze=args.unfreeze,
                                    audio_layers_to_unfreeze=args.unfreeze, freeze_encoders=args.freeze,
-                                   device=f"cuda:{local}", spec_augment=False)  # timed without SpecAugment
+                                   device=f"cuda:{local}", spec_augment=False,  # timed without SpecAugment
+                                   fp8_gemm=args.fp8)
     model.audio_cfg.layerdrop = 0.0
     step = TrainStep(model, warmup=100, total_steps=100000)
     B, nsamp, L = args.batch, int(args.seconds * 16000), args.tokens
@@ -213,15 +217,17 @@ def main():
         (args.unfreeze, args.align) in ((3, False), (5, True))
     gflop = (GFLOP_FWD_PER_PAIR if args.eval else GFLOP_PER_PAIR[args.unfreeze]) if known else None
     cname = {(3, False): "c2" if world == 1 else "c3", (5, True): "c4"}.get((args.unfreeze, args.align), "custom") \
-        if args.seconds == 10.0 and args.freeze == "partial" else ("c5-shape (bf16 GEMMs)" if args.freeze == "none"
-                                                                    else "custom")
+        if args.seconds == 10.0 and args.freeze == "partial" else (
+            ("c5-shape (MX-fp8 Conformer fwd GEMMs)" if args.fp8 else "c5-shape (bf16 GEMMs)") if args.freeze == "none"
+            else "custom")
+    peak = FP8_PEAK_TFLOPS if dom == "gemm_mx8_kernel" else BF16_PEAK_TFLOPS
     traffic, traffic_src = hbm_traffic(dom)
     out = {
         "metric": ("evaluated audio–text pairs/sec, forward only (whole node), 10s@16kHz + 64-tok" if args.eval else
                    "audio–text pairs/sec (whole node), 10s@16kHz + 64-tok, 1/2/4/8 MI355X"),
         "value": round(pairs, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "bf16",
+        "vs_baseline": None, "dtype": "bf16 + mxfp8-e4m3 (Conformer fwd GEMMs)" if args.fp8 else "bf16",
         "data": "synthetic (SURVEY §8d waveforms + token ids), random-init weights",
         "config": {"workload": f"{cname} per GPU: {B} pairs x ({args.seconds:g}s@16kHz audio + {L}-tok clean + "
                                f"{L}-tok corrupt), w2v-bert-2.0 Conformer 24L + XLM-R-base 12L, "
@@ -233,8 +239,8 @@ def main():
                    "seq_len_text": L, "parallelism": f"dp{world}"},
         "step_roofline_frac": round(pairs * gflop / (world * BF16_PEAK_TFLOPS * 1e3), 4) if gflop else None,
         "roofline": {"bound": "mfma", "kernel": dom, "launches_per_step": n_l // args.steps,
-                     "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
                      "avg_launch_us": round(tm / n_l * 1e6, 2), "algorithmic_gflop_per_launch": round(fl / n_l / 1e9, 3),
                      "gemm_ms_per_step_all_variants": round(gemm_time * 1e3, 2)},

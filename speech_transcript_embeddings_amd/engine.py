@@ -55,6 +55,11 @@ class Engine:
         # audio side's bandwidth-bound kernels.  STE_TEXT_STREAM=0: one stream (A/B runs).
         self.overlap = os.environ.get("STE_TEXT_STREAM", "1") != "0"
 
+    @property
+    def fp8(self):
+        """MX-fp8 forward GEMMs in the Conformer layers (model fp8_gemm=True, BASELINE config 5)."""
+        return bool(getattr(self.m, "fp8_gemm", False))
+
     WS_BYTES = 80 << 20   # split-K slabs of the weight-gradient GEMMs (largest: 7 x 3072 x 768 fp32)
 
     @property
@@ -157,46 +162,64 @@ class Engine:
         eps = c.layer_norm_eps
         tr = s.trainable_layer(pre + "ffn1_layer_norm.weight")
         sv = {"tr": tr, "seed": seed}
+        fp8 = self.fp8
+
+        def lin(xb, wname, bias, count=1, **kw):
+            """Forward nn.Linear: bf16 MFMA, or MX-fp8 (fp8_gemm: x block-quantised here unless it
+            arrives quantised as an (e4m3, scales) pair, W from ParamStore.wq)."""
+            if fp8:
+                xq = xb if isinstance(xb, tuple) else ops.mx8_quant(xb)
+                return ops.linear_mx8(xq, s.wq(wname, count), bias, **kw)
+            return ops.linear(xb, s.fused(wname, count, "w") if count > 1 else s.w(wname), bias, **kw)
+
+        def ffn_in(a, wname, bname, z):
+            """FFN intermediate (swish): bf16 output, and under fp8_gemm the MX-fp8 copy the output
+            GEMM reads; the bf16 copy is kept only for the trained layers' weight gradients."""
+            if not fp8:
+                h = lin(a, wname, s.p(bname), act=ACT_SWISH, pre_out=z, out_bf16=True)
+                return h, h
+            q = (self._e(M, F_, dtype=torch.uint8), self._e(M, F_ // 32, dtype=torch.uint8))
+            h = self._e(M, F_, dtype=BF16) if (tr and save) else False
+            lin(a, wname, s.p(bname), act=ACT_SWISH, pre_out=z, out=h, out_bf16=True, q_out=q)
+            return (h if h is not False else None), q
+
         # -- FFN1 (half-step)
         a1 = self._e(M, D, dtype=BF16)
         sv["st1"] = self._ln(x, pre + "ffn1_layer_norm", eps, yb=a1)
         z1 = self._e(M, F_, dtype=BF16) if save else None  # swish pre-activation, for backward only
-        h1 = ops.linear(a1, s.w(pre + "ffn1.intermediate_dense.weight"), s.p(pre + "ffn1.intermediate_dense.bias"),
-                        act=ACT_SWISH, pre_out=z1, out_bf16=True)
-        x1 = ops.linear(h1, s.w(pre + "ffn1.output_dense.weight"), s.p(pre + "ffn1.output_dense.bias"), alpha=0.5,
-                        residual=x)
+        h1, h1in = ffn_in(a1, pre + "ffn1.intermediate_dense.weight", pre + "ffn1.intermediate_dense.bias", z1)
+        x1 = lin(h1in, pre + "ffn1.output_dense.weight", s.p(pre + "ffn1.output_dense.bias"), alpha=0.5,
+                 residual=x)
         # -- relative-key MHSA
         a2 = self._e(M, D, dtype=BF16)
         sv["st2"] = self._ln(x1, pre + "self_attn_layer_norm", eps, yb=a2)
-        qkv = ops.linear(a2, s.fused(pre + "self_attn.linear_q.weight", 3, "w"),
-                         s.fused(pre + "self_attn.linear_q.bias", 3, "p"), out_bf16=True)
+        qkv = lin(a2, pre + "self_attn.linear_q.weight", s.fused(pre + "self_attn.linear_q.bias", 3, "p"), count=3,
+                  out_bf16=True)
         o = self._e(M, D, dtype=BF16)
         lse = self._e(b * H * T)
         ops.attention_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B=b, T=T, H=H, o=o, lse=lse, key_mask=mask32,
                           rel_E=s.w(pre + "self_attn.distance_embedding.weight"),
                           rel_left=c.left_max_position_embeddings, rel_right=c.right_max_position_embeddings,
                           scale=1.0 / math.sqrt(D // H))
-        x2 = ops.linear(o, s.w(pre + "self_attn.linear_out.weight"), s.p(pre + "self_attn.linear_out.bias"),
-                        residual=x1)
+        x2 = lin(o, pre + "self_attn.linear_out.weight", s.p(pre + "self_attn.linear_out.bias"), residual=x1)
         # -- convolution module
         a3 = self._e(M, D, dtype=BF16)
         sv["st3"] = self._ln(x2, pre + "conv_module.layer_norm", eps, yb=a3, row_scale=maskf)
-        pw1 = ops.linear(a3, s.w(pre + "conv_module.pointwise_conv1.weight"), None, out_bf16=True)
+        pw1 = lin(a3, pre + "conv_module.pointwise_conv1.weight", None, out_bf16=True)
         cv = self._e(M, D, dtype=BF16)
         ops.glu_dwconv_fwd(pw1, s.p(pre + "conv_module.depthwise_conv.weight").view(D, -1), cv, b, T)
         sw = self._e(M, D, dtype=BF16)
         sv["st4"] = self._ln(cv, pre + "conv_module.depthwise_layer_norm", eps, yb=sw, act=ACT_SWISH)
         p_conv = c.conformer_conv_dropout if train else 0.0
-        x3 = ops.linear(sw, s.w(pre + "conv_module.pointwise_conv2.weight"), None, residual=x2, drop_p=p_conv,
-                        seed=_site_seed(seed, 1))
+        x3 = lin(sw, pre + "conv_module.pointwise_conv2.weight", None, residual=x2, drop_p=p_conv,
+                 seed=_site_seed(seed, 1))
         # -- FFN2 (half-step) + final LN
         a5 = self._e(M, D, dtype=BF16)
         sv["st5"] = self._ln(x3, pre + "ffn2_layer_norm", eps, yb=a5)
         z2 = self._e(M, F_, dtype=BF16) if save else None
-        h2 = ops.linear(a5, s.w(pre + "ffn2.intermediate_dense.weight"), s.p(pre + "ffn2.intermediate_dense.bias"),
-                        act=ACT_SWISH, pre_out=z2, out_bf16=True)
-        x4 = ops.linear(h2, s.w(pre + "ffn2.output_dense.weight"), s.p(pre + "ffn2.output_dense.bias"), alpha=0.5,
-                        residual=x3)
+        h2, h2in = ffn_in(a5, pre + "ffn2.intermediate_dense.weight", pre + "ffn2.intermediate_dense.bias", z2)
+        x4 = lin(h2in, pre + "ffn2.output_dense.weight", s.p(pre + "ffn2.output_dense.bias"), alpha=0.5,
+                 residual=x3)
         x5 = self._e(M, D)
         x5b = self._e(M, D, dtype=BF16) if want_bf16 else None
         sv["st6"] = self._ln(x4, pre + "final_layer_norm", eps, y=x5, yb=x5b)

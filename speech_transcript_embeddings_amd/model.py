@@ -48,14 +48,18 @@ class EnhancedAudioTextModel(nn.Module):
     """ref:315-697.  Encoders are built from architecture configs (there is no
     network: weights are random-initialised or loaded with load_state_dict).
     spec_augment (default on, like the reference's w2v-bert config): SpecAugment time masking of
-    the audio encoder input in training mode (specaug.py)."""
+    the audio encoder input in training mode (specaug.py).
+    fp8_gemm (BASELINE config 5, "fp8 MFMA GEMMs"; default off): the Conformer layers' forward
+    nn.Linear GEMMs run MX-fp8 (e4m3 operands, E8M0 scales per 32 k; ste_gemm_mx8), gradients
+    stay bf16 (straight-through: dX/dW GEMMs read the bf16 weights and saved bf16 activations)."""
 
     def __init__(self, text_model_name="sentence-transformers/paraphrase-multilingual-mpnet-base-v2",
                  audio_model_name="facebook/w2v-bert-2.0", projection_dim=768, text_embedding_dim=768,
                  audio_embedding_dim=1024, dropout=0.1, use_cross_modal=True, use_attentive_pooling=True,
                  use_word_alignment=False, freeze_encoders="partial", text_layers_to_unfreeze=5,
-                 audio_layers_to_unfreeze=5, device="cuda", spec_augment=True):
+                 audio_layers_to_unfreeze=5, device="cuda", spec_augment=True, fp8_gemm=False):
         super().__init__()
+        self.fp8_gemm = fp8_gemm
         self.text_cfg = _resolve(text_model_name, _TEXT_CONFIGS, TextConfig)
         self.audio_cfg = _resolve(audio_model_name, _AUDIO_CONFIGS, AudioConfig)
         with torch.device("meta"):  # no host-side weights: values are initialised in the HBM store

@@ -84,18 +84,24 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
         q8 = mx8[2] if len(mx8) > 2 else (None, None)
         if out is False:  # fp8 copy only
             args.C = None
-        call("ste_gemm_mx8", C.byref(args), ptr(mx8[0]), ptr(mx8[1]), ptr(q8[0]), ptr(q8[1]), _s())
-        return q8 if out is False else out
+
+        def launch():
+            call("ste_gemm_mx8", C.byref(args), ptr(mx8[0]), ptr(mx8[1]), ptr(q8[0]), ptr(q8[1]), _s())
+        name = "gemm_mx8_kernel"
+    else:
+        def launch():
+            call("ste_gemm", C.byref(args), _s())
+        name = None
     if GEMM_TRACE is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
-        call("ste_gemm", C.byref(args), _s())
+        launch()
         ev1.record()
-        GEMM_TRACE.append((gemm_kernel_name(args), 2.0 * M * N * K * batch, ev0, ev1))
+        GEMM_TRACE.append((name or gemm_kernel_name(args), 2.0 * M * N * K * batch, ev0, ev1))
     else:
-        call("ste_gemm", C.byref(args), _s())
-    return out
+        launch()
+    return q8 if out is False else out
 
 
 GEMM_TRACE = None  # list while bench.py measures per-launch GEMM durations with HIP events

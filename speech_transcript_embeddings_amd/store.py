@@ -122,6 +122,7 @@ class ParamStore:
         self.params = params
         self._versions = {}
         self._wt = {}          # (name, count) -> (Wᵀ bf16, param versions, opt_epoch) (see wt())
+        self._wq = {}          # (name, count) -> ((W e4m3, E8M0 scales), versions, opt_epoch) (see wq())
         self.opt_epoch = 0     # fused optimizer steps so far (each refreshes the shadow of every trained weight)
         self.sync_shadow(force=True)
 
@@ -155,6 +156,29 @@ class ParamStore:
             return None
         base = self.grad[s.offset:s.offset + n]
         return base.view(s.shape[0] * count, *s.shape[1:]) if len(s.shape) > 1 else base
+
+    def _group_versions(self, name, count):
+        s = self.slots[name]
+        if count == 1:
+            names = [name]
+        else:
+            names = [n for n, t in self.slots.items() if s.offset <= t.offset < s.offset + s.numel * count]
+        return tuple(self.params[n]._version for n in names), s.segment in ("enc", "head")
+
+    def wq(self, name: str, count: int = 1):
+        """W as MX-fp8 (e4m3 [out, in] + E8M0 scales [out, in/32]), the B operand of the MX-fp8
+        forward GEMMs (model fp8_gemm=True, BASELINE config 5).  Quantised from the bf16 shadow
+        and cached with wt()'s invalidation rules (optimizer step for trained weights, _version
+        for writes outside it)."""
+        key = (name, count)
+        versions, trained = self._group_versions(name, count)
+        ent = self._wq.get(key)
+        if ent is not None and ent[1] == versions and (not trained or ent[2] == self.opt_epoch):
+            return ent[0]
+        src = self.fused(name, count, "w") if count > 1 else self.w(name)
+        q = ops.mx8_quant(src, *(ent[0] if ent is not None else (None, None)))
+        self._wq[key] = (q, versions, self.opt_epoch)
+        return q
 
     def wt(self, name: str, count: int = 1):
         """Wᵀ as a contiguous bf16 [in, out] matrix (the KC operand of dX = dY·W; `count` > 1:
