@@ -201,7 +201,7 @@ def main():
 
     # dominant-kernel roofline from per-launch HIP event timings of the timed steps
     agg = {}
-    for name, flops, e0, e1 in trace:
+    for name, flops, e0, e1, _shape in trace:
         a = agg.setdefault(name, [0, 0.0, 0.0])
         a[0] += 1
         a[1] += flops

@@ -131,6 +131,8 @@ typedef struct {
   const float* row_scale;           /* optional */
   int act;                          /* STE_ACT_NONE or STE_ACT_SWISH */
   float drop_p; uint64_t seed;      /* dropout on the output (index row*cols+col) */
+  void* q8; void* q8s; int64_t ldq8; /* MX-fp8 output (optional, cols % 128 == 0): e4m3 [rows][ldq8]
+                                        + E8M0 [rows][cols/32], the input of ste_gemm_mx8 */
 } ste_ln_fwd_args;
 int ste_layernorm_fwd(const ste_ln_fwd_args* a, void* stream);
 

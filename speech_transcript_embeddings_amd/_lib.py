@@ -59,6 +59,7 @@ class LnFwdArgs(C.Structure):
         ("row_scale", c_void_p),
         ("act", c_int),
         ("drop_p", c_float), ("seed", c_uint64),
+        ("q8", c_void_p), ("q8s", c_void_p), ("ldq8", c_int64),
     ]
 
 

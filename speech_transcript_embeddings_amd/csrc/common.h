@@ -52,6 +52,14 @@ STE_DEV double wave_sum_d(double v) {
 }
 
 // ---------------------------------------------------------------- activations
+// OCP MX block-scale exponent for e4m3 payloads: e = ceil(log2(amax/448)) (the block's largest
+// element maps to <= 448, no saturation), -127 (2^-127) for an all-zero block.
+STE_DEV int mx8_exp(float amax) {
+  if (!(amax > 0.f)) return -127;
+  int e2;
+  const float m = frexpf(amax * (1.0f / 448.0f), &e2);  // amax/448 = m·2^e2, m in [0.5, 1)
+  return max(-127, min(127, (m == 0.5f) ? e2 - 1 : e2));
+}
 STE_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 STE_DEV float swish_f(float x) { return x * sigmoidf_(x); }
 STE_DEV float swish_d(float x) {

@@ -120,12 +120,7 @@ STE_DEV void mx8_block_store(f32x8 v, uint8_t* q, uint8_t* s, int lane) {
   for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
   amax = fmaxf(amax, __shfl_xor(amax, 1));
   amax = fmaxf(amax, __shfl_xor(amax, 2));
-  int ex = -127;
-  if (amax > 0.f) {
-    int e2;
-    const float m = frexpf(amax * (1.0f / 448.0f), &e2);  // amax/448 = m·2^e2, m in [0.5, 1)
-    ex = max(-127, min(127, (m == 0.5f) ? e2 - 1 : e2));   // ceil(log2(amax/448))
-  }
+  const int ex = mx8_exp(amax);
   const float inv = ldexpf(1.0f, -ex);
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = fminf(fmaxf(v[e] * inv, -448.f), 448.f);

@@ -70,6 +70,21 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(ste_ln_fwd_args a) {
       }
       if (a.y) *reinterpret_cast<f32x4*>(a.y + (int64_t)row * a.ldy + col) = y;
       if (a.yb) store_bf16x4((bf16*)a.yb + (int64_t)row * a.ldyb + col, y);
+      if (a.q8) {  // MX-fp8 copy: 8 lanes x 4 columns = one 32-column block
+        float am = fmaxf(fmaxf(fabsf(y[0]), fabsf(y[1])), fmaxf(fabsf(y[2]), fabsf(y[3])));
+        am = fmaxf(am, __shfl_xor(am, 1));
+        am = fmaxf(am, __shfl_xor(am, 2));
+        am = fmaxf(am, __shfl_xor(am, 4));
+        const int ex = mx8_exp(am);
+        const float inv = ldexpf(1.0f, -ex);
+        uint32_t w = 0;
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(y[0] * inv, -448.f), 448.f),
+                                            fminf(fmaxf(y[1] * inv, -448.f), 448.f), w, false);
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(y[2] * inv, -448.f), 448.f),
+                                            fminf(fmaxf(y[3] * inv, -448.f), 448.f), w, true);
+        *reinterpret_cast<uint32_t*>((uint8_t*)a.q8 + (int64_t)row * a.ldq8 + col) = w;
+        if ((lane & 7) == 0) ((uint8_t*)a.q8s)[(int64_t)row * (a.cols >> 5) + (col >> 5)] = (uint8_t)(ex + 127);
+      }
     }
   }
 }
@@ -181,6 +196,8 @@ inline int grid_for(int rows, int cap = 1024) {
 extern "C" int ste_layernorm_fwd(const ste_ln_fwd_args* a, void* stream) {
   if (!a || a->rows <= 0 || a->cols <= 0 || (a->cols & 3) || a->cols > 2048 || !a->mean || !a->rstd)
     return STE_ERR_ARG;
+  if (a->q8 && (!a->q8s || (a->cols & 127) || a->ldq8 < a->cols || (a->ldq8 & 3) || (((uintptr_t)a->q8) & 3)))
+    return STE_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(grid_for(a->rows));
   if (a->cols <= 256) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(NT), 0, s, *a);

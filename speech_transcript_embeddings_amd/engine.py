@@ -183,17 +183,27 @@ class Engine:
             lin(a, wname, s.p(bname), act=ACT_SWISH, pre_out=z, out=h, out_bf16=True, q_out=q)
             return (h if h is not False else None), q
 
+        def ln_in(xin, name, st, **kw):
+            """LayerNorm feeding a Linear: bf16 output, or under fp8_gemm the MX-fp8 copy written by
+            the LN kernel itself (bf16 kept only for the trained layers' weight gradients)."""
+            if not fp8:
+                y = self._e(M, D, dtype=BF16)
+                sv[st] = self._ln(xin, name, eps, yb=y, **kw)
+                return y, y
+            y = self._e(M, D, dtype=BF16) if (tr and save) else None
+            q = (self._e(M, D, dtype=torch.uint8), self._e(M, D // 32, dtype=torch.uint8))
+            sv[st] = self._ln(xin, name, eps, yb=y, q8=q, **kw)
+            return y, q
+
         # -- FFN1 (half-step)
-        a1 = self._e(M, D, dtype=BF16)
-        sv["st1"] = self._ln(x, pre + "ffn1_layer_norm", eps, yb=a1)
+        a1, a1in = ln_in(x, pre + "ffn1_layer_norm", "st1")
         z1 = self._e(M, F_, dtype=BF16) if save else None  # swish pre-activation, for backward only
-        h1, h1in = ffn_in(a1, pre + "ffn1.intermediate_dense.weight", pre + "ffn1.intermediate_dense.bias", z1)
+        h1, h1in = ffn_in(a1in, pre + "ffn1.intermediate_dense.weight", pre + "ffn1.intermediate_dense.bias", z1)
         x1 = lin(h1in, pre + "ffn1.output_dense.weight", s.p(pre + "ffn1.output_dense.bias"), alpha=0.5,
                  residual=x)
         # -- relative-key MHSA
-        a2 = self._e(M, D, dtype=BF16)
-        sv["st2"] = self._ln(x1, pre + "self_attn_layer_norm", eps, yb=a2)
-        qkv = lin(a2, pre + "self_attn.linear_q.weight", s.fused(pre + "self_attn.linear_q.bias", 3, "p"), count=3,
+        a2, a2in = ln_in(x1, pre + "self_attn_layer_norm", "st2")
+        qkv = lin(a2in, pre + "self_attn.linear_q.weight", s.fused(pre + "self_attn.linear_q.bias", 3, "p"), count=3,
                   out_bf16=True)
         o = self._e(M, D, dtype=BF16)
         lse = self._e(b * H * T)
@@ -203,21 +213,18 @@ class Engine:
                           scale=1.0 / math.sqrt(D // H))
         x2 = lin(o, pre + "self_attn.linear_out.weight", s.p(pre + "self_attn.linear_out.bias"), residual=x1)
         # -- convolution module
-        a3 = self._e(M, D, dtype=BF16)
-        sv["st3"] = self._ln(x2, pre + "conv_module.layer_norm", eps, yb=a3, row_scale=maskf)
-        pw1 = lin(a3, pre + "conv_module.pointwise_conv1.weight", None, out_bf16=True)
+        a3, a3in = ln_in(x2, pre + "conv_module.layer_norm", "st3", row_scale=maskf)
+        pw1 = lin(a3in, pre + "conv_module.pointwise_conv1.weight", None, out_bf16=True)
         cv = self._e(M, D, dtype=BF16)
         ops.glu_dwconv_fwd(pw1, s.p(pre + "conv_module.depthwise_conv.weight").view(D, -1), cv, b, T)
-        sw = self._e(M, D, dtype=BF16)
-        sv["st4"] = self._ln(cv, pre + "conv_module.depthwise_layer_norm", eps, yb=sw, act=ACT_SWISH)
+        sw, swin = ln_in(cv, pre + "conv_module.depthwise_layer_norm", "st4", act=ACT_SWISH)
         p_conv = c.conformer_conv_dropout if train else 0.0
-        x3 = lin(sw, pre + "conv_module.pointwise_conv2.weight", None, residual=x2, drop_p=p_conv,
+        x3 = lin(swin, pre + "conv_module.pointwise_conv2.weight", None, residual=x2, drop_p=p_conv,
                  seed=_site_seed(seed, 1))
         # -- FFN2 (half-step) + final LN
-        a5 = self._e(M, D, dtype=BF16)
-        sv["st5"] = self._ln(x3, pre + "ffn2_layer_norm", eps, yb=a5)
+        a5, a5in = ln_in(x3, pre + "ffn2_layer_norm", "st5")
         z2 = self._e(M, F_, dtype=BF16) if save else None
-        h2, h2in = ffn_in(a5, pre + "ffn2.intermediate_dense.weight", pre + "ffn2.intermediate_dense.bias", z2)
+        h2, h2in = ffn_in(a5in, pre + "ffn2.intermediate_dense.weight", pre + "ffn2.intermediate_dense.bias", z2)
         x4 = lin(h2in, pre + "ffn2.output_dense.weight", s.p(pre + "ffn2.output_dense.bias"), alpha=0.5,
                  residual=x3)
         x5 = self._e(M, D)

@@ -98,7 +98,7 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
         ev0.record()
         launch()
         ev1.record()
-        GEMM_TRACE.append((name or gemm_kernel_name(args), 2.0 * M * N * K * batch, ev0, ev1))
+        GEMM_TRACE.append((name or gemm_kernel_name(args), 2.0 * M * N * K * batch, ev0, ev1, (M, N, K, batch)))
     else:
         launch()
     return q8 if out is False else out
@@ -149,7 +149,7 @@ def linear_dw(dy, x, **kw):
 
 # -------------------------------------------------------------- LayerNorm
 def layernorm_fwd(x, gamma, beta, eps, *, y=None, yb=None, mean=None, rstd=None, row_scale=None,
-                  act=_lib.ACT_NONE, drop_p=0.0, seed=0):
+                  act=_lib.ACT_NONE, drop_p=0.0, seed=0, q8=None):
     rows, cols = x.shape
     if mean is None:
         mean = torch.empty(rows, device=x.device, dtype=F32)
@@ -166,6 +166,8 @@ def layernorm_fwd(x, gamma, beta, eps, *, y=None, yb=None, mean=None, rstd=None,
     a.mean, a.rstd = ptr(mean), ptr(rstd)
     a.row_scale = ptr(row_scale)
     a.act, a.drop_p, a.seed = int(act), float(drop_p), int(seed) & (2**64 - 1)
+    if q8 is not None:  # (e4m3 [rows, cols], E8M0 [rows, cols/32]): MX-fp8 copy for ste_gemm_mx8
+        a.q8, a.q8s, a.ldq8 = ptr(q8[0]), ptr(q8[1]), _ld(q8[0])
     call("ste_layernorm_fwd", C.byref(a), _s())
     return mean, rstd
 

@@ -155,6 +155,26 @@ def test_gemm_mx8(ops, M, N, K):
     assert torch.equal(q2[0], q[0]) and torch.equal(q2[1], q[1])
 
 
+def test_layernorm_mx8_output(ops):
+    """LN forward's fused MX-fp8 copy (fp8_gemm: the LN feeding a Conformer Linear): scales are
+    ceil(log2(amax/448)) of the fp32 output's 32-column blocks, payload = e4m3(y / 2^e)."""
+    torch.manual_seed(6)
+    rows, cols = 777, 1024
+    x = torch.randn(rows, cols, device=DEV) * 3 + 1
+    g, b = torch.randn(cols, device=DEV), torch.randn(cols, device=DEV) * 0.1
+    y = torch.empty(rows, cols, device=DEV)
+    q = (torch.empty(rows, cols, device=DEV, dtype=torch.uint8),
+         torch.empty(rows, cols // 32, device=DEV, dtype=torch.uint8))
+    ops.layernorm_fwd(x, g, b, 1e-5, y=y, q8=q, act=1)
+    yb = y.view(rows, cols // 32, 32)
+    amax = yb.abs().amax(-1)
+    e = torch.where(amax > 0, torch.ceil(torch.log2(amax / 448.0)), torch.full_like(amax, -127.0)).clamp(-127, 127)
+    assert torch.equal(q[1].long() - 127, e.long())
+    qref = (yb / torch.pow(2.0, e).unsqueeze(-1)).view(rows, cols).to(torch.float8_e4m3fn).view(torch.uint8)
+    assert (q[0] != qref).float().mean().item() < 1e-4
+    assert rel_err(_mx8_dequant(*q), y.double()) < 4e-2
+
+
 def test_gemm_epilogues(ops):
     from speech_transcript_embeddings_amd import _lib
     torch.manual_seed(1)
