@@ -1,7 +1,7 @@
 """The fused training step and its optimizer tail, single GPU or data-parallel.
 
 One step (the body of ref:training/trainer_unfreeze.py:train_epoch, ref:1057-1117, with
-accumulation_steps = 1):
+accumulation_steps micro-batches per optimizer step, 1 by default):
     GPU fbank from raw waveforms (replaces the 12 CPU DataLoader workers' extractor calls)
  -> forward (engine.py)  -> L2-normalise -> B x 2B similarity on the fp32 MFMA
  -> AlignmentAwareInfoNCE -> backward (engine.py)
@@ -281,8 +281,17 @@ class TrainStep:
     """fbank -> forward -> loss -> backward -> all-reduce -> clip + AdamW (+ schedule)."""
 
     def __init__(self, model: EnhancedAudioTextModel, lr=2.1e-3, warmup=100, total_steps=10000, temperature=0.1,
-                 alignment_weight=0.5, corrupt_gamma=0.35, max_norm=1.0, pad_value=1.0, gather_embeddings=True):
+                 alignment_weight=0.5, corrupt_gamma=0.35, max_norm=1.0, pad_value=1.0, gather_embeddings=True,
+                 accumulation_steps=1):
+        """accumulation_steps (ref train_epoch :1064-1117): each call is one micro-batch whose loss
+        gradient is scaled by 1/accumulation_steps and summed into the flat gradient buffer; the
+        data-parallel sync, clip, AdamW and scheduler step run on every accumulation_steps-th
+        call (the sync overlapped with that micro-batch's backward) and on flush(), the
+        reference's `is_last_batch` step after a partial window."""
         self.model = model
+        self.acc = max(1, int(accumulation_steps))
+        self._micro = 0
+        self._ids = []
         self.opt = FusedAdamW(model, lr=lr, max_norm=max_norm)
         self.sched = LinearWarmupSchedule(warmup, total_steps)
         self.gradsync = GradSync(model.store, pad_id=model.text_cfg.pad_token_id)
@@ -326,22 +335,46 @@ class TrainStep:
         # backward
         dsp, dsn = e(B), e(B)
         dal = e(B, L) if align is not None else None
-        ops.pair_loss_bwd(sp, sn, align, B, L, self.tau, self.aw, self.gamma, None, dsp, dsn, dal)
+        gscale = None if self.acc == 1 else torch.full((1,), 1.0 / self.acc, device=st.device, dtype=F32)
+        ops.pair_loss_bwd(sp, sn, align, B, L, self.tau, self.aw, self.gamma, gscale, dsp, dsn, dal)
         dan, dtp, dtn = e(B, P), e(B, P), e(B, P)
         ops.pair_sim_bwd(an, tn_all[:B], tn_all[B:], dsp, dsn, dan, dtp, dtn)
         g_tp, g_tn, g_a = e(B, P), e(B, P), e(B, P)
         ops.l2norm_bwd(tn_all[:B], nrm[:B], dtp, g_tp)
         ops.l2norm_bwd(tn_all[B:], nrm[B:2 * B], dtn, g_tn)
         ops.l2norm_bwd(an, nrm[2 * B:], dan, g_a)
-        st.grad.zero_()
-        ids_all = ctx["t_ids"].reshape(-1)
+        if self._micro == 0:
+            st.grad.zero_()
+            self._ids = []
+        self._ids.append(ctx["t_ids"].reshape(-1))
+        self._micro += 1
+        final = self._micro == self.acc
+        ids_all = self._ids[0] if len(self._ids) == 1 else torch.cat(self._ids)
         eng.backward(ctx, g_tp, g_tn, g_a, dal,
-                     stage_done=lambda stg: self.gradsync.stage_done(stg, ids_all))
+                     stage_done=(lambda stg: self.gradsync.stage_done(stg, ids_all)) if final else None)
+        self.last = {"loss": loss, "s_pos": sp, "s_neg": sn}
+        if final:
+            self._optimizer_step()
+        return loss
+
+    def _optimizer_step(self):
         self.gradsync.finish()
         self.opt.step(self.sched.factor())  # reference order: optimizer.step() then scheduler.step()
         self.sched.step()
-        self.last = {"loss": loss, "s_pos": sp, "s_neg": sn}
-        return loss
+        self._micro = 0
+        self._ids = []
+
+    def flush(self):
+        """Step on a partial accumulation window (ref :1064-1066 `is_last_batch`): sync the
+        accumulated gradients (not overlapped: the backward already ran), clip, AdamW, schedule.
+        Returns whether a step was taken."""
+        if self._micro == 0:
+            return False
+        ids_all = torch.cat(self._ids)
+        for stg in ("heads", "audio", "text"):
+            self.gradsync.stage_done(stg, ids_all)
+        self._optimizer_step()
+        return True
 
     def optimizer_state_dict(self):
         """The optimizer state as the reference's training loop would save it after this many

@@ -246,3 +246,50 @@ def test_fp8_gemm_matches_oracle():
     worst.sort(reverse=True)
     print("worst fp8 grad-norm errors:", worst[:5])
     assert worst[0][0] < 0.1, worst[0]
+
+
+def test_gradient_accumulation_matches_full_batch():
+    """TrainStep(accumulation_steps=N) (ref train_epoch :1064-1117): N micro-batches of b with
+    loss/N summed into the gradient buffer equal one batch of N*b (the loss is a per-sample
+    mean), the optimizer steps once per window, and flush() steps on a partial window with the
+    reference's 1/N scaling (ref :1064-1066 is_last_batch).  Dropout off so both runs see the
+    same function; no clipping (clip_grad_norm_ would rescale).  Power-of-two N scale every bf16
+    cotangent exactly, so those runs agree to fp32 summation order; N = 3 rounds the scaled
+    cotangents differently, and the loss gradient's ds·(t_neg − t_pos) cancellation amplifies
+    that bf16 rounding, so it is checked at the gradient-norm level."""
+    from speech_transcript_embeddings_amd.train import TrainStep, synthetic_batch
+    meta, _ = load("noalign")
+
+    def build():
+        m = mini_model(meta, spec_augment=False)
+        m.dropout = 0.0
+        m.audio_cfg.conformer_conv_dropout = 0.0
+        m.audio_cfg.layerdrop = 0.0
+        m.text_cfg.hidden_dropout_prob = 0.0
+        m.text_cfg.attention_probs_dropout_prob = 0.0
+        return m
+
+    data = synthetic_batch(4, 16000, 12, vocab=meta["mini"]["text"]["vocab_size"], seed=3)
+    halves = [tuple(t[:2] for t in data), tuple(t[2:] for t in data)]
+
+    def run(acc, seq, flush=False):
+        m = build()
+        st = TrainStep(m, lr=1e-3, warmup=1, total_steps=10, accumulation_steps=acc, max_norm=1e9)
+        for k, i in enumerate(seq):
+            st(*halves[i])
+            assert st.opt.t == (k + 1) // acc
+        if flush:
+            assert st.flush() and not st.flush()
+        assert st.opt.t == 1 and st._micro == 0
+        torch.cuda.synchronize()
+        return m.store.grad.clone()
+
+    m1 = build()
+    s1 = TrainStep(m1, lr=1e-3, warmup=1, total_steps=10, max_norm=1e9)
+    s1(*data)
+    torch.cuda.synchronize()
+    g_full = m1.store.grad.clone()
+    assert rel(run(2, [0, 1]), g_full) < 1e-5  # fp32 summation order (1.0e-6 measured)
+    assert rel(run(4, [0, 1], flush=True), g_full * 0.5) < 1e-5
+    g3 = run(3, [0, 1], flush=True)
+    assert abs(g3.norm().item() / (g_full.norm().item() * 2.0 / 3.0) - 1.0) < 2e-2
