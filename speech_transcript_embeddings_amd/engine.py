@@ -323,17 +323,22 @@ class Engine:
         self._ln_bwd(da1, sv["x"], sv["st1"], pre + "ffn1_layer_norm", dres=dx1, dx=dx0)
         return dx0
 
-    def audio_backward(self, dh, ctx):
+    def audio_backward(self, dh, ctx, layers_done=None):
+        """layers_done() is called once every trainable Conformer layer's gradients are final
+        (after the lowest trainable layer), so their all-reduce overlaps the frozen layers."""
         c = self.acfg
         b, T = ctx["a_b"], ctx["a_T"]
         maskf, mask32 = ctx["a_maskf"], ctx["a_mask32"]
+        lo = next((i for i in range(c.num_hidden_layers)
+                   if self.s.trainable_layer(f"audio_encoder.encoder.layers.{i}.ffn1_layer_norm.weight")), None)
         dx = dh
         for i in reversed(range(c.num_hidden_layers)):
             sv = ctx["a_layers"][i]
-            if sv is None:
-                continue
-            dx = self._conformer_bwd(i, sv, dx, b, T, maskf, mask32)
-            ctx["a_layers"][i] = None
+            if sv is not None:
+                dx = self._conformer_bwd(i, sv, dx, b, T, maskf, mask32)
+                ctx["a_layers"][i] = None
+            if layers_done is not None and i == lo:
+                layers_done()
         s = self.s
         if ctx.get("a_spec") is not None:  # SpecAugment rows: gradient to masked_spec_embed, not the projection
             ops.spec_mask_bwd(dx, ctx["a_spec"], maskf, s.g("audio_encoder.masked_spec_embed"))
@@ -740,7 +745,8 @@ class Engine:
 
     def backward(self, ctx, d_tp, d_tn, d_af, d_align, stage_done=None):
         """Backward of the whole step.  stage_done(name) is called once the gradients of a
-        parameter block are final ("heads", then "audio", then "text"), so a data-parallel
+        parameter block are final (GradSync.STAGES order: "heads", "audio_layers", "audio",
+        "text"), so a data-parallel
         caller can start their collective while the rest of the backward runs."""
         nb = ctx["t_nb"]
         d_tf = self._e(nb, self.m.projection_dim)
@@ -758,14 +764,14 @@ class Engine:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 self.text_backward(dth, ctx)
-            self.audio_backward(dah, ctx)
+            self.audio_backward(dah, ctx, (lambda: stage_done("audio_layers")) if stage_done else None)
             main.wait_stream(side)
             del dah
             if stage_done:
                 stage_done("audio")
                 stage_done("text")
         else:
-            self.audio_backward(dah, ctx)
+            self.audio_backward(dah, ctx, (lambda: stage_done("audio_layers")) if stage_done else None)
             del dah
             if stage_done:
                 stage_done("audio")

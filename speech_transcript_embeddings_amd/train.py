@@ -191,6 +191,11 @@ class GradSync:
     """
 
     WORDS = "text_encoder.embeddings.word_embeddings.weight"
+    # in the order the backward finalises them: the heads; the trainable Conformer layers (the
+    # top k, final once the backward has passed the lowest of them, while the frozen layers'
+    # input gradients still run); the rest of the audio encoder (feature projection, SpecAugment
+    # embedding: final at the very end); the text encoder (side stream, joined at the end)
+    STAGES = ("heads", "audio_layers", "audio", "text")
 
     def __init__(self, store, bucket_mb: int = 256, pad_id: int = 1):
         self.store = store
@@ -209,7 +214,10 @@ class GradSync:
         words = store.slots.get(self.WORDS)
         self.words = words if words is not None and words.segment == "enc" else None
         self.ranges = {"heads": span(lambda x: x.segment == "head"),
-                       "audio": span(lambda x: x.segment == "enc" and x.name.startswith("audio_encoder.")),
+                       "audio_layers": span(lambda x: x.segment == "enc" and
+                                            x.name.startswith("audio_encoder.encoder.layers.")),
+                       "audio": span(lambda x: x.segment == "enc" and x.name.startswith("audio_encoder.") and
+                                     not x.name.startswith("audio_encoder.encoder.layers.")),
                        "text": span(lambda x: x.segment == "enc" and x.name.startswith("text_encoder."))}
         if self.words is not None and self.ranges["text"]:
             (a, b), w0, w1 = self.ranges["text"][0], self.words.offset, self.words.offset + self.words.numel
@@ -371,7 +379,7 @@ class TrainStep:
         if self._micro == 0:
             return False
         ids_all = torch.cat(self._ids)
-        for stg in ("heads", "audio", "text"):
+        for stg in GradSync.STAGES:
             self.gradsync.stage_done(stg, ids_all)
         self._optimizer_step()
         return True

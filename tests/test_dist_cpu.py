@@ -85,7 +85,7 @@ def _sync_case(rank, world):
     expect = sum(local(r)[0] for r in range(world)) / world
     gs = GradSync(_Store(g, slots))
     gs.bucket = 29  # several buckets + ragged ones
-    for stage in ("heads", "audio", "text"):
+    for stage in GradSync.STAGES:
         gs.stage_done(stage, ids)
     gs.finish()
     n = gs.store.n_grad
