@@ -191,6 +191,11 @@ typedef struct {
   float* delta;       /* workspace [B*H*T] */
   float* dE;          /* fp32 [left+right+1, 64], accumulated (may be NULL) */
   float* gwork;       /* workspace [B*H*T*80] fp32, required when dE != NULL */
+  /* optional low half of O (bf16, row stride ldolo): the forward writes bf16(O - bf16(O)),
+   * the backward forms delta = rowsum(dO·(O + O_lo)) from it, i.e. from the ~fp32 output.
+   * With near-uniform attention O ≈ mean(V) and dS = P(dP - delta) is a small difference of
+   * large terms, so a delta from the bf16-rounded O alone is the dominant error of dQ/dK/dE. */
+  void* o_lo; int64_t ldolo;
 } ste_attn_args;
 int ste_attention_fwd(const ste_attn_args* a, void* stream);
 int ste_attention_bwd(const ste_attn_args* a, void* stream);
@@ -230,9 +235,13 @@ int ste_attn_pool_fwd(const void* t, const float* w2, const float* b2, const voi
                       void* stream);
 /* Backward: dpooled fp32 [B,H] -> dh fp32 [B*L,H] (+=), dt bf16 [B*L,Hh]
  * (= dscore*w2*(1-t^2): the gradient at the scorer's first Linear output, tanh'
- * included), dw2 fp32 [Hh] (+=), db2 fp32 [1] (+=). */
+ * included), optional dt_lo bf16 [B*L,Hh] = bf16(dt - bf16(dt)) (the low half, for a
+ * two-pass weight-gradient GEMM), dw2 fp32 [Hh] (+=), db2 fp32 [1] (+=), db1 fp32 [Hh] (+=,
+ * the first Linear's bias gradient Σ_l dt_l summed in fp32; may be NULL).
+ * work: fp32 [B*L] scratch.  Replaces the autograd of ref:184-211. */
 int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float* weights, const float* dpooled,
-                      int B, int L, int Hh, int H, float* dh, void* dt, float* dw2, float* db2, void* stream);
+                      int B, int L, int Hh, int H, float* dh, void* dt, void* dt_lo, float* dw2, float* db2,
+                      float* db1, float* work, void* stream);
 
 /* Pooling without the scorer, use_attentive_pooling=False
  * (ref:training/trainer_unfreeze.py:578-580 text `last_hidden_state[:, 0, :]`, :621-636 audio

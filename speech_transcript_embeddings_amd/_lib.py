@@ -102,6 +102,7 @@ class AttnArgs(C.Structure):
         ("delta", c_void_p),
         ("dE", c_void_p),
         ("gwork", c_void_p),
+        ("o_lo", c_void_p), ("ldolo", c_int64),
     ]
 
 
@@ -127,7 +128,7 @@ _SIGS = {
     "ste_attn_pool_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     "ste_attn_pool_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ste_mean_pool_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),
     "ste_weighted_pool_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),

@@ -72,6 +72,17 @@ STE_DEV bf16x8 pack_acc(f32x4 a, f32x4 b) {
   return v;
 }
 
+// low halves of the same accumulator pair: (bf16)(x - hi) for the hi/lo split of P
+STE_DEV bf16x8 pack_acc_lo(f32x4 a, f32x4 b, bf16x8 hi) {
+  bf16x8 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = (bf16)(a[i] - (float)hi[i]);
+    v[i + 4] = (bf16)(b[i] - (float)hi[i + 4]);
+  }
+  return v;
+}
+
 STE_DEV void stage_E(char* sE, const bf16* E, int nrel, int rows, int tid) {
   for (int c = tid; c < rows * 8; c += NT) {
     int row = c >> 3, ch = c & 7;
@@ -149,6 +160,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(ste_attn_args a) {
   const uint32_t thresh = (uint32_t)(a.drop_p * 4294967296.0);
   const float inv_keep = DROP ? 1.0f / (1.0f - a.drop_p) : 1.0f;
   const uint64_t drow = ((uint64_t)(b * H + h) * T + myq) * (uint64_t)T;
+  const bool split = a.o_lo != nullptr;
 
   float m = -INFINITY, l = 0.f;
   f32x4 o[4];
@@ -233,6 +245,11 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(ste_attn_args a) {
       const bf16x8 pb = pack_acc(s[2 * u], s[2 * u + 1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(frag_tr(tV, dt * 16, u, lane), pb, o[dt]);
+      if (split) {  // P = hi + lo: O to ~fp32 precision (see ste_attn_args.o_lo)
+        const bf16x8 pl = pack_acc_lo(s[2 * u], s[2 * u + 1], pb);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(frag_tr(tV, dt * 16, u, lane), pl, o[dt]);
+      }
     }
     if (more) {
       tile_st(sK + (cur ^ 1) * TILE, rk, tid);
@@ -244,8 +261,14 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(ste_attn_args a) {
   if (myq < T) {
     const float inv_l = 1.0f / l;
     bf16* O = (bf16*)a.o + (int64_t)(bT + myq) * a.ldo + h * HD;
+    if (a.o_lo) {
+      bf16* Ol = (bf16*)a.o_lo + (int64_t)(bT + myq) * a.ldolo + h * HD;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) store_bf16x4(O + 16 * dt + 4 * g, o[dt] * inv_l);
+      for (int dt = 0; dt < 4; ++dt) store_bf16x4_split(O + 16 * dt + 4 * g, Ol + 16 * dt + 4 * g, o[dt] * inv_l);
+    } else {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) store_bf16x4(O + 16 * dt + 4 * g, o[dt] * inv_l);
+    }
     if (g == 0) a.lse[(int64_t)(b * H + h) * T + myq] = m + logf(l);
   }
 }
@@ -260,13 +283,15 @@ __global__ void attn_delta_kernel(ste_attn_args a) {
   const int b = row / a.T, q = row % a.T;
   const bf16* dO = (const bf16*)a.dout + row * a.lddo + h * HD;
   const bf16* O = (const bf16*)a.o + row * a.ldo + h * HD;
+  const bf16* Ol = a.o_lo ? (const bf16*)a.o_lo + row * a.ldolo + h * HD : nullptr;
   float acc = 0.f;
 #pragma unroll
   for (int c = 0; c < HD; c += 8) {
     bf16x8 x = *reinterpret_cast<const bf16x8*>(dO + c);
     bf16x8 y = *reinterpret_cast<const bf16x8*>(O + c);
+    bf16x8 z = Ol ? *reinterpret_cast<const bf16x8*>(Ol + c) : bf16x8{};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc += (float)x[e] * (float)y[e];
+    for (int e = 0; e < 8; ++e) acc += (float)x[e] * ((float)y[e] + (float)z[e]);
   }
   a.delta[(int64_t)(b * a.H + h) * a.T + q] = acc;
 }
@@ -652,6 +677,12 @@ STE_DEV bf16x8 frag_tr_asm(const char* t, int cb, int u, int lane) {
   return join_tr(ds_read_tr16_asm(t + tr_off(r0, quad)), ds_read_tr16_asm(t + tr_off(r0 + 16, quad)));
 }
 
+// SPLIT (o_lo requested, i.e. a training forward whose backward needs delta): the PV product
+// runs on P = bf16(P) + bf16(P - bf16(P)), so O carries ~16 mantissa bits of P.  The backward
+// recomputes P in fp32 and needs delta = Σ_k P_k dP_k = dO·O with THAT P: with near-uniform
+// attention the bf16 rounding of P alone moves O by ~1e-4·|mean V|, which the cancellation in
+// dS = P(dP - delta) amplifies into percent-level errors of dQ, dK and dE.
+template <bool SPLIT>
 __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
   using namespace rel2;
   extern __shared__ __attribute__((aligned(16))) char sm[];
@@ -826,6 +857,11 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
         const bf16x8 pb = pack_acc(s[gq][2 * u], s[gq][2 * u + 1]);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pb, o[gq][dt]);
+        if (SPLIT) {
+          const bf16x8 pl = pack_acc_lo(s[gq][2 * u], s[gq][2 * u + 1], pb);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pl, o[gq][dt]);
+        }
       }
     if (kt + 1 < nkt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (this wave's pieces)
@@ -839,8 +875,15 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
     if (myq < T) {
       const float inv_l = 1.0f / l[gq];
       bf16* O = (bf16*)a.o + (int64_t)(bT + myq) * a.ldo + h * HD;
+      if (SPLIT) {
+        bf16* Ol = (bf16*)a.o_lo + (int64_t)(bT + myq) * a.ldolo + h * HD;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) store_bf16x4(O + 16 * dt + 4 * g, o[gq][dt] * inv_l);
+        for (int dt = 0; dt < 4; ++dt)
+          store_bf16x4_split(O + 16 * dt + 4 * g, Ol + 16 * dt + 4 * g, o[gq][dt] * inv_l);
+      } else {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) store_bf16x4(O + 16 * dt + 4 * g, o[gq][dt] * inv_l);
+      }
       // natural-log LSE.  A row whose every key is masked (scores all finfo.min, as in the
       // reference: a uniform distribution over the T keys) is stored as -inf: fp32 cannot
       // hold finfo.min + log(T), and the v2 backward kernels read -inf as "p = 1/T".
@@ -880,6 +923,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel2_kernel(ste_attn_args a
   const bf16* Vb = (const bf16*)a.v + h * HD;
   const bf16* dOb = (const bf16*)a.dout + h * HD;
   const bf16* Ob = (const bf16*)a.o + h * HD;
+  const bf16* Olb = a.o_lo ? (const bf16*)a.o_lo + h * HD : nullptr;
   const int q0 = tile * DQ_Q + w * 16, myq = q0 + li;
   const bool qvalid = myq < T;
   const int64_t rowid = (int64_t)(b * H + h) * T + myq;
@@ -893,8 +937,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel2_kernel(ste_attn_args a
     qf[s] = qvalid ? *reinterpret_cast<const bf16x8*>(Qb + off * a.ldq + 32 * s + 8 * g) : bf16x8{};
     df[s] = qvalid ? *reinterpret_cast<const bf16x8*>(dOb + off * a.lddo + 32 * s + 8 * g) : bf16x8{};
     const bf16x8 of = qvalid ? *reinterpret_cast<const bf16x8*>(Ob + off * a.ldo + 32 * s + 8 * g) : bf16x8{};
+    const bf16x8 ol = (qvalid && Olb) ? *reinterpret_cast<const bf16x8*>(Olb + off * a.ldolo + 32 * s + 8 * g)
+                                      : bf16x8{};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) dpart += (float)df[s][e] * (float)of[e];
+    for (int e = 0; e < 8; ++e) dpart += (float)df[s][e] * ((float)of[e] + (float)ol[e]);
   }
   dpart += __shfl_xor(dpart, 16, 64);
   dpart += __shfl_xor(dpart, 32, 64);
@@ -1352,6 +1398,7 @@ bool rel_v2() {
 int check(const ste_attn_args* a) {
   if (!a || a->B <= 0 || a->T <= 0 || a->H <= 0) return STE_ERR_ARG;
   if ((a->ldq & 7) || (a->ldk & 7) || (a->ldv & 7) || (a->ldo & 7)) return STE_ERR_SHAPE;
+  if (a->o_lo && (a->ldolo & 7)) return STE_ERR_SHAPE;
   if (a->rel_E && a->rel_left + a->rel_right + 1 > NREL) return STE_ERR_SHAPE;
   if (a->drop_p < 0.f || a->drop_p >= 1.f) return STE_ERR_ARG;
   return 0;
@@ -1367,7 +1414,8 @@ extern "C" int ste_attention_fwd(const ste_attn_args* a, void* stream) {
   const bool rel = a->rel_E != nullptr, drop = a->drop_p > 0.f;
   if (rel && !drop && rel_v2()) {
     dim3 g2((unsigned)(((a->T + rel2::BQ - 1) / rel2::BQ) * a->H * a->B));
-    hipLaunchKernelGGL(attn_fwd_rel2_kernel, g2, dim3(NT), rel2::FWD_LDS, s, *a);
+    if (a->o_lo) hipLaunchKernelGGL(attn_fwd_rel2_kernel<true>, g2, dim3(NT), rel2::FWD_LDS, s, *a);
+    else hipLaunchKernelGGL(attn_fwd_rel2_kernel<false>, g2, dim3(NT), rel2::FWD_LDS, s, *a);
     STE_CHECK_LAUNCH();
     return 0;
   }

@@ -33,6 +33,18 @@ STE_DEV void store_bf16x4(bf16* p, f32x4 v) {
   o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
   *reinterpret_cast<bf16x4*>(p) = o;
 }
+// hi/lo split of fp32 values: hi = bf16(v), lo = bf16(v - hi); hi + lo carries ~16 mantissa
+// bits (used where a backward needs the fp32 value of a bf16-stored forward output)
+STE_DEV void store_bf16x4_split(bf16* hi_p, bf16* lo_p, f32x4 v) {
+  bf16x4 h, l;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    h[i] = (bf16)v[i];
+    l[i] = (bf16)(v[i] - (float)h[i]);
+  }
+  *reinterpret_cast<bf16x4*>(hi_p) = h;
+  *reinterpret_cast<bf16x4*>(lo_p) = l;
+}
 
 // ---------------------------------------------------------------- wave reductions
 STE_DEV float wave_sum(float v) {

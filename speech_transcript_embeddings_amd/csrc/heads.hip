@@ -73,54 +73,76 @@ __global__ __launch_bounds__(NT) void pool_fwd_kernel(const bf16* t, const float
   }
 }
 
-// dz (pre-tanh gradient of the scorer's first Linear) = dscore * w2 * (1 - t^2)
-__global__ __launch_bounds__(NT) void pool_bwd_kernel(const bf16* t, const float* w2, const bf16* h,
-                                                    const float* weights, const float* dpooled, int L, int Hh, int H,
-                                                    float* dh, bf16* dz, float* dw2, float* db2) {
-  extern __shared__ float sdw[];  // L
-  __shared__ float red[8];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+// Backward, three launches spread over (batch, row chunks) so the [B*L, H] reads fill the chip:
+//   pool_dp_kernel     dP[l] = h_l·dpooled                               grid (B, ceil(L/16))
+//   pool_dscore_kernel ds[l] = w_l (dP[l] - Σ_j w_j dP[j]), db2 += Σ ds   grid B
+//   pool_dz_kernel     dh_l += w_l dpooled;  dz_l = ds_l w2 (1 - t_l²) (bf16 hi [+ lo]);
+//                      dw2 += Σ_l ds_l t_l;  db1 += Σ_l dz_l in fp32     grid (B, ceil(L/32))
+// Σ_l ds_l = 0 (softmax), so the scorer's bias gradient Σ_l dz_l is a small difference of large
+// terms: it is summed from the fp32 dz here, never from the bf16-rounded copy, and the optional
+// low half dz_lo = bf16(dz - bf16(dz)) lets the weight-gradient GEMM see dz to ~16 bits.
+constexpr int POOL_DP_ROWS = 16;
+constexpr int POOL_DZ_ROWS = 32;
+
+__global__ __launch_bounds__(NT) void pool_dp_kernel(const bf16* h, const float* dpooled, int L, int H, float* dp_out) {
+  const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float* dp = dpooled + (int64_t)b * H;
-  for (int l = w; l < L; l += NT / 64) {
-    float s = dot_bf16_f32(h + (int64_t)(b * L + l) * H, dp, H, lane);
-    if (lane == 0) sdw[l] = s;
+  const int l1 = min(L, (int)(blockIdx.y + 1) * POOL_DP_ROWS);
+  for (int l = blockIdx.y * POOL_DP_ROWS + w; l < l1; l += NT / 64) {
+    const float s = dot_bf16_f32(h + (int64_t)(b * L + l) * H, dp, H, lane);
+    if (lane == 0) dp_out[b * L + l] = s;
   }
-  __syncthreads();
+}
+
+__global__ __launch_bounds__(NT) void pool_dscore_kernel(const float* weights, int L, float* dsc, float* db2) {
+  __shared__ float red[8];
+  const int b = blockIdx.x, tid = threadIdx.x;
   float acc = 0.f;
-  for (int l = tid; l < L; l += NT) acc += weights[b * L + l] * sdw[l];
+  for (int l = tid; l < L; l += NT) acc += weights[b * L + l] * dsc[b * L + l];
   const float tot = block_sum(acc, red);
   float dbs = 0.f;
   for (int l = tid; l < L; l += NT) {
-    const float ds = weights[b * L + l] * (sdw[l] - tot);
-    sdw[l] = ds;
+    const float ds = weights[b * L + l] * (dsc[b * L + l] - tot);
+    dsc[b * L + l] = ds;
     dbs += ds;
   }
-  dbs = block_sum(dbs, red);  // contains a barrier: sdw now holds dscore
+  dbs = block_sum(dbs, red);
   if (tid == 0 && db2) atomicAdd(db2, dbs);
+}
+
+__global__ __launch_bounds__(NT) void pool_dz_kernel(const bf16* t, const float* w2, const float* weights,
+                                                   const float* dpooled, const float* dsc, int L, int Hh, int H,
+                                                   float* dh, bf16* dz, bf16* dz_lo, float* dw2, float* db1) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int l0 = blockIdx.y * POOL_DZ_ROWS, l1 = min(L, l0 + POOL_DZ_ROWS);
   // dh[l][c] += w[l] * dpooled[c]
+  const float* dp = dpooled + (int64_t)b * H;
   for (int c = tid * 4; c < H; c += NT * 4) {
     const f32x4 d = *reinterpret_cast<const f32x4*>(dp + c);
-    for (int l = 0; l < L; ++l) {
+    for (int l = l0; l < l1; ++l) {
       f32x4* o = reinterpret_cast<f32x4*>(dh + (int64_t)(b * L + l) * H + c);
       *o = *o + d * weights[b * L + l];
     }
   }
-  // dz and dw2 partials
   for (int k = tid * 4; k < Hh; k += NT * 4) {
     const f32x4 wv = *reinterpret_cast<const f32x4*>(w2 + k);
-    f32x4 g2 = {0.f, 0.f, 0.f, 0.f};
-    for (int l = 0; l < L; ++l) {
-      const f32x4 tv = load_bf16x4(t + (int64_t)(b * L + l) * Hh + k);
-      const float ds = sdw[l];
+    f32x4 g2 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
+    for (int l = l0; l < l1; ++l) {
+      const int64_t off = (int64_t)(b * L + l) * Hh + k;
+      const f32x4 tv = load_bf16x4(t + off);
+      const float ds = dsc[b * L + l];
       g2 += tv * ds;
       f32x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = ds * wv[e] * (1.f - tv[e] * tv[e]);
-      store_bf16x4(dz + (int64_t)(b * L + l) * Hh + k, o);
+      g1 += o;
+      if (dz_lo) store_bf16x4_split(dz + off, dz_lo + off, o);
+      else store_bf16x4(dz + off, o);
     }
-    if (dw2) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(dw2 + k + e, g2[e]);
+    for (int e = 0; e < 4; ++e) {
+      if (dw2) atomicAdd(dw2 + k + e, g2[e]);
+      if (db1) atomicAdd(db1 + k + e, g1[e]);
     }
   }
 }
@@ -423,11 +445,17 @@ extern "C" int ste_attn_pool_fwd(const void* t, const float* w2, const float* b2
 }
 
 extern "C" int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float* weights,
-                                 const float* dpooled, int B, int L, int Hh, int H, float* dh, void* dt, float* dw2,
-                                 float* db2, void* stream) {
-  if (B <= 0 || L <= 0 || (Hh & 3) || (H & 3) || L > 8192) return STE_ERR_SHAPE;
-  hipLaunchKernelGGL(pool_bwd_kernel, dim3(B), dim3(NT), L * sizeof(float), (hipStream_t)stream, (const bf16*)t, w2,
-                     (const bf16*)h, weights, dpooled, L, Hh, H, dh, (bf16*)dt, dw2, db2);
+                                 const float* dpooled, int B, int L, int Hh, int H, float* dh, void* dt, void* dt_lo,
+                                 float* dw2, float* db2, float* db1, float* work, void* stream) {
+  if (B <= 0 || L <= 0 || (Hh & 3) || (H & 3) || !work || !dt) return STE_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(pool_dp_kernel, dim3(B, (L + POOL_DP_ROWS - 1) / POOL_DP_ROWS), dim3(NT), 0, s, (const bf16*)h,
+                     dpooled, L, H, work);
+  STE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(pool_dscore_kernel, dim3(B), dim3(NT), 0, s, weights, L, work, db2);
+  STE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(pool_dz_kernel, dim3(B, (L + POOL_DZ_ROWS - 1) / POOL_DZ_ROWS), dim3(NT), 0, s, (const bf16*)t,
+                     w2, weights, dpooled, work, L, Hh, H, dh, (bf16*)dt, (bf16*)dt_lo, dw2, db1);
   STE_CHECK_LAUNCH();
   return 0;
 }

@@ -206,11 +206,12 @@ class Engine:
         qkv = lin(a2in, pre + "self_attn.linear_q.weight", s.fused(pre + "self_attn.linear_q.bias", 3, "p"), count=3,
                   out_bf16=True)
         o = self._e(M, D, dtype=BF16)
+        o_lo = self._e(M, D, dtype=BF16) if save else None   # low half of O for the backward's delta
         lse = self._e(b * H * T)
         ops.attention_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B=b, T=T, H=H, o=o, lse=lse, key_mask=mask32,
                           rel_E=s.w(pre + "self_attn.distance_embedding.weight"),
                           rel_left=c.left_max_position_embeddings, rel_right=c.right_max_position_embeddings,
-                          scale=1.0 / math.sqrt(D // H))
+                          scale=1.0 / math.sqrt(D // H), o_lo=o_lo)
         x2 = lin(o, pre + "self_attn.linear_out.weight", s.p(pre + "self_attn.linear_out.bias"), residual=x1)
         # -- convolution module
         a3, a3in = ln_in(x2, pre + "conv_module.layer_norm", "st3", row_scale=maskf)
@@ -230,7 +231,7 @@ class Engine:
         x5 = self._e(M, D)
         x5b = self._e(M, D, dtype=BF16) if want_bf16 else None
         sv["st6"] = self._ln(x4, pre + "final_layer_norm", eps, y=x5, yb=x5b)
-        sv.update(x=x, z1=z1, x1=x1, qkv=qkv, o=o, lse=lse, x2=x2, pw1=pw1, cv=cv, x3=x3, z2=z2, x4=x4, p_conv=p_conv)
+        sv.update(x=x, z1=z1, x1=x1, qkv=qkv, o=o, o_lo=o_lo, lse=lse, x2=x2, pw1=pw1, cv=cv, x3=x3, z2=z2, x4=x4, p_conv=p_conv)
         if tr:
             sv.update(a1=a1, h1=h1, a2=a2, a3=a3, sw=sw, a5=a5, h2=h2)
         return x5, x5b, sv
@@ -298,7 +299,7 @@ class Engine:
                           dqkv[:, D:2 * D], dqkv[:, 2 * D:], B=b, T=T, H=H, delta=delta, key_mask=mask32,
                           rel_E=s.w(pre + "self_attn.distance_embedding.weight"),
                           rel_left=c.left_max_position_embeddings, rel_right=c.right_max_position_embeddings,
-                          scale=1.0 / math.sqrt(D // H), dE=gE, gwork=gwork)
+                          scale=1.0 / math.sqrt(D // H), dE=gE, gwork=gwork, o_lo=sv["o_lo"])
         del do, delta, gwork
         da2 = self._dx(dqkv, pre + "self_attn.linear_q.weight", 3, out_bf16=True)
         if tr:
@@ -396,9 +397,11 @@ class Engine:
         qkv = ops.linear(xb, s.fused(pre + "attention.self.query.weight", 3, "w"),
                          s.fused(pre + "attention.self.query.bias", 3, "p"), out_bf16=True)
         o = self._e(M, D, dtype=BF16)
+        o_lo = self._e(M, D, dtype=BF16) if save else None
         lse = self._e(nb * H * L)
         ops.attention_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B=nb, T=L, H=H, o=o, lse=lse,
-                          key_mask=mask32, scale=1.0 / math.sqrt(D // H), drop_p=ap, seed=_site_seed(seed, 1))
+                          key_mask=mask32, scale=1.0 / math.sqrt(D // H), drop_p=ap, seed=_site_seed(seed, 1),
+                          o_lo=o_lo)
         y1 = ops.linear(o, s.w(pre + "attention.output.dense.weight"), s.p(pre + "attention.output.dense.bias"),
                         residual=x, drop_p=hp, seed=_site_seed(seed, 2))
         x1 = self._e(M, D)
@@ -412,7 +415,7 @@ class Engine:
         x2 = self._e(M, D)
         x2b = self._e(M, D, dtype=BF16)
         sv["st2"] = self._ln(y2, pre + "output.LayerNorm", eps, y=x2, yb=x2b)
-        sv.update(qkv=qkv, o=o, lse=lse, y1=y1, zt=zt, y2=y2)
+        sv.update(qkv=qkv, o=o, o_lo=o_lo, lse=lse, y1=y1, zt=zt, y2=y2)
         if tr:
             sv.update(xb=xb, x1b=x1b, h=h)
         return x2, x2b, sv
@@ -452,7 +455,7 @@ class Engine:
         delta = self._e(nb * H * L)
         ops.attention_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], sv["o"], sv["lse"], do, dqkv[:, :D],
                           dqkv[:, D:2 * D], dqkv[:, 2 * D:], B=nb, T=L, H=H, delta=delta, key_mask=mask32,
-                          scale=1.0 / math.sqrt(D // H), drop_p=ap, seed=_site_seed(seed, 1))
+                          scale=1.0 / math.sqrt(D // H), drop_p=ap, seed=_site_seed(seed, 1), o_lo=sv["o_lo"])
         del do, delta
         dx0 = self._dx(dqkv, pre + "attention.self.query.weight", 3, residual=dy1)
         if tr:
@@ -536,12 +539,19 @@ class Engine:
             return
         t = sv["t"]
         dz = self._e(*t.shape, dtype=BF16)
+        gw1 = s.g(name + ".attention.0.weight")
+        dz_lo = self._e(*t.shape, dtype=BF16) if gw1 is not None else None
         gw2 = s.g(name + ".attention.2.weight")
+        # Σ_l dscore_l = 0 makes the scorer's first-Linear gradients small differences of large
+        # terms: the bias gradient is summed in fp32 by the kernel, the weight gradient runs on
+        # dz = hi + lo (two GEMM passes)
         ops.attn_pool_bwd(t, s.p(name + ".attention.2.weight").view(-1), sv["hb"], sv["w"], dpooled, nb, L, dh, dz,
-                          None if gw2 is None else gw2.view(-1), s.g(name + ".attention.2.bias"))
+                          None if gw2 is None else gw2.view(-1), s.g(name + ".attention.2.bias"),
+                          db1=s.g(name + ".attention.0.bias"), dz_lo=dz_lo)
         ops.linear_dx(dz, s.w(name + ".attention.0.weight"), out=dh, beta=1.0)
         self._dw(dz, sv["hb"], name + ".attention.0.weight")
-        self._db(dz, name + ".attention.0.bias")
+        if dz_lo is not None:
+            self._dw(dz_lo, sv["hb"], name + ".attention.0.weight")
 
     def heads_forward(self, th, thb, ah, ahb, train, base_seed, ctx):
         s = self.s

@@ -198,8 +198,9 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, *, beta=None, dx=None, dxb=None, dre
 
 # -------------------------------------------------------------- attention
 def attention_fwd(q, k, v, *, B, T, H, o, lse, key_mask=None, rel_E=None, rel_left=64, rel_right=8,
-                  scale=0.125, drop_p=0.0, seed=0):
-    """q/k/v/o: bf16 [B*T, *] views (row-major, head h at columns h*64..), lse fp32 [B*H*T]."""
+                  scale=0.125, drop_p=0.0, seed=0, o_lo=None):
+    """q/k/v/o: bf16 [B*T, *] views (row-major, head h at columns h*64..), lse fp32 [B*H*T].
+    o_lo (optional, bf16 like o): receives bf16(O - bf16(O)) for the backward's delta."""
     a = AttnArgs()
     a.B, a.T, a.H = B, T, H
     a.q, a.ldq = ptr(q), _ld(q)
@@ -210,12 +211,14 @@ def attention_fwd(q, k, v, *, B, T, H, o, lse, key_mask=None, rel_E=None, rel_le
     a.key_mask = ptr(key_mask)
     a.rel_E, a.rel_left, a.rel_right = ptr(rel_E), rel_left, rel_right
     a.scale, a.drop_p, a.seed = float(scale), float(drop_p), int(seed) & (2**64 - 1)
+    if o_lo is not None:
+        a.o_lo, a.ldolo = ptr(o_lo), _ld(o_lo)
     call("ste_attention_fwd", C.byref(a), _s())
     return a
 
 
 def attention_bwd(q, k, v, o, lse, dout, dq, dk, dv, *, B, T, H, delta, key_mask=None, rel_E=None, rel_left=64,
-                  rel_right=8, scale=0.125, drop_p=0.0, seed=0, dE=None, gwork=None):
+                  rel_right=8, scale=0.125, drop_p=0.0, seed=0, dE=None, gwork=None, o_lo=None):
     a = AttnArgs()
     a.B, a.T, a.H = B, T, H
     a.q, a.ldq = ptr(q), _ld(q)
@@ -231,6 +234,8 @@ def attention_bwd(q, k, v, o, lse, dout, dq, dk, dv, *, B, T, H, delta, key_mask
     a.dk, a.lddk = ptr(dk), _ld(dk)
     a.dv, a.lddv = ptr(dv), _ld(dv)
     a.delta, a.dE, a.gwork = ptr(delta), ptr(dE), ptr(gwork)
+    if o_lo is not None:
+        a.o_lo, a.ldolo = ptr(o_lo), _ld(o_lo)
     call("ste_attention_bwd", C.byref(a), _s())
 
 
@@ -269,9 +274,12 @@ def attn_pool_fwd(t, w2, b2, h, mask, B, L, weights, pooled, pooled_bf16=None):
          ptr(weights), ptr(pooled), ptr(pooled_bf16), _s())
 
 
-def attn_pool_bwd(t, w2, h, weights, dpooled, B, L, dh, dz, dw2=None, db2=None):
+def attn_pool_bwd(t, w2, h, weights, dpooled, B, L, dh, dz, dw2=None, db2=None, db1=None, dz_lo=None):
+    """AttentivePooling backward: dh += ..., dz (bf16, + optional low half dz_lo), dw2/db2 and the
+    first Linear's bias gradient db1 (fp32 column sums of dz) accumulated."""
+    work = torch.empty(B * L, device=t.device, dtype=F32)
     call("ste_attn_pool_bwd", ptr(t), ptr(w2), ptr(h), ptr(weights), ptr(dpooled), B, L, t.shape[-1], h.shape[-1],
-         ptr(dh), ptr(dz), ptr(dw2), ptr(db2), _s())
+         ptr(dh), ptr(dz), ptr(dz_lo), ptr(dw2), ptr(db2), ptr(db1), ptr(work), _s())
 
 
 def mean_pool_fwd(h, mask, B, L, cls, weights, pooled, pooled_bf16=None):

@@ -5,16 +5,20 @@ copied to the oracle), eval mode, batch 2.
 
 Checked: the three normalised embeddings and alignment scores (bf16 bound of north_star:
 1e-2 relative), and the gradient of every parameter that receives one, for random cotangents
-on the outputs (the loss-derived cotangent is a near-cancelling difference, see
-test_model_gpu.py::test_backward_random_cotangents).  Gradients are compared tensor-wise by
-relative L2 norm of the difference: the median tensor within 2.5e-2, the worst within 5e-2
-(measured: median 0.66 % for both c2 and c4 shapes, worst 3.3 %; with the alignment head the
-oracle re-runs with the HIP path's ReLU gate, 79 of 49,152 gates flip).  The gradients
-cross all 24 Conformer layers (feature_projection is trainable) on bf16 MFMA operands, so
-per-tensor errors grow with depth beyond the north_star's 1e-2 bf16 bound for outputs.  The worst tensors are the q/k projections of the deepest trainable
-Conformer layer: their gradients pass through the attention backward's dS = P(dP - delta)
-with bf16 MFMA operands (P, dS, K, Q) and delta from the bf16-stored output O, a
-cancellation that random-init (near-uniform) attention makes worst-case (measured 3.3 %)."""
+on the outputs (the loss-derived cotangent is a near-cancelling pos/neg difference, see
+test_model_gpu.py::test_forward_backward_matches_golden_and_oracle).  Gradients are compared
+tensor-wise by relative L2 norm of the difference: median within 1e-2, worst within 3e-2
+(measured: median 0.66 %, worst 2.3 % for c2 and c4 shapes; with the alignment head the
+oracle re-runs with the HIP path's ReLU gate).
+
+The gradients cross all 24 Conformer layers (feature_projection is trainable) on bf16 MFMA
+operands.  Random-init encoders produce activations that are nearly identical across frames
+(a large common component), so every softmax backward dS = P(dP - delta) is a small
+difference of large terms: delta is formed from the ~fp32 attention output (ste_attn_args.o_lo,
+the forward's PV product on P = hi + lo), which took the q/k projections of the deepest
+trainable layer from 3.3 % to 1.7 %.  The worst tensors left are the audio attentive-pooling
+scorer (2.3 %): its tanh activations are stored bf16 and share the same common component.
+"""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -117,6 +121,6 @@ def test_full_size_vs_oracle(align):
     errs.sort(reverse=True)
     assert len(errs) > 50
     median = errs[len(errs) // 2][0]
-    print(f"grad rel err: worst {errs[0]}, median {median:.2e}, n={len(errs)}, gate flips {flips}")
-    assert median < 2.5e-2, median
-    assert errs[0][0] < 5e-2, errs[:5]
+    print(f"grad rel err: worst {errs[:8]}, median {median:.2e}, n={len(errs)}, gate flips {flips}")
+    assert median < 1e-2, median
+    assert errs[0][0] < 3e-2, errs[:5]
