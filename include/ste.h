@@ -191,7 +191,8 @@ typedef struct {
   float* delta;       /* workspace [B*H*T] */
   float* dE;          /* fp32 [left+right+1, 64], accumulated (may be NULL) */
   float* gwork;       /* workspace [B*H*T*80] fp32, required when dE != NULL */
-  /* optional low half of O (bf16, row stride ldolo): the forward writes bf16(O - bf16(O)),
+  /* optional low half of O (bf16, row stride ldolo): the forward (whose PV product runs on
+   * P split into bf16 hi + lo halves, so O is ~fp32-accurate) writes bf16(O - bf16(O)), and
    * the backward forms delta = rowsum(dO·(O + O_lo)) from it, i.e. from the ~fp32 output.
    * With near-uniform attention O ≈ mean(V) and dS = P(dP - delta) is a small difference of
    * large terms, so a delta from the bf16-rounded O alone is the dominant error of dQ/dK/dE. */
@@ -216,8 +217,8 @@ int ste_glu_dwconv_bwd(const void* pre, const float* w, const void* dout, void* 
  * (tf:models/seamless_m4t/feature_extraction_seamless_m4t.py:112-138,140-301,
  * tf:audio_utils.py:809-1017) fused with ref:training/trainer_unfreeze.py:880-921
  * (custom_collate_fn padding).  wav fp32 [B, ld_wav]; lengths int32 [B].
- * feats fp32 [B, Tmax, 160]; mask int64 [B, Tmax]; work fp32 >= 2048 + B*Fmax*80
- * with Fmax = 2*Tmax (constant tables + log-mel).  mask_mode 0: collate semantics (1 for t < T_b);
+ * feats fp32 [B, Tmax, 160]; mask int64 [B, Tmax]; work fp32 >= 2048 + B*Fmax*80 + B*160
+ * with Fmax = 2*Tmax (constant tables + log-mel + per-clip CMVN statistics).  mask_mode 0: collate semantics (1 for t < T_b);
  * mask_mode 1: extractor semantics (0 for a padded odd frame).
  */
 int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* lengths, int B, int Tmax, float pad_value,
@@ -300,6 +301,26 @@ int ste_pair_loss_fwd(const float* S, int64_t ldS, int off_neg, const float* ali
 int ste_pair_loss_bwd(const float* s_pos, const float* s_neg, const float* align, int B, int L, float tau,
                       float aw, float gamma, const float* gscale, float* ds_pos, float* ds_neg, float* dalign,
                       void* stream);
+
+/* ------------------------------------- data-parallel global similarity --
+ * north_star: "an RCCL all-gather of embeddings ... before the similarity matmul".  After the
+ * all-gather, S_g = A_g·[Tpos_g;Tneg_g]ᵀ (ste_similarity, [NB, 2NB]).
+ * ste_pair_metrics: per row i of S [NB rows, ldS], accumulates into acc fp64[6]:
+ *   Σ sigmoid(S[i][i]/τ), Σ sigmoid(S[i][off_neg+i]/τ) (ref to_human_readable :924-939, the
+ *   clean / corrupt similarities train_epoch reports :1120-1161), Σ [s_pos > s_neg],
+ *   Σ [argmax_{j<NB} S[i][j] == i] (in-batch top-1 retrieval), row count, and
+ *   loss_w·Σ_r losses[r] (the ranks' batch losses, e.g. x local batch; losses may be NULL).
+ * ste_inbatch_ce: optional in-batch-negative InfoNCE (weight 0 = the reference's loss, D1):
+ *   local rows i < B of S (ldS) over NB global clean transcripts, target row0+i:
+ *   loss[0] += weight/B Σ CE_i (loss-scale gscale (optional) multiplies dS only);
+ *   dS[i][j] = weight·gs/B·(softmax_j − δ_{j,row0+i})/τ.
+ * ste_rowmat_f32: out[r][p] += Σ_c X[r*sxr + c*sxc]·Y[c*P + p]  (R rows, P % 4 == 0). */
+int ste_pair_metrics(const float* S, int64_t ldS, int NB, int off_neg, float tau, const float* losses, int nloss,
+                     float loss_w, double* acc, void* stream);
+int ste_inbatch_ce(const float* S, int64_t ldS, int B, int NB, int row0, float tau, float weight, const float* gscale,
+                   float* loss, float* dS, int64_t lddS, void* stream);
+int ste_rowmat_f32(const float* X, int64_t sxr, int64_t sxc, const float* Y, int R, int C, int P, float* out,
+                   void* stream);
 /* Gradients of s_pos[i] = <a_i, tp_i>, s_neg[i] = <a_i, tn_i> (the diagonals of S). */
 int ste_pair_sim_bwd(const float* a, const float* tp, const float* tn, const float* ds_pos, const float* ds_neg,
                      int B, int P, float* da, float* dtp, float* dtn, void* stream);

@@ -152,6 +152,11 @@ _SIGS = {
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     "ste_pair_sim_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p, c_void_p]),
+    "ste_pair_metrics": (c_int, [c_void_p, c_int64, c_int, c_int, c_float, c_void_p, c_int, c_float, c_void_p,
+                                 c_void_p]),
+    "ste_inbatch_ce": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p,
+                               c_int64, c_void_p]),
+    "ste_rowmat_f32": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "ste_text_embed_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
     "ste_text_embed_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,

@@ -9,9 +9,14 @@
 //   -> 512-point radix-2 FFT in LDS (fp32, twiddles from double sincos) -> |X|^2
 //   -> 80 kaldi-scale triangular mel filters built in mel space (sparse, per-block
 //   table) -> max(1.1920929e-7, .) -> natural log.
-// Kernel 2 (one block per clip): per-mel-bin mean / unbiased variance over the clip's
-// frames in fp64, (x-mean)/sqrt(var+1e-7), pad odd frame counts with padding_value,
-// stack frame pairs into 160-d rows, zero rows beyond the clip, write the mask.
+// Kernel 2 (one block per clip): per-mel-bin mean and unbiased variance over the clip's
+// frames exactly as numpy evaluates them on the extractor's float32 log-mel array
+// (tf:…seamless_m4t…:256-261: x.mean(0), x.var(0, ddof=1), (x - mean)/sqrt(var + 1e-7)):
+// float32 sums accumulated frame by frame in order (numpy's reduction over a non-contiguous
+// axis), IEEE float32 division and square root.  A bin whose frames are all equal (silence at
+// the log floor) therefore reproduces the reference's non-zero rounding residue bit for bit.
+// Kernel 3 (rows of many clips per block): (x - mean)/std, pad odd frame counts with
+// padding_value, stack frame pairs into 160-d rows, zero rows beyond the clip, write the mask.
 // HBM-bound: 4 B/sample in, 640 B per stacked frame + mask out.
 #include "common.h"
 #include "../../include/ste.h"
@@ -180,65 +185,66 @@ __global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restri
     const int st = sm_start[m], ln = sm_len[m], of = sm_off[m];
     float acc = 0.f;
     for (int i = 0; i < ln; ++i) acc += sm_w[of + i] * pw[st + i];
-    out[m] = logf(fmaxf(acc, 1.192092955078125e-07f));
+    out[m] = (float)log((double)fmaxf(acc, 1.192092955078125e-07f));  // float64 log, as numpy
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
   }  // frames of this wave
 }
 
-__global__ __launch_bounds__(256) void fbank_cmvn_kernel(const int32_t* __restrict__ lengths, int Fmax, int Tmax,
-                                                       const float* __restrict__ work, float pad_value,
+// per-clip CMVN statistics: stats[b][m] = mean, stats[b][NMEL + m] = sqrt(var + 1e-7)
+__global__ __launch_bounds__(128) void fbank_stats_kernel(const int32_t* __restrict__ lengths, int Fmax,
+                                                        const float* __restrict__ work, float* __restrict__ stats) {
+  const int b = blockIdx.x, m = threadIdx.x;
+  if (m >= NMEL) return;
+  const int len = lengths[b];
+  const int F = len >= FRAME ? 1 + (len - FRAME) / HOP : 0;
+  const float* x = work + (int64_t)b * Fmax * NMEL + m;
+  float s = 0.f;
+  for (int f = 0; f < F; ++f) s = __fadd_rn(s, x[(int64_t)f * NMEL]);
+  const float mean = F > 0 ? __fdiv_rn(s, (float)F) : 0.f;
+  float q = 0.f;
+  for (int f = 0; f < F; ++f) {
+    const float d = __fsub_rn(x[(int64_t)f * NMEL], mean);
+    q = __fadd_rn(q, __fmul_rn(d, d));
+  }
+  const float var = F > 1 ? __fdiv_rn(q, (float)(F - 1)) : 0.f;
+  stats[(int64_t)b * 2 * NMEL + m] = mean;
+  stats[(int64_t)b * 2 * NMEL + NMEL + m] = __fsqrt_rn(__fadd_rn(var, 1e-7f));
+}
+
+constexpr int NORM_ROWS = 8;   // stacked rows per block of the normalise / stack kernel
+
+__global__ __launch_bounds__(256) void fbank_norm_kernel(const int32_t* __restrict__ lengths, int Fmax, int Tmax,
+                                                       const float* __restrict__ work,
+                                                       const float* __restrict__ stats, float pad_value,
                                                        float* __restrict__ feats, int64_t* __restrict__ mask,
                                                        int mask_mode) {
-  __shared__ double ssum[3][NMEL], ssq[3][NMEL];
-  __shared__ float smean[NMEL], sinv[NMEL];
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int b = blockIdx.y, tid = threadIdx.x;
   const int len = lengths[b];
   const int F = len >= FRAME ? 1 + (len - FRAME) / HOP : 0;
   const int Tb = (F + 1) / 2;
   const float* x = work + (int64_t)b * Fmax * NMEL;
-  const int m = tid % NMEL, part = tid / NMEL;  // 3 partitions of frames (tid < 240)
-  if (part < 3) {
-    double s = 0.0;
-    for (int f = part; f < F; f += 3) s += x[(int64_t)f * NMEL + m];
-    ssum[part][m] = s;
-  }
-  __syncthreads();
-  if (tid < NMEL) {
-    const double mean = (ssum[0][tid] + ssum[1][tid] + ssum[2][tid]) / (double)(F > 0 ? F : 1);
-    smean[tid] = (float)mean;
-  }
-  __syncthreads();
-  if (part < 3) {
-    const double mu = smean[m];
-    double q = 0.0;
-    for (int f = part; f < F; f += 3) {
-      const double d = x[(int64_t)f * NMEL + m] - mu;
-      q += d * d;
-    }
-    ssq[part][m] = q;
-  }
-  __syncthreads();
-  if (tid < NMEL) {
-    const double var = (ssq[0][tid] + ssq[1][tid] + ssq[2][tid]) / (double)(F > 1 ? F - 1 : 1);
-    sinv[tid] = (float)(1.0 / sqrt(var + 1e-7));
-  }
-  __syncthreads();
-  float* o = feats + (int64_t)b * Tmax * (2 * NMEL);
-  for (int i = tid; i < Tmax * 2 * NMEL; i += 256) {
-    const int t = i / (2 * NMEL), c = i % (2 * NMEL);
+  const float* st = stats + (int64_t)b * 2 * NMEL;
+  const int t0 = blockIdx.x * NORM_ROWS;
+  float* o = feats + ((int64_t)b * Tmax + t0) * (2 * NMEL);
+  for (int i = tid; i < NORM_ROWS * 2 * NMEL; i += 256) {
+    const int t = t0 + i / (2 * NMEL), c = i % (2 * NMEL);
+    if (t >= Tmax) break;
     const int f = 2 * t + (c >= NMEL), mm = c % NMEL;
     // beyond the clip: collate zero-padding (mode 0) or the extractor's batch padding value (mode 1)
     float val = mask_mode == 0 ? 0.f : pad_value;
-    if (t < Tb) val = f < F ? (x[(int64_t)f * NMEL + mm] - smean[mm]) * sinv[mm] : pad_value;
+    if (t < Tb) val = f < F ? __fdiv_rn(__fsub_rn(x[(int64_t)f * NMEL + mm], st[mm]), st[NMEL + mm]) : pad_value;
     o[i] = val;
   }
-  for (int t = tid; t < Tmax; t += 256) {
-    int64_t mv;
-    if (mask_mode == 0) mv = t < Tb ? 1 : 0;
-    else mv = (t < Tb && 2 * t + 1 < F) ? 1 : 0;
-    mask[(int64_t)b * Tmax + t] = mv;
+  if (tid < NORM_ROWS) {
+    const int t = t0 + tid;
+    if (t < Tmax) {
+      int64_t mv;
+      if (mask_mode == 0) mv = t < Tb ? 1 : 0;
+      else mv = (t < Tb && 2 * t + 1 < F) ? 1 : 0;
+      mask[(int64_t)b * Tmax + t] = mv;
+    }
   }
 }
 
@@ -257,8 +263,11 @@ extern "C" int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* length
   hipLaunchKernelGGL(fbank_logmel_kernel, dim3((Fmax + fpb - 1) / fpb, B), dim3(256), 0, s, wav, ld_wav, lengths,
                      Fmax, tab, logmel);
   STE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(fbank_cmvn_kernel, dim3(B), dim3(256), 0, s, lengths, Fmax, Tmax, logmel, pad_value, feats,
-                     mask, mask_mode);
+  float* stats = work + TABLE_FLOATS + (int64_t)B * Fmax * NMEL;
+  hipLaunchKernelGGL(fbank_stats_kernel, dim3(B), dim3(128), 0, s, lengths, Fmax, logmel, stats);
+  STE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(fbank_norm_kernel, dim3((Tmax + NORM_ROWS - 1) / NORM_ROWS, B), dim3(256), 0, s, lengths, Fmax,
+                     Tmax, logmel, stats, pad_value, feats, mask, mask_mode);
   STE_CHECK_LAUNCH();
   return 0;
 }

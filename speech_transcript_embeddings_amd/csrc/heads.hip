@@ -432,6 +432,92 @@ __global__ __launch_bounds__(NT) void pair_sim_bwd_kernel(const float* a, const 
   }
 }
 
+// ------------------------------------ data-parallel global similarity
+// Rows of the global matrix S = A_g·[Tpos_g ; Tneg_g]ᵀ ([NB x 2NB], NB = ranks x local batch),
+// one block per row i: the reference's metrics on its diagonals (ref train_epoch :1120-1161:
+// to_human_readable = sigmoid(s/0.1), clean / corrupt / gap), the pair accuracy s_pos > s_neg and
+// the in-batch top-1 retrieval hit (argmax over the NB clean transcripts == i).
+// acc (fp64, accumulated): [Σ sigmoid(s_pos/τ), Σ sigmoid(s_neg/τ), Σ [s_pos > s_neg], Σ hit, rows,
+//                            loss_w · Σ_r losses[r] (the ranks' batch losses x local batch)]
+__global__ __launch_bounds__(NT) void pair_metrics_kernel(const float* S, int64_t ldS, int NB, int off_neg, float tau,
+                                                        const float* losses, int nloss, float loss_w, double* acc) {
+  __shared__ float rv[8];
+  __shared__ int ri[8];
+  const int i = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* row = S + (int64_t)i * ldS;
+  float best = -INFINITY;
+  int bj = 0x7fffffff;
+  for (int j = tid; j < NB; j += NT) {
+    const float v = row[j];
+    if (v > best || (v == best && j < bj)) { best = v; bj = j; }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oj = __shfl_xor(bj, o, 64);
+    if (ov > best || (ov == best && oj < bj)) { best = ov; bj = oj; }
+  }
+  if (lane == 0) { rv[w] = best; ri[w] = bj; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int k = 1; k < NT / 64; ++k)
+      if (rv[k] > best || (rv[k] == best && ri[k] < bj)) { best = rv[k]; bj = ri[k]; }
+    const float sp = row[i], sn = row[off_neg + i];
+    atomicAdd(acc + 0, (double)sigmoidf_(sp / tau));
+    atomicAdd(acc + 1, (double)sigmoidf_(sn / tau));
+    atomicAdd(acc + 2, sp > sn ? 1.0 : 0.0);
+    atomicAdd(acc + 3, bj == i ? 1.0 : 0.0);
+    atomicAdd(acc + 4, 1.0);
+    if (i == 0 && losses) {
+      double ls = 0.0;
+      for (int r = 0; r < nloss; ++r) ls += (double)losses[r];
+      atomicAdd(acc + 5, ls * (double)loss_w);
+    }
+  }
+}
+
+// Optional in-batch-negative InfoNCE (off by default: the reference's loss has no cross-sample
+// term): local audio rows i against all NB clean transcripts of the global batch,
+// logits S[i][j]/τ, target row0 + i.  loss += w·gs/B Σ_i CE_i;  dS[i][j] = w·gs/B (softmax_j - δ)/τ.
+__global__ __launch_bounds__(NT) void inbatch_ce_kernel(const float* S, int64_t ldS, int B, int NB, int row0, float tau,
+                                                      float weight, const float* gscale, float* loss, float* dS,
+                                                      int64_t lddS) {
+  __shared__ float red[8];
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const float* row = S + (int64_t)i * ldS;
+  const float it = 1.0f / tau;
+  float mx = -INFINITY;
+  for (int j = tid; j < NB; j += NT) mx = fmaxf(mx, row[j] * it);
+  mx = block_max(mx, red);
+  float sum = 0.f;
+  for (int j = tid; j < NB; j += NT) sum += __expf(row[j] * it - mx);
+  sum = block_sum(sum, red);
+  const float lse = mx + __logf(sum);
+  const float c = weight * (gscale ? gscale[0] : 1.f) / (float)B;
+  const int t = row0 + i;
+  for (int j = tid; j < NB; j += NT) {
+    const float p = __expf(row[j] * it - lse);
+    dS[(int64_t)i * lddS + j] = c * (p - (j == t ? 1.f : 0.f)) * it;
+  }
+  if (tid == 0) atomicAdd(loss, c * (lse - row[t] * it) / (gscale ? gscale[0] : 1.f));
+}
+
+// out[r][p] += Σ_c X[r*sxr + c*sxc] · Y[c][p]  (small fp32 products of the in-batch backward:
+// dA = dS·T_g and dT_g = dSᵀ·A); one block per output row.
+__global__ __launch_bounds__(NT) void rowmat_f32_kernel(const float* X, int64_t sxr, int64_t sxc, const float* Y, int C,
+                                                      int P, float* out) {
+  const int r = blockIdx.x;
+  for (int p0 = threadIdx.x * 4; p0 < P; p0 += NT * 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < C; ++c) {
+      const float x = X[(int64_t)r * sxr + (int64_t)c * sxc];
+      acc += x * *reinterpret_cast<const f32x4*>(Y + (int64_t)c * P + p0);
+    }
+    f32x4* o = reinterpret_cast<f32x4*>(out + (int64_t)r * P + p0);
+    *o = *o + acc;
+  }
+}
+
 }  // namespace
 
 extern "C" int ste_attn_pool_fwd(const void* t, const float* w2, const float* b2, const void* h, const int32_t* mask,
@@ -547,6 +633,32 @@ extern "C" int ste_pair_sim_bwd(const float* a, const float* tp, const float* tn
   if (B <= 0 || P <= 0) return STE_ERR_SHAPE;
   hipLaunchKernelGGL(pair_sim_bwd_kernel, dim3(B), dim3(NT), 0, (hipStream_t)stream, a, tp, tn, ds_pos, ds_neg, P,
                      da, dtp, dtn);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_pair_metrics(const float* S, int64_t ldS, int NB, int off_neg, float tau, const float* losses,
+                                int nloss, float loss_w, double* acc, void* stream) {
+  if (NB <= 0 || ldS < off_neg + NB) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(pair_metrics_kernel, dim3(NB), dim3(NT), 0, (hipStream_t)stream, S, ldS, NB, off_neg, tau, losses,
+                     nloss, loss_w, acc);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_inbatch_ce(const float* S, int64_t ldS, int B, int NB, int row0, float tau, float weight,
+                              const float* gscale, float* loss, float* dS, int64_t lddS, void* stream) {
+  if (B <= 0 || NB <= 0 || row0 < 0 || row0 + B > NB || ldS < NB || lddS < NB) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(inbatch_ce_kernel, dim3(B), dim3(NT), 0, (hipStream_t)stream, S, ldS, B, NB, row0, tau, weight,
+                     gscale, loss, dS, lddS);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_rowmat_f32(const float* X, int64_t sxr, int64_t sxc, const float* Y, int R, int C, int P,
+                              float* out, void* stream) {
+  if (R <= 0 || C <= 0 || (P & 3)) return STE_ERR_SHAPE;
+  hipLaunchKernelGGL(rowmat_f32_kernel, dim3(R), dim3(NT), 0, (hipStream_t)stream, X, sxr, sxc, Y, C, P, out);
   STE_CHECK_LAUNCH();
   return 0;
 }

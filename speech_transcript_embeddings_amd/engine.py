@@ -54,6 +54,9 @@ class Engine:
         # the audio encoder: its GEMMs are too small to fill 256 CUs (8,192 rows) and overlap the
         # audio side's bandwidth-bound kernels.  STE_TEXT_STREAM=0: one stream (A/B runs).
         self.overlap = os.environ.get("STE_TEXT_STREAM", "1") != "0"
+        # layerdrop draws (tf:…wav2vec2_bert…:519-522): the global torch RNG unless a trainer sets a
+        # generator (TrainStep broadcasts one seed so every data-parallel rank drops the same layers)
+        self.layerdrop_gen = None
 
     @property
     def fp8(self):
@@ -141,7 +144,7 @@ class Engine:
         xb = None
         nl = c.num_hidden_layers
         for i in range(nl):
-            if train and c.layerdrop > 0 and float(torch.rand([])) < c.layerdrop:
+            if train and c.layerdrop > 0 and float(torch.rand([], generator=self.layerdrop_gen)) < c.layerdrop:
                 layers.append(None)
                 continue
             last = i == nl - 1

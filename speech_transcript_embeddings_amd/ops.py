@@ -105,6 +105,25 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
 
 
 GEMM_TRACE = None  # list while bench.py measures per-launch GEMM durations with HIP events
+# list while bench.py measures the HBM-bound kernels (fbank, LayerNorm): (name, algorithmic
+# bytes, ev0, ev1) per launch, timed with HIP events on the launching (current) stream
+HBM_TRACE = None
+
+
+def _traced(name, nbytes, launch):
+    if HBM_TRACE is None:
+        launch()
+        return
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    launch()
+    ev1.record()
+    HBM_TRACE.append((name, float(nbytes), ev0, ev1))
+
+
+def _nb(t):
+    return 0 if t is None else t.numel() * t.element_size()
 
 
 def gemm_kernel_name(args: GemmArgs) -> str:
@@ -168,7 +187,10 @@ def layernorm_fwd(x, gamma, beta, eps, *, y=None, yb=None, mean=None, rstd=None,
     a.act, a.drop_p, a.seed = int(act), float(drop_p), int(seed) & (2**64 - 1)
     if q8 is not None:  # (e4m3 [rows, cols], E8M0 [rows, cols/32]): MX-fp8 copy for ste_gemm_mx8
         a.q8, a.q8s, a.ldq8 = ptr(q8[0]), ptr(q8[1]), _ld(q8[0])
-    call("ste_layernorm_fwd", C.byref(a), _s())
+    # algorithmic bytes: read x, write every requested output, 8 B/row of statistics
+    nbytes = rows * cols * (x.element_size() + (4 if y is not None else 0) + (2 if yb is not None else 0) +
+                            (1 + 1 / 32 if q8 is not None else 0)) + 8 * rows + 8 * cols
+    _traced("layernorm_fwd", nbytes, lambda: call("ste_layernorm_fwd", C.byref(a), _s()))
     return mean, rstd
 
 
@@ -192,7 +214,10 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, *, beta=None, dx=None, dxb=None, dre
     a.drop_p, a.seed, a.out_scale = float(drop_p), int(seed) & (2**64 - 1), float(out_scale)
     a.in_drop_p, a.in_seed = float(in_drop_p), int(in_seed) & (2**64 - 1)
     a.out_row_scale, a.dsum = ptr(out_row_scale), ptr(dsum)
-    call("ste_layernorm_bwd", C.byref(a), _s())
+    # algorithmic bytes: read dy, x (and dres), write dx / dxb, 8 B/row of statistics
+    nbytes = rows * cols * (dy.element_size() + x.element_size() + (4 if dres is not None else 0) +
+                            (4 if dx is not None else 0) + (2 if dxb is not None else 0)) + 8 * rows + 16 * cols
+    _traced("layernorm_bwd", nbytes, lambda: call("ste_layernorm_bwd", C.byref(a), _s()))
     return dx, dxb
 
 
@@ -262,9 +287,11 @@ def fbank(wav, lengths, Tmax, *, pad_value=1.0, mask_mode=0, feats=None, mask=No
     if mask is None:
         mask = torch.empty((B, Tmax), device=dev, dtype=torch.int64)
     if work is None:
-        work = torch.empty(2048 + B * 2 * Tmax * 80, device=dev, dtype=F32)
-    call("ste_fbank", ptr(wav), wav.stride(0), ptr(lengths), B, Tmax, float(pad_value), ptr(feats), ptr(mask),
-         int(mask_mode), ptr(work), _s())
+        work = torch.empty(2048 + B * 2 * Tmax * 80 + B * 160, device=dev, dtype=F32)
+    # algorithmic bytes: the waveforms once, the stacked features and the mask
+    nbytes = 4 * B * wav.shape[1] + _nb(feats) + _nb(mask)
+    _traced("fbank", nbytes, lambda: call("ste_fbank", ptr(wav), wav.stride(0), ptr(lengths), B, Tmax,
+                                          float(pad_value), ptr(feats), ptr(mask), int(mask_mode), ptr(work), _s()))
     return feats, mask
 
 
@@ -346,6 +373,32 @@ def pair_loss_bwd(s_pos, s_neg, align, B, L, tau, aw, gamma, gscale, ds_pos, ds_
 def pair_sim_bwd(a, tp, tn, ds_pos, ds_neg, da, dtp, dtn):
     call("ste_pair_sim_bwd", ptr(a), ptr(tp), ptr(tn), ptr(ds_pos), ptr(ds_neg), a.shape[0], a.shape[1], ptr(da),
          ptr(dtp), ptr(dtn), _s())
+
+
+def pair_metrics(S, off_neg, tau, acc, losses=None, loss_w=1.0):
+    """acc fp64[6] += [Σ sigmoid(s_pos/τ), Σ sigmoid(s_neg/τ), Σ s_pos>s_neg, Σ top-1 hit, rows,
+    loss_w·Σ losses] over S's rows (ste_pair_metrics)."""
+    call("ste_pair_metrics", ptr(S), _ld(S), S.shape[0], int(off_neg), float(tau), ptr(losses),
+         0 if losses is None else losses.numel(), float(loss_w), ptr(acc), _s())
+
+
+def inbatch_ce(S, B, NB, row0, tau, weight, gscale, loss, dS):
+    """In-batch-negative InfoNCE over the NB global clean transcripts: loss += ..., dS [B, NB] written."""
+    call("ste_inbatch_ce", ptr(S), _ld(S), B, NB, int(row0), float(tau), float(weight), ptr(gscale), ptr(loss),
+         ptr(dS), _ld(dS), _s())
+
+
+def rowmat(X, Y, out, transpose_x=False):
+    """out[R, P] += X·Y (or Xᵀ·Y) for small fp32 matrices (X [R, C] or [C, R], Y [C, P])."""
+    if transpose_x:
+        C, R = X.shape
+        sxr, sxc = X.stride(1), X.stride(0)
+    else:
+        R, C = X.shape
+        sxr, sxc = X.stride(0), X.stride(1)
+    assert Y.shape[0] == C and Y.is_contiguous() and out.shape == (R, Y.shape[1]) and out.is_contiguous()
+    call("ste_rowmat_f32", ptr(X), sxr, sxc, ptr(Y), R, C, Y.shape[1], ptr(out), _s())
+    return out
 
 
 # -------------------------------------------------------------- embedding

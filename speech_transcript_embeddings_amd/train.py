@@ -154,6 +154,11 @@ class FusedAdamW:
         g0 = pgs[0]
         self.wd, self.betas, self.eps = float(g0["weight_decay"]), tuple(g0["betas"]), float(g0["eps"])
 
+    def total_norm(self):
+        """clip_grad_norm_'s return value for the last step (the pre-clip global gradient norm);
+        reads the on-device Σg² (host sync)."""
+        return math.sqrt(float(self.sumsq.item()))
+
     def step(self, lr_factor: float = 1.0):
         st = self.store
         self.t += 1
@@ -178,15 +183,22 @@ class FusedAdamW:
 class GradSync:
     """Data-parallel gradient averaging, overlapped with the backward.
 
-    The flat gradient buffer is split into the blocks the backward finishes in order:
-    heads, audio encoder, text encoder.  As engine.backward reports a block final, its
-    dense ranges are all-reduced asynchronously (RCCL ring over xGMI, <= bucket_mb per
-    call, average) while the remaining backward kernels run; the collective waits only for
-    the work already enqueued.  The 250,002 x 768 word-embedding gradient is exchanged
-    row-sparse: each rank extracts the rows of its own token ids (ste_rows_extract),
-    all-gathers fixed-capacity (id, row) lists and adds every rank's list in rank order
-    (ste_rows_accumulate), so every rank ends with the same averaged dense gradient that
-    an all-reduce would give, from ~2*b*L rows instead of 192 M values.
+    The flat gradient buffer is split into the blocks the backward finishes in order
+    (STAGES), and engine.backward calls stage_done(name) as each becomes final:
+      "heads"         after the heads' backward (before either encoder's);
+      "audio_layers"  the trainable Conformer layers, once the backward has passed the lowest of
+                      them (the frozen layers' input-gradient passes still run behind it);
+      "audio"         the rest of the audio encoder (feature projection, SpecAugment embedding),
+                      at the end of the audio backward;
+      "text"          the text encoder (its backward runs on the side stream; joined at the end).
+    Each block's dense ranges are all-reduced asynchronously (RCCL ring over xGMI, <= bucket_mb
+    per call, average) while the remaining backward kernels run.  The 250,002 x 768
+    word-embedding gradient is exchanged row-sparse: each rank extracts the rows of its own token
+    ids (ste_rows_extract), all-gathers fixed-capacity (id, row) lists and adds every rank's list in
+    rank order (ste_rows_accumulate), so every rank ends with the same averaged dense gradient an
+    all-reduce would give, from ~2*b*L rows instead of 192 M values.  When the lists would not be
+    smaller than the table (world x capacity >= vocab / 2, e.g. long accumulation windows), the
+    table goes through the dense all-reduce instead.
     `finish()` waits for every collective (on the current stream) before clip + AdamW.
     """
 
@@ -205,11 +217,21 @@ class GradSync:
         self.sparse = None
         grad_slots = [sl for sl in store.slots.values() if sl.segment in ("enc", "head")]
 
+        ordered = sorted(grad_slots, key=lambda x: x.offset)
+
         def span(pred):
-            sl = [x for x in grad_slots if pred(x)]
-            if not sl:
-                return []
-            return [(min(x.offset for x in sl), max(x.offset + x.numel for x in sl))]
+            """The contiguous runs of matching slots in buffer order (a slot of another block
+            ends a run), so a block never swallows another block's slots."""
+            runs, cur = [], None
+            for x in ordered:
+                if pred(x):
+                    cur = [x.offset, x.offset + x.numel] if cur is None else [cur[0], x.offset + x.numel]
+                elif cur is not None:
+                    runs.append(tuple(cur))
+                    cur = None
+            if cur is not None:
+                runs.append(tuple(cur))
+            return runs
 
         words = store.slots.get(self.WORDS)
         self.words = words if words is not None and words.segment == "enc" else None
@@ -220,12 +242,22 @@ class GradSync:
                                      not x.name.startswith("audio_encoder.encoder.layers.")),
                        "text": span(lambda x: x.segment == "enc" and x.name.startswith("text_encoder."))}
         if self.words is not None and self.ranges["text"]:
-            (a, b), w0, w1 = self.ranges["text"][0], self.words.offset, self.words.offset + self.words.numel
-            self.ranges["text"] = [r for r in ((a, w0), (w1, b)) if r[1] > r[0]]
-        # the blocks must tile [0, n_grad) without overlap (checked once)
+            w0, w1 = self.words.offset, self.words.offset + self.words.numel
+            cut = []
+            for a, b in self.ranges["text"]:
+                cut += [r for r in ((a, min(b, w0)), (max(a, w1), b)) if r[1] > r[0]] if a < w1 and w0 < b else [(a, b)]
+            self.ranges["text"] = cut
+        # the blocks must not overlap, and every gradient slot must lie inside exactly one block
+        # (a slot no block covers would never be synchronised and the replicas would drift)
         cov = sorted(r for rs in self.ranges.values() for r in rs)
         for (a0, b0), (a1, b1) in zip(cov, cov[1:]):
             assert b0 <= a1, "gradient blocks overlap"
+        for x in grad_slots:
+            if self.words is not None and x.name == self.WORDS:
+                continue
+            inside = [k for k, rs in self.ranges.items()
+                      if any(a <= x.offset and x.offset + x.numel <= b for a, b in rs)]
+            assert len(inside) == 1, f"gradient slot {x.name} is in {len(inside)} sync blocks"
         self._flags = None
 
     @staticmethod
@@ -253,7 +285,7 @@ class GradSync:
         dev = st.device
         if self._flags is None:
             self._flags = torch.zeros(sl.shape[0], device=dev, dtype=torch.int32)
-        cap = ids.numel()
+        cap = min(ids.numel(), sl.shape[0])
         out_ids = torch.empty(cap, device=dev, dtype=torch.int32)
         rows = torch.empty(cap, D, device=dev, dtype=F32)
         count = torch.empty(1, device=dev, dtype=torch.int32)
@@ -265,12 +297,22 @@ class GradSync:
         w2 = dist.all_gather_into_tensor(all_rows, rows, async_op=True)
         self.sparse = (g2, all_ids, all_rows, cap, ws, (w1, w2), (out_ids, rows))
 
+    def sparse_pays(self, n_ids: int) -> bool:
+        """Row-sparse word-table exchange only while world x capacity rows stay well below the
+        table (with long accumulation windows the (id, row) lists outgrow a dense
+        all-reduce of the 250,002 x 768 table)."""
+        ws = dist.get_world_size()
+        return ws * min(n_ids, self.words.shape[0]) < self.words.shape[0] // 2
+
     def stage_done(self, stage, ids=None):
         if not self.active():
             return
         self._reduce(self.ranges[stage])
-        if stage == "text" and self.words is not None and ids is not None:
-            self._sparse_words(ids)
+        if stage == "text" and self.words is not None:
+            if ids is not None and self.sparse_pays(ids.numel()):
+                self._sparse_words(ids)
+            else:
+                self._reduce([(self.words.offset, self.words.offset + self.words.numel)])
 
     def finish(self):
         for w in self.works:
@@ -285,17 +327,137 @@ class GradSync:
             self.sparse = None
 
 
+class EmbeddingExchange:
+    """north_star's "RCCL all-gather of embeddings over xGMI before the similarity matmul"
+    (SURVEY §8e, D1).
+
+    start() (after the forward): the L2-normalised audio, clean and corrupted transcript
+    embeddings [B, P] of every rank are all-gathered asynchronously into A_g [NB, P] and
+    T_g = [Tpos_g; Tneg_g] [2NB, P] (NB = ranks x B); the collective runs on RCCL's stream
+    while the local loss and the backward proceed.
+    finish() (after the backward): waits, forms the global similarity matrix
+    S_g = A_g·T_gᵀ [NB, 2NB] on the fp32 MFMA (its diagonals are every rank's s_pos / s_neg,
+    the reference's per-sample logits, ref :1073-1074) and accumulates the reference's epoch
+    metrics on the device (ref train_epoch :1120-1161: sample-weighted loss, clean / corrupt
+    similarity as sigmoid(s/0.1), gap) plus the pair accuracy and the in-batch top-1 retrieval
+    rate; epoch_metrics() syncs them to the host once.
+    Optional in-batch negatives (in_batch_weight > 0; 0 by default = the reference's loss): the
+    gather is awaited before the loss, the local rows S = A·Tpos_gᵀ [B, NB] feed an InfoNCE over
+    all NB clean transcripts of the global batch (target: the sample's own), the audio gradient
+    is dS·Tpos_g and the transcript gradient dSᵀ·A is reduce-scattered (sum) to the owning
+    ranks before their L2-normalise backward.  With one process the same code runs without
+    collectives (NB = B)."""
+
+    def __init__(self, tau: float = 0.1, in_batch_weight: float = 0.0):
+        self.tau, self.weight = float(tau), float(in_batch_weight)
+        self.acc = None
+        self.steps = 0
+        self._pending = None
+
+    @staticmethod
+    def world():
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_world_size(), dist.get_rank()
+        return 1, 0
+
+    def start(self, an, tn_all):
+        ws, rank = self.world()
+        B, P = an.shape
+        NB = ws * B
+        if ws == 1:
+            self._pending = (an, tn_all, [], B, 1, 0)
+            return
+        A_g = torch.empty(NB, P, device=an.device, dtype=F32)
+        T_g = torch.empty(2 * NB, P, device=an.device, dtype=F32)
+        works = [dist.all_gather_into_tensor(A_g, an, async_op=True),
+                 dist.all_gather_into_tensor(T_g[:NB], tn_all[:B], async_op=True),
+                 dist.all_gather_into_tensor(T_g[NB:], tn_all[B:], async_op=True)]
+        self._pending = (A_g, T_g, works, B, ws, rank)
+
+    def _wait(self):
+        A_g, T_g, works, B, ws, rank = self._pending
+        for w in works:
+            w.wait()
+        self._pending = (A_g, T_g, [], B, ws, rank)
+        return A_g, T_g, B, ws, rank
+
+    def in_batch(self, an, gscale, loss, dan, dtp):
+        """Adds the in-batch InfoNCE value to loss and its gradients to dan / dtp (the cotangents of
+        the local normalised audio / clean transcript embeddings)."""
+        A_g, T_g, B, ws, rank = self._wait()
+        NB = ws * B
+        e = lambda *sh: torch.empty(sh, device=an.device, dtype=F32)  # noqa: E731
+        S = e(B, NB)
+        ops.similarity(an, T_g[:NB], S)
+        dS = e(B, NB)
+        ops.inbatch_ce(S, B, NB, rank * B, self.tau, self.weight, gscale, loss, dS)
+        ops.rowmat(dS, T_g[:NB], dan)                      # d a_i   += Σ_j dS_ij t_j
+        dT = torch.zeros(NB, an.shape[1], device=an.device, dtype=F32)
+        ops.rowmat(dS, an, dT, transpose_x=True)           # d t_j   += Σ_i dS_ij a_i (every rank's t_j)
+        if ws > 1:
+            if dist.get_backend() == "gloo" and dT.is_cuda:   # gloo reduce-scatters host tensors only
+                mine = torch.empty(B, an.shape[1], dtype=F32)
+                dist.reduce_scatter_tensor(mine, dT.cpu(), op=dist.ReduceOp.SUM)
+                mine = mine.to(dT.device)
+            else:
+                mine = e(B, an.shape[1])
+                dist.reduce_scatter_tensor(mine, dT, op=dist.ReduceOp.SUM)
+            ops.axpby(dtp, mine)
+        else:
+            ops.axpby(dtp, dT)
+
+    def finish(self, loss):
+        """Global similarity matrix + on-device metric accumulation (after the backward)."""
+        if self._pending is None:
+            return
+        A_g, T_g, B, ws, rank = self._wait()
+        self._pending = None
+        NB = ws * B
+        dev = A_g.device
+        if self.acc is None:
+            self.acc = torch.zeros(6, device=dev, dtype=torch.float64)
+        losses = loss
+        if ws > 1:
+            losses = torch.empty(ws, device=dev, dtype=F32)
+            dist.all_gather_into_tensor(losses, loss)
+        S = torch.empty(NB, 2 * NB, device=dev, dtype=F32)
+        ops.similarity(A_g, T_g, S)
+        ops.pair_metrics(S, NB, self.tau, self.acc, losses=losses, loss_w=float(B))
+        self.last_S = S
+        self.steps += 1
+
+    def epoch_metrics(self, reset: bool = True):
+        """The reference's train_epoch return keys (ref :1156-1162) over the global batch, plus
+        pair_accuracy (s_pos > s_neg) and in_batch_top1 (retrieval among the clean transcripts).
+        One device->host transfer."""
+        if self.acc is None or self.acc[4].item() == 0:
+            return {}
+        a = self.acc.cpu().tolist()
+        n = a[4]
+        out = {"loss": a[5] / n, "clean_similarity": a[0] / n, "corrupt_similarity": a[1] / n,
+               "similarity_gap": (a[0] - a[1]) / n, "pair_accuracy": a[2] / n, "in_batch_top1": a[3] / n,
+               "samples": int(n)}
+        if reset:
+            self.acc.zero_()
+        return out
+
+
 class TrainStep:
     """fbank -> forward -> loss -> backward -> all-reduce -> clip + AdamW (+ schedule)."""
 
     def __init__(self, model: EnhancedAudioTextModel, lr=2.1e-3, warmup=100, total_steps=10000, temperature=0.1,
                  alignment_weight=0.5, corrupt_gamma=0.35, max_norm=1.0, pad_value=1.0, gather_embeddings=True,
-                 accumulation_steps=1):
+                 accumulation_steps=1, in_batch_weight=0.0):
         """accumulation_steps (ref train_epoch :1064-1117): each call is one micro-batch whose loss
         gradient is scaled by 1/accumulation_steps and summed into the flat gradient buffer; the
         data-parallel sync, clip, AdamW and scheduler step run on every accumulation_steps-th
         call (the sync overlapped with that micro-batch's backward) and on flush(), the
-        reference's `is_last_batch` step after a partial window."""
+        reference's `is_last_batch` step after a partial window.
+        gather_embeddings: the EmbeddingExchange (global similarity matrix + on-device epoch
+        metrics); in_batch_weight > 0 adds its optional in-batch-negative InfoNCE term (0 keeps
+        the reference's loss exactly).
+        Data parallel: rank 0's layerdrop seed is broadcast so every rank drops the same Conformer
+        layers (tf:…wav2vec2_bert…:519-522 draws one number per layer per batch)."""
         self.model = model
         self.acc = max(1, int(accumulation_steps))
         self._micro = 0
@@ -305,8 +467,19 @@ class TrainStep:
         self.gradsync = GradSync(model.store, pad_id=model.text_cfg.pad_token_id)
         self.tau, self.aw, self.gamma = temperature, alignment_weight, corrupt_gamma
         self.pad_value = pad_value
-        self.gather_embeddings = gather_embeddings
+        self.gather_embeddings = gather_embeddings or in_batch_weight > 0
+        self.exchange = EmbeddingExchange(temperature, in_batch_weight) if self.gather_embeddings else None
+        self.in_batch_weight = float(in_batch_weight)
         self.last = {}
+        self._sync_layerdrop_seed()
+
+    def _sync_layerdrop_seed(self):
+        seed = torch.randint(0, 2**62, (1,), dtype=torch.int64)
+        if GradSync.active():
+            t = seed.to(self.model.store.device) if dist.get_backend() == "nccl" else seed.clone()
+            dist.broadcast(t, src=0)
+            seed = t.cpu()
+        self.model.engine.layerdrop_gen = torch.Generator().manual_seed(int(seed.item()))
 
     def features(self, wav, lengths):
         """GPU fbank for a batch of raw 16 kHz waveforms -> (input_values, attention_mask_audio)."""
@@ -315,11 +488,17 @@ class TrainStep:
         return ops.fbank(wav, lengths, T, pad_value=self.pad_value, mask_mode=0)
 
     def __call__(self, wav, lengths, ids_pos, mask_pos, ids_neg, mask_neg):
+        """One micro-batch from raw 16 kHz waveforms (GPU fbank first)."""
+        feats, amask = self.features(wav, lengths)
+        return self.step_batch({"input_ids_pos": ids_pos, "attention_mask_pos": mask_pos, "input_ids_neg": ids_neg,
+                                "attention_mask_neg": mask_neg, "input_values": feats,
+                                "attention_mask_audio": amask})
+
+    def step_batch(self, batch):
+        """One micro-batch given the reference's collated batch dict (custom_collate_fn layout,
+        ref :913-921: input_values are features), on the GPU."""
         m = self.model
         m.train()
-        feats, amask = self.features(wav, lengths)
-        batch = {"input_ids_pos": ids_pos, "attention_mask_pos": mask_pos, "input_ids_neg": ids_neg,
-                 "attention_mask_neg": mask_neg, "input_values": feats, "attention_mask_audio": amask}
         st = m.store
         st.sync_shadow()
         eng = m.engine
@@ -338,8 +517,8 @@ class TrainStep:
         sp, sn, loss = e(B), e(B), e(1)
         L = align.shape[1] if align is not None else 0
         ops.pair_loss_fwd(S, B, align, B, L, self.tau, self.aw, self.gamma, sp, sn, loss)
-        if self.gather_embeddings and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            self._gather_metrics(an, tn_all)
+        if self.exchange is not None:
+            self.exchange.start(an, tn_all)   # async all-gather of the embeddings (overlaps the backward)
         # backward
         dsp, dsn = e(B), e(B)
         dal = e(B, L) if align is not None else None
@@ -347,6 +526,8 @@ class TrainStep:
         ops.pair_loss_bwd(sp, sn, align, B, L, self.tau, self.aw, self.gamma, gscale, dsp, dsn, dal)
         dan, dtp, dtn = e(B, P), e(B, P), e(B, P)
         ops.pair_sim_bwd(an, tn_all[:B], tn_all[B:], dsp, dsn, dan, dtp, dtn)
+        if self.in_batch_weight > 0:
+            self.exchange.in_batch(an, gscale, loss, dan, dtp)
         g_tp, g_tn, g_a = e(B, P), e(B, P), e(B, P)
         ops.l2norm_bwd(tn_all[:B], nrm[:B], dtp, g_tp)
         ops.l2norm_bwd(tn_all[B:], nrm[B:2 * B], dtn, g_tn)
@@ -361,9 +542,17 @@ class TrainStep:
         eng.backward(ctx, g_tp, g_tn, g_a, dal,
                      stage_done=(lambda stg: self.gradsync.stage_done(stg, ids_all)) if final else None)
         self.last = {"loss": loss, "s_pos": sp, "s_neg": sn}
+        if self.exchange is not None:
+            self.exchange.finish(loss)
         if final:
             self._optimizer_step()
         return loss
+
+    def epoch_metrics(self):
+        """train_epoch's return dict (ref :1156-1162) over the global batch, synced once."""
+        out = self.exchange.epoch_metrics() if self.exchange is not None else {}
+        out["optimizer_steps"] = self.opt.t
+        return out
 
     def _optimizer_step(self):
         self.gradsync.finish()
@@ -394,14 +583,6 @@ class TrainStep:
         self.opt.load_state_dict(sd)
         self.sched.step_count = self.opt.t
 
-    def _gather_metrics(self, an, tn_all):
-        ws = dist.get_world_size()
-        ga = [torch.empty_like(an) for _ in range(ws)]
-        dist.all_gather(ga, an)
-        gt = [torch.empty_like(tn_all) for _ in range(ws)]
-        dist.all_gather(gt, tn_all)
-        self.last["global_emb"] = (ga, gt)
-
 
 def synthetic_batch(B, n_samples, L, vocab=250000, device="cuda", seed=0, rank=0):
     """SURVEY §8d synthetic inputs: 0.1·N(0,1) + 3 sinusoids waveforms, ids ~ U[5, vocab) with
@@ -423,4 +604,5 @@ def synthetic_batch(B, n_samples, L, vocab=250000, device="cuda", seed=0, rank=0
     return wav, lengths, ids, mask, neg.contiguous(), mask.clone()
 
 
-__all__ = ["TrainStep", "FusedAdamW", "LinearWarmupSchedule", "GradSync", "synthetic_batch", "_lib"]
+__all__ = ["TrainStep", "FusedAdamW", "LinearWarmupSchedule", "GradSync", "EmbeddingExchange", "synthetic_batch",
+           "_lib"]

@@ -108,6 +108,32 @@ def fbank_fixture(T):
     print("fbank_golden.npz", {k: v.shape for k, v in out.items()})
 
 
+def fbank_long_fixture(T):
+    """Config-size clips (tests/golden/fbank_cases.py): the reference extractor's features/masks
+    and the reference collate over all of them -> fbank_golden_long.npz (waveforms rebuilt from
+    seeds by the tests, not stored)."""
+    from transformers import SeamlessM4TFeatureExtractor
+    sys.path.insert(0, str(HERE))
+    from fbank_cases import LONG_CASES, long_case_wave
+    fe = SeamlessM4TFeatureExtractor(feature_size=80, num_mel_bins=80, padding_value=1.0, sampling_rate=16000,
+                                     stride=2)
+    out, items = {}, []
+    for name, _, _ in LONG_CASES:
+        r = fe(long_case_wave(name), sampling_rate=16000, return_tensors="np")
+        out[f"{name}_feats"] = r["input_features"][0].astype(np.float32)
+        out[f"{name}_mask"] = r["attention_mask"][0].astype(np.int64)
+        items.append({
+            "input_ids_pos": torch.zeros(4, dtype=torch.long), "attention_mask_pos": torch.ones(4, dtype=torch.long),
+            "input_ids_neg": torch.zeros(4, dtype=torch.long), "attention_mask_neg": torch.ones(4, dtype=torch.long),
+            "input_values": torch.from_numpy(out[f"{name}_feats"]),
+            "attention_mask_audio": torch.from_numpy(out[f"{name}_mask"])})
+    batch = T.custom_collate_fn(items)
+    out["batch_mask"] = batch["attention_mask_audio"].numpy()
+    out["cases"] = np.array([c[0] for c in LONG_CASES])
+    np.savez_compressed(HERE / "fbank_golden_long.npz", **out)
+    print("fbank_golden_long.npz", {k: v.shape for k, v in out.items()})
+
+
 def synth_batch(T, B=2, L=12, vocab=1000):
     from transformers import SeamlessM4TFeatureExtractor
     fe = SeamlessM4TFeatureExtractor(feature_size=80, num_mel_bins=80, padding_value=1.0, sampling_rate=16000,
@@ -229,7 +255,11 @@ def param_count_fixture(T):
 
 if __name__ == "__main__":
     T = import_reference()
+    if "--fbank-long" in sys.argv:  # only the config-size fbank fixture
+        fbank_long_fixture(T)
+        sys.exit(0)
     fbank_fixture(T)
+    fbank_long_fixture(T)
     model_fixture(T, use_align=False)
     model_fixture(T, use_align=True)
     model_fixture(T, use_align=False, attentive=False)  # CLS text / masked-mean audio (ref:578-580,621-636)

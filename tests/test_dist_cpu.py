@@ -7,8 +7,13 @@
 * The DP design claim — per-rank gradients of equal local batches, averaged, equal the
   global-batch gradient — checked with the oracle's autograd on the golden mini model
   (alignment head on, so the per-sample alignment weighting is covered too).
-* The embedding all-gather used for global similarity metrics and the per-rank synthetic
-  data shards.
+* EmbeddingExchange (train.py), north_star's all-gather of embeddings before the similarity
+  matmul: the global matrix's diagonals are every rank's local s_pos / s_neg, the on-device
+  metrics equal the reference's formulas over the global batch, and the optional in-batch
+  InfoNCE term (value and both embedding gradients, including the reduce-scattered transcript
+  gradient) equals a torch autograd restatement over the global batch.  Its HIP kernels are
+  replaced by torch stand-ins here (checked on the GPU in tests/test_dist_gpu.py).
+* The layerdrop seed broadcast and the per-rank synthetic data shards.
 """
 import json
 import os
@@ -65,13 +70,14 @@ def _sync_case(rank, world):
     slots = [("text_encoder.embeddings.word_embeddings.weight", 0, (V, D), "enc"),
              ("text_encoder.encoder.layer.1.x", 200, (37,), "enc"),
              ("audio_encoder.encoder.layers.0.x", 240, (101,), "enc"),
-             ("text_proj.weight", 344, (61,), "head"),
+             ("audio_encoder.feature_projection.projection.weight", 344, (13,), "enc"),
+             ("text_proj.weight", 360, (45,), "head"),
              ("text_encoder.pooler.dense.weight", 408, (9,), "nograd")]
 
     def local(r):
         g = torch.zeros(417)
         gen = torch.Generator().manual_seed(100 + r)
-        for a, b in ((200, 237), (240, 341), (344, 405)):  # the dense slots (gaps = alignment padding)
+        for a, b in ((200, 237), (240, 341), (344, 357), (360, 405)):  # dense slots (gaps = alignment padding)
             g[a:b] = torch.randn(b - a, generator=gen)
         ids = torch.randint(2, V, (12,), generator=gen)
         ids[3] = 1  # padding_idx: never a gradient row
@@ -84,12 +90,104 @@ def _sync_case(rank, world):
     g[408:] = 7.0 + rank  # beyond n_grad: must stay untouched
     expect = sum(local(r)[0] for r in range(world)) / world
     gs = GradSync(_Store(g, slots))
+    assert all(gs.ranges[k] for k in GradSync.STAGES), gs.ranges   # every stage has a non-empty block
     gs.bucket = 29  # several buckets + ragged ones
     for stage in GradSync.STAGES:
         gs.stage_done(stage, ids)
     gs.finish()
     n = gs.store.n_grad
     return (g[:n] - expect[:n]).abs().max().item(), bool(torch.all(g[408:] == 7.0 + rank))
+
+
+def _exchange_stand_ins():
+    """torch stand-ins (test-only) for the exchange's HIP kernels."""
+    from speech_transcript_embeddings_amd import ops
+
+    def similarity(a, t, S):
+        S.copy_(a @ t.t())
+
+    def pair_metrics(S, off_neg, tau, acc, losses=None, loss_w=1.0):
+        NB = S.shape[0]
+        i = torch.arange(NB)
+        sp, sn = S[i, i], S[i, off_neg + i]
+        acc[0] += torch.sigmoid(sp / tau).double().sum()
+        acc[1] += torch.sigmoid(sn / tau).double().sum()
+        acc[2] += (sp > sn).double().sum()
+        acc[3] += (S[:, :NB].argmax(1) == i).double().sum()
+        acc[4] += NB
+        if losses is not None:
+            acc[5] += losses.double().sum() * loss_w
+
+    def inbatch_ce(S, B, NB, row0, tau, weight, gscale, loss, dS):
+        lg = S[:, :NB] / tau
+        tgt = torch.arange(B) + row0
+        p = torch.softmax(lg, 1)
+        loss += weight / B * torch.nn.functional.cross_entropy(lg, tgt, reduction="sum")
+        oh = torch.zeros_like(p)
+        oh[torch.arange(B), tgt] = 1.0
+        dS.copy_(weight / B * (p - oh) / tau)
+
+    def rowmat(X, Y, out, transpose_x=False):
+        out += (X.t() if transpose_x else X) @ Y
+        return out
+
+    def axpby(y, x, alpha=1.0, beta=1.0):
+        y.mul_(beta).add_(alpha * x)
+        return y
+    ops.similarity, ops.pair_metrics, ops.inbatch_ce, ops.rowmat, ops.axpby = \
+        similarity, pair_metrics, inbatch_ce, rowmat, axpby
+
+
+def _exchange_case(rank, world):
+    import torch.nn.functional as F
+    from speech_transcript_embeddings_amd.train import EmbeddingExchange
+    _exchange_stand_ins()
+    B, P, tau, lam = 3, 8, 0.1, 0.7
+
+    def emb(r):
+        g = torch.Generator().manual_seed(500 + r)
+        return [F.normalize(torch.randn(B, P, generator=g), dim=1) for _ in range(3)]  # a, tpos, tneg
+    a, tp, tn = emb(rank)
+    tn_all = torch.cat([tp, tn]).contiguous()
+    loss = torch.tensor([0.25 + rank])
+    ex = EmbeddingExchange(tau, in_batch_weight=lam)
+    ex.start(a, tn_all)
+    # in-batch term (its own loss accumulator and cotangents, zero-initialised)
+    lterm = torch.zeros(1)
+    dan, dtp = torch.zeros(B, P), torch.zeros(B, P)
+    ex.in_batch(a, None, lterm, dan, dtp)
+    ex.finish(loss)
+    out = {}
+    S = ex.last_S
+    NB = world * B
+    i = torch.arange(NB)
+    local_sp, local_sn = (a * tp).sum(1), (a * tn).sum(1)
+    out["diag_ok"] = bool(torch.allclose(S[i, i][rank * B:(rank + 1) * B], local_sp, atol=1e-6) and
+                          torch.allclose(S[i, NB + i][rank * B:(rank + 1) * B], local_sn, atol=1e-6))
+    # metrics over the global batch, the reference's formulas (ref :1120-1161)
+    E = [emb(r) for r in range(world)]
+    A_g = torch.cat([e[0] for e in E])
+    Tp_g, Tn_g = torch.cat([e[1] for e in E]), torch.cat([e[2] for e in E])
+    sp_g, sn_g = (A_g * Tp_g).sum(1), (A_g * Tn_g).sum(1)
+    m = ex.epoch_metrics()
+    want = {"clean_similarity": torch.sigmoid(sp_g / tau).mean().item(),
+            "corrupt_similarity": torch.sigmoid(sn_g / tau).mean().item(),
+            "pair_accuracy": (sp_g > sn_g).double().mean().item(),
+            "in_batch_top1": ((A_g @ Tp_g.t()).argmax(1) == torch.arange(NB)).double().mean().item(),
+            "loss": sum(0.25 + r for r in range(world)) / world}
+    out["metrics_ok"] = all(abs(m[k] - v) < 1e-6 for k, v in want.items()) and m["samples"] == NB
+    # in-batch term vs autograd over the global batch: rank r's term is lam/B Σ_{i in r} CE_i and
+    # its backward cotangents must be d(Σ_r L_r)/d(its own a, tpos) (GradSync then averages)
+    Ag = A_g.clone().requires_grad_()
+    Tg = Tp_g.clone().requires_grad_()
+    lg = Ag @ Tg.t() / tau
+    terms = [lam / B * F.cross_entropy(lg[r * B:(r + 1) * B], torch.arange(r * B, (r + 1) * B), reduction="sum")
+             for r in range(world)]
+    sum(terms).backward()
+    out["inbatch_loss_err"] = abs(lterm.item() - terms[rank].item())
+    sl = slice(rank * B, (rank + 1) * B)
+    out["inbatch_grad_err"] = max((dan - Ag.grad[sl]).abs().max().item(), (dtp - Tg.grad[sl]).abs().max().item())
+    return out
 
 
 def _worker(rank, world, port, q):
@@ -127,15 +225,24 @@ def _worker(rank, world, port, q):
         flat /= world
         full = grads(slice(0, B))
         out["dp_rel"] = ((flat - full).norm() / full.norm()).item()
-        # 3. embedding all-gather for global metrics
-        ts = TrainStep.__new__(TrainStep)
-        ts.last = {}
-        an = torch.full((3, 4), float(rank))
-        tn = torch.full((6, 4), float(10 + rank))
-        ts._gather_metrics(an, tn)
-        ga, gt = ts.last["global_emb"]
-        out["gather_ok"] = all(torch.equal(ga[r], torch.full((3, 4), float(r))) for r in range(world)) and \
-            all(torch.equal(gt[r], torch.full((6, 4), float(10 + r))) for r in range(world))
+        # 3. EmbeddingExchange: global similarity matrix, metrics, optional in-batch InfoNCE
+        out.update(_exchange_case(rank, world))
+        # layerdrop seed: identical draws on every rank
+        from speech_transcript_embeddings_amd.train import TrainStep as _TS
+        ts = _TS.__new__(_TS)
+
+        class _M:
+            class engine:
+                layerdrop_gen = None
+
+            class store:
+                device = torch.device("cpu")
+        ts.model = _M
+        ts._sync_layerdrop_seed()
+        draws = torch.rand(8, generator=_M.engine.layerdrop_gen)
+        alld = [torch.empty_like(draws) for _ in range(world)]
+        dist.all_gather(alld, draws)
+        out["layerdrop_same"] = all(torch.equal(alld[0], d) for d in alld)
         # 4. per-rank data shards differ (weak scaling: every rank its own local batch)
         wav, lens, ids, *_ = synthetic_batch(2, 4000, 8, device="cpu", rank=rank)
         allw = [torch.empty_like(wav) for _ in range(world)]
@@ -164,6 +271,8 @@ def test_data_parallel_gloo_world2():
     for r, out in res.items():
         assert out["sync_err"] < 1e-6 and out["tail_ok"], (r, out["sync_err"])
         assert out["dp_rel"] < 1e-5, (r, out["dp_rel"])
-        assert out["gather_ok"], r
+        assert out["diag_ok"] and out["metrics_ok"], (r, out)
+        assert out["inbatch_loss_err"] < 1e-5 and out["inbatch_grad_err"] < 1e-5, (r, out)
+        assert out["layerdrop_same"], r
         assert out["shards_differ"], r
 

@@ -32,6 +32,23 @@ def test_fbank_oracle_collate_matches_reference(fb):
     np.testing.assert_allclose(feats, fb["batch_feats"], atol=2e-4, rtol=0)
 
 
+def test_fbank_oracle_config_size_clips():
+    """10 s / 30 s / odd-F / zero-segment-in-loud / silent clips (tests/golden/fbank_cases.py)
+    against the reference extractor's outputs (fbank_golden_long.npz); measured <= 1.0e-4."""
+    import sys
+    sys.path.insert(0, str(GOLDEN))
+    from fbank_cases import LONG_CASES, long_case_wave
+    z = np.load(GOLDEN / "fbank_golden_long.npz")
+    items = []
+    for c, _, _ in LONG_CASES:
+        feats, mask = fbank_ref.extract(long_case_wave(c), padding_value=1.0)
+        np.testing.assert_array_equal(mask, z[f"{c}_mask"])
+        np.testing.assert_allclose(feats, z[f"{c}_feats"], atol=2e-4, rtol=0, err_msg=c)
+        items.append(feats)
+    _, bmask = fbank_ref.collate(items)
+    np.testing.assert_array_equal(bmask, z["batch_mask"])
+
+
 def test_num_stacked_frames_survey_values():
     assert fbank_ref.num_stacked_frames(32000) == 99
     assert fbank_ref.num_stacked_frames(160000) == 499
