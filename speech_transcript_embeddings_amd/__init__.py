@@ -6,4 +6,6 @@ GPU fbank -> w2v-bert Conformer + XLM-R encoders -> pooling / projection /
 cross-modal heads -> AlignmentAwareInfoNCE -> backward -> clip -> AdamW, with
 every hot op a hand-written HIP kernel in libste.so (include/ste.h).
 """
-__version__ = "0.1.0"
+__version__ = "0.2.0"
+
+from . import torch_ops  # noqa: E402,F401  (torch.ops.ste.* custom operators)

@@ -719,6 +719,136 @@ class Engine:
         self._pool_bwd("text_pooling", hs["tpool"], dtpooled, dth, nb, L)
         self._pool_bwd("audio_pooling", hs["apool"], dapooled, dah, ab, T)
 
+    # ------------------------------------ standalone cross-modal attention (public API)
+    def _mask32(self, mask_i64, n):
+        m = self._e(n, dtype=torch.int32)
+        _lib.call("ste_mask_i64_to_f32", mask_i64.contiguous().data_ptr(), None, m.data_ptr(), n, _lib.stream_ptr())
+        return m
+
+    def cross_forward(self, tproj, th, tmask, aproj, ah, amask, train, seed):
+        """apply_cross_modal_attention (ref:643-682) for one call: text [b,P] + hidden [b,L,Ht],
+        audio [b,P] + hidden [b,T,Ha] -> (text_fused, audio_fused) [b,P] fp32 and the saved
+        context.  The fused training step shares one audio K/V between the pos and neg calls
+        (heads_forward); this is the reference's per-call form behind the public method."""
+        s = self.s
+        m = self.m
+        b, L, Ht = th.shape
+        T, Ha = ah.shape[1], ah.shape[2]
+        P = m.projection_dim
+        nh = m.xattn_heads
+        p_x = m.dropout if train else 0.0
+        thb = ops.cast_bf16(th.contiguous(), self._e(b * L, Ht, dtype=BF16))
+        ahb = ops.cast_bf16(ah.contiguous(), self._e(b * T, Ha, dtype=BF16))
+        tprojb = ops.cast_bf16(tproj.contiguous(), self._e(b, P, dtype=BF16))
+        aprojb = ops.cast_bf16(aproj.contiguous(), self._e(b, P, dtype=BF16))
+        tm32 = self._mask32(tmask, b * L) if tmask is not None else None
+        am32 = self._mask32(amask, b * T) if amask is not None else None
+        # text -> audio
+        aseqb = ops.linear(ahb, s.w("audio_seq_to_projection.weight"), s.p("audio_seq_to_projection.bias"),
+                           out_bf16=True)
+        kva = ops.linear(aseqb, s.fused("text_to_audio_attention.key.weight", 2, "w"),
+                         s.fused("text_to_audio_attention.key.bias", 2, "p"), out_bf16=True)
+        qt = ops.linear(tprojb, s.w("text_to_audio_attention.query.weight"), s.p("text_to_audio_attention.query.bias"))
+        probs_t, att_t = self._e(b * nh * T), self._e(b, P)
+        seed_t, seed_a = _site_seed(seed, 1), _site_seed(seed, 2)
+        ops.xattn1_fwd(qt, kva[:, :P], kva[:, P:], am32, b, T, nh, probs_t, att_t, drop_p=p_x, seed=seed_t)
+        att_tb = ops.cast_bf16(att_t, self._e(b, P, dtype=BF16))
+        tcat = self._e(b, 2 * P, dtype=BF16)
+        ops.linear(att_tb, s.w("text_to_audio_attention.out_proj.weight"), s.p("text_to_audio_attention.out_proj.bias"),
+                   out=tcat[:, P:])
+        _copy_bf16(tprojb, tcat[:, :P])
+        # audio -> text
+        tseqb = ops.linear(thb, s.w("text_seq_to_projection.weight"), s.p("text_seq_to_projection.bias"),
+                           out_bf16=True)
+        kvt = ops.linear(tseqb, s.fused("audio_to_text_attention.key.weight", 2, "w"),
+                         s.fused("audio_to_text_attention.key.bias", 2, "p"), out_bf16=True)
+        qa = ops.linear(aprojb, s.w("audio_to_text_attention.query.weight"), s.p("audio_to_text_attention.query.bias"))
+        probs_a, att_a = self._e(b * nh * L), self._e(b, P)
+        ops.xattn1_fwd(qa, kvt[:, :P], kvt[:, P:], tm32, b, L, nh, probs_a, att_a, drop_p=p_x, seed=seed_a)
+        att_ab = ops.cast_bf16(att_a, self._e(b, P, dtype=BF16))
+        acat = self._e(b, 2 * P, dtype=BF16)
+        ops.linear(att_ab, s.w("audio_to_text_attention.out_proj.weight"), s.p("audio_to_text_attention.out_proj.bias"),
+                   out=acat[:, P:])
+        _copy_bf16(aprojb, acat[:, :P])
+        # fusion Linear + LN
+        yt = ops.linear(tcat, s.w("text_fusion.0.weight"), s.p("text_fusion.0.bias"))
+        tfused = self._e(b, P)
+        st_t = self._ln(yt, "text_fusion.1", 1e-5, y=tfused)
+        ya = ops.linear(acat, s.w("audio_fusion.0.weight"), s.p("audio_fusion.0.bias"))
+        afused = self._e(b, P)
+        st_a = self._ln(ya, "audio_fusion.1", 1e-5, y=afused)
+        sv = dict(b=b, L=L, T=T, thb=thb, ahb=ahb, tprojb=tprojb, aprojb=aprojb, aseqb=aseqb, kva=kva, qt=qt,
+                  probs_t=probs_t, att_tb=att_tb, seed_t=seed_t, tseqb=tseqb, kvt=kvt, qa=qa, probs_a=probs_a,
+                  att_ab=att_ab, seed_a=seed_a, p_x=p_x, tcat=tcat, acat=acat, yt=yt, st_t=st_t, ya=ya, st_a=st_a)
+        return tfused, afused, sv
+
+    def cross_backward(self, sv, d_tf, d_af):
+        """-> (d text_projected [b,P], d text_hidden [b*L,Ht], d audio_projected [b,P],
+        d audio_hidden [b*T,Ha]) fp32; parameter gradients += into the flat buffer."""
+        s = self.s
+        m = self.m
+        b, L, T = sv["b"], sv["L"], sv["T"]
+        P = m.projection_dim
+        nh = m.xattn_heads
+        Ht, Ha = sv["thb"].shape[1], sv["ahb"].shape[1]
+        d_tproj, d_aproj = self._z(b, P), self._z(b, P)
+        dth, dah = self._z(b * L, Ht), self._z(b * T, Ha)
+        dyt = self._e(b, P, dtype=BF16)
+        self._ln_bwd(d_tf.contiguous(), sv["yt"], sv["st_t"], "text_fusion.1", dxb=dyt, dsum=s.g("text_fusion.0.bias"))
+        dtcat = ops.linear_dx(dyt, s.w("text_fusion.0.weight"))
+        self._dw(dyt, sv["tcat"], "text_fusion.0.weight")
+        dya = self._e(b, P, dtype=BF16)
+        self._ln_bwd(d_af.contiguous(), sv["ya"], sv["st_a"], "audio_fusion.1", dxb=dya, dsum=s.g("audio_fusion.0.bias"))
+        dacat = ops.linear_dx(dya, s.w("audio_fusion.0.weight"))
+        self._dw(dya, sv["acat"], "audio_fusion.0.weight")
+        _add_(d_tproj, dtcat[:, :P])
+        _add_(d_aproj, dacat[:, :P])
+        # text -> audio
+        datt = dtcat[:, P:].contiguous()
+        dattb = ops.cast_bf16(datt, self._e(b, P, dtype=BF16))
+        dq_in = ops.linear_dx(dattb, s.w("text_to_audio_attention.out_proj.weight"))
+        self._dw(dattb, sv["att_tb"], "text_to_audio_attention.out_proj.weight")
+        self._db(datt, "text_to_audio_attention.out_proj.bias")
+        dqt = self._e(b, P)
+        dkv = self._z(b * T, 2 * P)
+        ops.xattn1_bwd(sv["qt"], sv["kva"][:, :P], sv["kva"][:, P:], sv["probs_t"], dq_in, b, T, nh, dqt, dkv[:, :P],
+                       dkv[:, P:], drop_p=sv["p_x"], seed=sv["seed_t"])
+        dqtb = ops.cast_bf16(dqt, self._e(b, P, dtype=BF16))
+        ops.linear_dx(dqtb, s.w("text_to_audio_attention.query.weight"), out=d_tproj, beta=1.0)
+        self._dw(dqtb, sv["tprojb"], "text_to_audio_attention.query.weight")
+        self._db(dqt, "text_to_audio_attention.query.bias")
+        dkvb = ops.cast_bf16(dkv, self._e(b * T, 2 * P, dtype=BF16))
+        daseq = self._dx(dkvb, "text_to_audio_attention.key.weight", 2)
+        self._dw(dkvb, sv["aseqb"], "text_to_audio_attention.key.weight", fused=2)
+        self._db(dkv, "text_to_audio_attention.key.bias", fused=2)
+        daseqb = ops.cast_bf16(daseq, self._e(b * T, P, dtype=BF16))
+        self._dx(daseqb, "audio_seq_to_projection.weight", out=dah, beta=1.0)
+        self._dw(daseqb, sv["ahb"], "audio_seq_to_projection.weight")
+        self._db(daseq, "audio_seq_to_projection.bias")
+        # audio -> text
+        datta = dacat[:, P:].contiguous()
+        dattab = ops.cast_bf16(datta, self._e(b, P, dtype=BF16))
+        dqa_in = ops.linear_dx(dattab, s.w("audio_to_text_attention.out_proj.weight"))
+        self._dw(dattab, sv["att_ab"], "audio_to_text_attention.out_proj.weight")
+        self._db(datta, "audio_to_text_attention.out_proj.bias")
+        dqa = self._e(b, P)
+        dkvt = self._z(b * L, 2 * P)
+        ops.xattn1_bwd(sv["qa"], sv["kvt"][:, :P], sv["kvt"][:, P:], sv["probs_a"], dqa_in, b, L, nh, dqa,
+                       dkvt[:, :P], dkvt[:, P:], drop_p=sv["p_x"], seed=sv["seed_a"])
+        dqab = ops.cast_bf16(dqa, self._e(b, P, dtype=BF16))
+        ops.linear_dx(dqab, s.w("audio_to_text_attention.query.weight"), out=d_aproj, beta=1.0)
+        self._dw(dqab, sv["aprojb"], "audio_to_text_attention.query.weight")
+        self._db(dqa, "audio_to_text_attention.query.bias")
+        dkvtb = ops.cast_bf16(dkvt, self._e(b * L, 2 * P, dtype=BF16))
+        dtseq = ops.linear_dx(dkvtb, s.fused("audio_to_text_attention.key.weight", 2, "w"))
+        self._dw(dkvtb, sv["tseqb"], "audio_to_text_attention.key.weight", fused=2)
+        self._db(dkvt, "audio_to_text_attention.key.bias", fused=2)
+        dtseqb = ops.cast_bf16(dtseq, self._e(b * L, P, dtype=BF16))
+        ops.linear_dx(dtseqb, s.w("text_seq_to_projection.weight"), out=dth, beta=1.0)
+        self._dw(dtseqb, sv["thb"], "text_seq_to_projection.weight")
+        self._db(dtseq, "text_seq_to_projection.bias")
+        return d_tproj, dth, d_aproj, dah
+
     # ------------------------------------------------------- word alignment
     def _align_fwd(self, th, thb_pos, ahb, b, L, T, ctx, train, seed, hs):
         from .align import align_forward

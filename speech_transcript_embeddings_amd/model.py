@@ -18,7 +18,7 @@ import logging
 import torch
 from torch import nn
 
-from . import ops
+from . import ops, torch_ops  # noqa: F401  (registers the ste:: custom ops)
 from .engine import Engine
 from .modules import (AttentivePooling, AudioConfig, AudioEncoder, CrossModalAttention, EnhancedProjection,
                       TextConfig, TextEncoder, WordLevelAlignmentModule)
@@ -202,33 +202,140 @@ class EnhancedAudioTextModel(nn.Module):
         self.last_alignment_scores = outs[3] if self.use_word_alignment else None
         return tpn, tnn, an
 
-    # the sub-steps of the reference API, forward-only (inference utilities)
-    @torch.no_grad()
+    # the sub-steps of the reference API (compute_pos_neg_embeddings' building blocks).  Each is
+    # differentiable: one autograd node whose backward runs the engine's HIP backward for that
+    # block and accumulates parameter gradients into the flat buffer (.grad views), so code
+    # written against the reference's methods (ref :508-563) trains unmodified.  Under no_grad
+    # they run forward-only without saved activations.
     def encode_text(self, input_ids, attention_mask=None):
-        """ref:567-585 (forward only): (projection [B,P], last_hidden_state [B,L,H])."""
-        e = self.engine
-        ctx = {}
+        """ref:567-585: (projection [B,P], last_hidden_state [B,L,H])."""
         if attention_mask is None:
             attention_mask = torch.ones_like(input_ids)
-        h, hb = e.text_forward(input_ids.contiguous(), attention_mask.contiguous(), False, 0, ctx, save=False)
-        sv = {}
-        B, L = input_ids.shape
-        _, pb = e._pool_fwd("text_pooling", hb, ctx["t_mask32"], B, L, sv)
-        proj = e._proj_fwd("text_projection", pb, B, False, 0, {})
-        return proj, h.view(B, L, -1)
+        ids, mask = input_ids.contiguous(), attention_mask.contiguous()
+        if not torch.is_grad_enabled():
+            return self._encode_nograd("text", ids, mask)
+        return _EncodeFn.apply(self, "text", ids, mask, self.store.master[:1].detach().requires_grad_(True))
 
-    @torch.no_grad()
     def encode_audio(self, input_values, attention_mask=None):
-        """ref:587-641 (forward only): (projection [B,P], last_hidden_state [B,T,H])."""
-        e = self.engine
-        ctx = {}
+        """ref:587-641: (projection [B,P], last_hidden_state [B,T,H])."""
         B, T, _ = input_values.shape
         if attention_mask is None:
             attention_mask = torch.ones(B, T, dtype=torch.int64, device=input_values.device)
-        h, hb = e.audio_forward(input_values.contiguous(), attention_mask.contiguous(), False, 0, ctx, save=False)
-        _, pb = e._pool_fwd("audio_pooling", hb, ctx["a_mask32"], B, T, {})
-        proj = e._proj_fwd("audio_projection", pb, B, False, 0, {})
-        return proj, h.view(B, T, -1)
+        x, mask = input_values.contiguous(), attention_mask.contiguous()
+        if not torch.is_grad_enabled():
+            return self._encode_nograd("audio", x, mask)
+        return _EncodeFn.apply(self, "audio", x, mask, self.store.master[:1].detach().requires_grad_(True))
+
+    def apply_cross_modal_attention(self, text_projected, text_hidden, text_mask, audio_projected, audio_hidden,
+                                    audio_mask):
+        """ref:643-682: (text_fused [B,P], audio_fused [B,P]); identity without use_cross_modal."""
+        if not self.use_cross_modal:
+            return text_projected, audio_projected
+        self.store.sync_shadow()
+        if not torch.is_grad_enabled():
+            tf, af, _ = self.engine.cross_forward(text_projected, text_hidden, text_mask, audio_projected, audio_hidden,
+                                                  audio_mask, self.training, _call_seed(self.training))
+            return tf, af
+        return _CrossFn.apply(self, text_projected, text_hidden, text_mask, audio_projected, audio_hidden, audio_mask,
+                              self.store.master[:1].detach().requires_grad_(True))
+
+    def _encode_nograd(self, kind, x, mask):
+        self.store.sync_shadow()
+        e = self.engine
+        ctx = {}
+        if kind == "text":
+            B, L = x.shape
+            h, hb = e.text_forward(x, mask, self.training, _call_seed(self.training), ctx, save=False)
+            m32, pool, proj = ctx["t_mask32"], "text_pooling", "text_projection"
+        else:
+            B, L = x.shape[:2]
+            h, hb = e.audio_forward(x, mask, self.training, _call_seed(self.training), ctx, save=False)
+            m32, pool, proj = ctx["a_mask32"], "audio_pooling", "audio_projection"
+        _, pb = e._pool_fwd(pool, hb, m32, B, L, {})
+        out = e._proj_fwd(proj, pb, B, self.training, _call_seed(self.training), {})
+        return out, h.view(B, L, -1)
+
+
+def _call_seed(train: bool) -> int:
+    """Dropout seed of one API call (counter-based dropout, recomputed in backward)."""
+    return int(torch.randint(0, 2**62, (1,)).item()) if train else 0
+
+
+class _EncodeFn(torch.autograd.Function):
+    """encode_text / encode_audio as one autograd node: encoder -> pooling -> projection forward
+    on the engine (activations saved), backward = projection, pooling and encoder backward."""
+
+    @staticmethod
+    def forward(fctx, model, kind, x, mask, dummy):
+        model.store.sync_shadow()
+        e = model.engine
+        ctx = {}
+        train = model.training
+        seed = _call_seed(train)
+        if kind == "text":
+            B, L = x.shape
+            h, hb = e.text_forward(x, mask, train, seed, ctx, save=True)
+            m32, pool, proj = ctx["t_mask32"], "text_pooling", "text_projection"
+        else:
+            B, L = x.shape[:2]
+            h, hb = e.audio_forward(x, mask, train, seed, ctx, save=True)
+            m32, pool, proj = ctx["a_mask32"], "audio_pooling", "audio_projection"
+        sv_pool, sv_proj = {}, {}
+        _, pb = e._pool_fwd(pool, hb, m32, B, L, sv_pool)
+        out = e._proj_fwd(proj, pb, B, train, _site(seed), sv_proj)
+        fctx.model, fctx.kind, fctx.ctx = model, kind, ctx
+        fctx.saved = (sv_pool, sv_proj, B, L, h.shape[-1], pool, proj)
+        return out, h.view(B, L, -1)
+
+    @staticmethod
+    def backward(fctx, d_out, d_hidden):
+        model, e = fctx.model, fctx.model.engine
+        sv_pool, sv_proj, B, L, H, pool, proj = fctx.saved
+        model.store.attach_grads()
+        if d_hidden is not None:
+            dh = d_hidden.reshape(B * L, H).float().contiguous().clone()
+        else:
+            dh = torch.zeros(B * L, H, device=model.store.device)
+        if d_out is not None:
+            dpooled = torch.zeros(B, H, device=model.store.device)
+            e._proj_bwd(proj, sv_proj, d_out.float().contiguous(), dpooled)
+            e._pool_bwd(pool, sv_pool, dpooled, dh, B, L)
+        if fctx.kind == "text":
+            e.text_backward(dh, fctx.ctx)
+        else:
+            e.audio_backward(dh, fctx.ctx)
+        fctx.ctx = fctx.saved = None
+        return None, None, None, None, None
+
+
+class _CrossFn(torch.autograd.Function):
+    """apply_cross_modal_attention as one autograd node (engine.cross_forward / cross_backward)."""
+
+    @staticmethod
+    def forward(fctx, model, tproj, th, tmask, aproj, ah, amask, dummy):
+        tf, af, sv = model.engine.cross_forward(tproj, th, tmask, aproj, ah, amask, model.training,
+                                                _call_seed(model.training))
+        fctx.model, fctx.sv = model, sv
+        fctx.shapes = (th.shape, ah.shape)
+        return tf, af
+
+    @staticmethod
+    def backward(fctx, d_tf, d_af):
+        model = fctx.model
+        sv = fctx.sv
+        b = sv["b"]
+        P = model.projection_dim
+        z = lambda: torch.zeros(b, P, device=model.store.device)  # noqa: E731
+        model.store.attach_grads()
+        d_tproj, dth, d_aproj, dah = model.engine.cross_backward(sv, d_tf if d_tf is not None else z(),
+                                                                 d_af if d_af is not None else z())
+        fctx.sv = None
+        ts, as_ = fctx.shapes
+        return None, d_tproj, dth.view(ts), None, d_aproj, dah.view(as_), None, None
+
+
+def _site(seed: int) -> int:
+    return (seed * 0x9E3779B97F4A7C15 + 1) & ((1 << 62) - 1)
 
 
 def _l2_normalise(tf_p, tf_n, af):
@@ -286,43 +393,6 @@ class AlignmentAwareInfoNCE(nn.Module):
         self.corrupt_gamma = corrupt_gamma
 
     def forward(self, s_pos, s_neg, alignment_scores=None):
-        return _LossFn.apply(s_pos, s_neg, alignment_scores, self)
-
-
-class _LossFn(torch.autograd.Function):
-    @staticmethod
-    def forward(fctx, s_pos, s_neg, align, mod):
-        B = s_pos.shape[0]
-        S = torch.stack([s_pos, s_neg], 1).contiguous()  # [B, 2]: diag of S[:, :1] trick -> use ldS=2
-        # pair_loss reads s_pos at S[i*ldS + i] and s_neg at S[i*ldS + off + i]; with ldS=1, off=B
-        flat = torch.cat([s_pos, s_neg]).contiguous().view(1, 2 * B)
-        sp = torch.empty(B, device=s_pos.device)
-        sn = torch.empty(B, device=s_pos.device)
-        loss = torch.empty(1, device=s_pos.device)
-        L = align.shape[1] if align is not None else 0
-        al = align.contiguous().float() if align is not None else None
-        _pair_loss_1d(flat, B, al, L, mod, sp, sn, loss)
-        fctx.save_for_backward(sp, sn, al if al is not None else torch.empty(0, device=s_pos.device))
-        fctx.mod, fctx.has_align, fctx.L = mod, align is not None, L
-        del S
-        return loss[0]
-
-    @staticmethod
-    def backward(fctx, dloss):
-        sp, sn, al = fctx.saved_tensors
-        mod = fctx.mod
-        B = sp.shape[0]
-        dsp, dsn = torch.empty_like(sp), torch.empty_like(sn)
-        dal = torch.empty(B, fctx.L, device=sp.device) if fctx.has_align else None
-        gs = dloss.reshape(1).float().contiguous()
-        ops.pair_loss_bwd(sp, sn, al if fctx.has_align else None, B, fctx.L, mod.temperature, mod.alignment_weight,
-                          mod.corrupt_gamma, gs, dsp, dsn, dal)
-        return dsp, dsn, dal, None
-
-
-def _pair_loss_1d(flat, B, al, L, mod, sp, sn, loss):
-    # ste_pair_loss_fwd indexes S[i*ldS + i] / S[i*ldS + off_neg + i]: with ldS = 0 that is flat[i] / flat[B + i]
-    from . import _lib
-    _lib.call("ste_pair_loss_fwd", flat.data_ptr(), 0, B, None if al is None else al.data_ptr(), B, L,
-              float(mod.temperature), float(mod.alignment_weight), float(mod.corrupt_gamma), sp.data_ptr(),
-              sn.data_ptr(), loss.data_ptr(), _lib.stream_ptr())
+        """The ste::pair_loss custom op (torch_ops.py): pair_loss_fwd / pair_loss_bwd kernels."""
+        return torch.ops.ste.pair_loss(s_pos, s_neg, alignment_scores, float(self.temperature),
+                                       float(self.alignment_weight), float(self.corrupt_gamma))
