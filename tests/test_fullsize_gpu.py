@@ -1,7 +1,11 @@
-"""Full-size parity (BASELINE configs c2/c4 dimensions: w2v-bert-2.0 24 x 1024 Conformer,
-XLM-R-base 12 x 768 text encoder, 10 s @ 16 kHz clips, 64-token transcripts): the HIP path
-against the oracle's CPU fp32 autograd on the SAME weights (the GPU model's own random init,
-copied to the oracle), eval mode, batch 2.
+"""Full-size parity at every BASELINE config's shapes (w2v-bert-2.0 24 x 1024 Conformer,
+XLM-R-base 12 x 768 text encoder): the HIP path against the oracle's CPU fp32 autograd on the
+SAME weights (the GPU model's own random init, copied to the oracle), eval mode.
+  c1  B=4, 2 s clips, 16-token transcripts, 3+3 unfrozen
+  c2  B=2, 10 s clips, 64 tokens, 3+3 unfrozen          (c3 = c2 shapes per GPU)
+  c4  B=2, 10 s, 64 tokens, 5+5 unfrozen + alignment head
+  c5  B=1, 30 s clips (T = 1499), 64 tokens, every encoder layer trainable (freeze_encoders
+      "none"), bf16 GEMMs and, separately, the MX-fp8 Conformer forward GEMMs (fp8_gemm=True)
 
 Checked: the three normalised embeddings and alignment scores (bf16 bound of north_star:
 1e-2 relative), and the gradient of every parameter that receives one, for random cotangents
@@ -27,23 +31,30 @@ from oracle import ref_model as R
 
 pytestmark = pytest.mark.gpu
 
+CONFIGS = {  # name: (batch, samples, tokens, unfreeze k, align, freeze_encoders, fp8)
+    "c1": (4, 32000, 16, 3, False, "partial", False),
+    "c2": (2, 160000, 64, 3, False, "partial", False),
+    "c4": (2, 160000, 64, 5, True, "partial", False),
+    "c5": (1, 480000, 64, 3, False, "none", False),
+    "c5_fp8": (1, 480000, 64, 3, False, "none", True),
+}
+
 
 def _rel(a, b):
     a, b = a.detach().double().cpu(), b.detach().double().cpu()
     return ((a - b).norm() / (b.norm() + 1e-30)).item()
 
 
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("align", [False, True])
-def test_full_size_vs_oracle(align):
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cname", list(CONFIGS))
+def test_full_size_vs_oracle(cname):
     from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
     from speech_transcript_embeddings_amd.train import synthetic_batch
-    k = 5 if align else 3
+    B, N, L, k, align, freeze, fp8 = CONFIGS[cname]
     torch.manual_seed(0)
     model = EnhancedAudioTextModel(use_word_alignment=align, text_layers_to_unfreeze=k, audio_layers_to_unfreeze=k,
-                                   device="cuda")
+                                   freeze_encoders=freeze, device="cuda", fp8_gemm=fp8)
     model.eval()
-    B, N, L = 2, 160000, 64
     wav, lens, ids, mask, neg, nmask = synthetic_batch(B, N, L, device="cuda", seed=3)
     from speech_transcript_embeddings_amd import ops
     T = ((1 + (N - 400) // 160) + 1) // 2
@@ -71,9 +82,13 @@ def test_full_size_vs_oracle(align):
     torch.autograd.backward(outs, [c.cuda() for c in cots])
     torch.cuda.synchronize()
 
-    cfg = R.ModelCfg(use_word_alignment=align, text_layers_to_unfreeze=k, audio_layers_to_unfreeze=k)
+    if freeze == "none":
+        cfg = R.ModelCfg(use_word_alignment=align, text_layers_to_unfreeze=12, audio_layers_to_unfreeze=24)
+    else:
+        cfg = R.ModelCfg(use_word_alignment=align, text_layers_to_unfreeze=k, audio_layers_to_unfreeze=k)
     names = [n for n, _ in model.named_parameters()]
     trainable = R.trainable_names(names, cfg)
+    assert trainable == {n for n, p_ in model.named_parameters() if p_.requires_grad}
     sd = {n: t.detach().float().cpu() for n, t in model.state_dict().items()}
     p = {n: sd[n].clone().requires_grad_(n in trainable) for n in names}
     bc = {kk: v.cpu() for kk, v in batch.items()}
@@ -105,8 +120,12 @@ def test_full_size_vs_oracle(align):
             R.F = R_F
         assert flips < 0.01 * gate.numel(), flips
     ref = [tpn, tnn, an] + ([al] if align else [])
+    # fp8 bound (north_star states fp32 / bf16 only).  e4m3 keeps 3 mantissa bits, so
+    # every forward GEMM of the 24 Conformer layers carries a few-percent quantisation error; at
+    # full depth the embeddings land within 1e-1 of fp32 (measured 8.1 %; 4.4 % at mini depth)
+    out_tol = 1e-1 if fp8 else 1e-2
     for name, got, want in zip(["txt_pos", "txt_neg", "aud", "align"], outs, ref):
-        assert _rel(got, want) < 1e-2, (name, _rel(got, want))
+        assert _rel(got, want) < out_tol, (name, _rel(got, want))
     torch.autograd.backward(ref, cots)
     params = dict(model.named_parameters())
     errs = []
@@ -121,6 +140,11 @@ def test_full_size_vs_oracle(align):
     errs.sort(reverse=True)
     assert len(errs) > 50
     median = errs[len(errs) // 2][0]
-    print(f"grad rel err: worst {errs[:8]}, median {median:.2e}, n={len(errs)}, gate flips {flips}")
-    assert median < 1e-2, median
-    assert errs[0][0] < 3e-2, errs[:5]
+    print(f"[{cname}] grad rel err: worst {errs[:6]}, median {median:.2e}, n={len(errs)}, gate flips {flips}")
+    if fp8:
+        # elementwise vs fp32 with fp8-quantised forward activations (straight-through bf16
+        # backward): measured median 12 %, worst 26 % (bf16 c5: 0.7 % / 2.1 %)
+        assert median < 2e-1 and errs[0][0] < 4e-1, (median, errs[:5])
+    else:
+        assert median < 1e-2, median
+        assert errs[0][0] < 3e-2, errs[:5]
