@@ -3,6 +3,8 @@ committed summaries under profiles/.
 
   kernel stats  (same columns as rocprofv3 --stats kernel_stats.csv):
     python profiles/rocpd_tools.py stats gpurun_out/prof/run_results.db > profiles/rNN_bench_kernel_stats.csv
+  per-kernel means of SQ counters from --pmc passes (e.g. of profiles/attn_probe.py):
+    python profiles/rocpd_tools.py pmc gpurun_out/p1/run_results.db gpurun_out/p2/run_results.db
   per-launch HBM traffic from separate FETCH_SIZE / WRITE_SIZE passes of bench.py:
     python profiles/rocpd_tools.py traffic gpurun_out/pmc_fetch/run_results.db gpurun_out/pmc_write/run_results.db \
         > profiles/rNN_hbm_traffic.json
@@ -70,8 +72,28 @@ def traffic(fdb, wdb):
                      indent=1))
 
 
+def pmc(*dbs):
+    """Per-kernel mean of every collected counter (one row per kernel, one column per counter)
+    over all dispatches of one or more --pmc passes."""
+    acc = defaultdict(lambda: defaultdict(list))
+    for db in dbs:
+        c = sqlite3.connect(db)
+        rows = c.execute("select dispatch_id, kernel_name, counter_name, value from counters_collection").fetchall()
+        per = defaultdict(float)
+        names = {}
+        for d, k, cn, v in rows:
+            per[(d, cn)] += float(v)
+            names[d] = k
+        for (d, cn), v in per.items():
+            acc[short(names[d])][cn].append(v)
+    out = {k: {cn: round(sum(v) / len(v), 1) for cn, v in sorted(cs.items())} for k, cs in acc.items()}
+    print(json.dumps(out, indent=1))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2])
+    elif sys.argv[1] == "pmc":
+        pmc(*sys.argv[2:])
     else:
         traffic(sys.argv[2], sys.argv[3])

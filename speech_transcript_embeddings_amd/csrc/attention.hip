@@ -23,6 +23,10 @@
 #include "common.h"
 #include "../../include/ste.h"
 
+#ifndef STE_ABLATE
+#define STE_ABLATE 0   // timing-ablation builds only (profiles/attn_ablate.sh); 0 in the library
+#endif
+
 namespace {
 
 constexpr int HD = 64;
@@ -893,6 +897,253 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
   }
 }
 
+// ============================================== relative-key forward, v3 (audio self-attention)
+// Same block shape, K/V ring and hi/lo P split as v2, with the per-score vector work cut down
+// (rel2 measured ~17 VALU instructions per score, more than its MFMA time):
+//  * the relative term comes from a per-query-row BIAS TABLE built once per block: row q holds
+//    c2·Q_q·E[clamp(k - q) + left] for the 88 keys k in [ks - 4, ks + 84), ks = floor4(q - left),
+//    already clamped and scaled, so a lane's 4 consecutive keys read one aligned float4 (offset
+//    clamped into the table: keys before it are bin 0, keys after it the last bin).  Row stride
+//    92 floats keeps the 16 rows of a read on distinct banks;
+//  * every score is then one FMA (s·c2 + bias) before the max; out-of-band tiles use the row's
+//    constant edge bias; key masks / keys past T are applied only on tiles that have such keys;
+//  * the running max is rescaled lazily (only when some row of the group grew) and row sums stay
+//    per lane until the end.
+namespace rel3 {
+constexpr int WQ = 32, BQ = 128;
+constexpr int TW = 92;                     // bias-table row stride (floats); 92 mod 64 = 28
+constexpr int TKEYS = 88;                  // keys per row: [ks - 4, ks + 84)
+constexpr int KV = 2 * TILE;
+constexpr int MASK_OFF = 2 * KV;
+constexpr int TAB_OFF = MASK_OFF + 512;
+constexpr int FWD_LDS = TAB_OFF + 4 * WQ * TW * 4;   // 80,384 B: two blocks per CU
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+}  // namespace rel3
+
+__global__ __launch_bounds__(NT, 2) void attn_fwd_rel3_kernel(ste_attn_args a) {
+  using namespace rel3;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T = a.T, H = a.H;
+  const int ntile = (T + BQ - 1) / BQ;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = id % ntile, bh = id / ntile, h = bh % H, b = bh / H, bT = b * T;
+  const int left = a.rel_left, right = a.rel_right, nrel = left + right + 1;
+  const bf16* Qb = (const bf16*)a.q + h * HD;
+  const bf16* Kb = (const bf16*)a.k + h * HD;
+  const bf16* Vb = (const bf16*)a.v + h * HD;
+  const int qw = tile * BQ + w * WQ;
+  const float c2 = a.scale * LOG2E;
+
+  bf16x8 qf[2][2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int q = qw + 16 * gq + li;
+      qf[gq][s] = q < T ? *reinterpret_cast<const bf16x8*>(Qb + (int64_t)(bT + q) * a.ldq + 32 * s + 8 * g) : bf16x8{};
+    }
+  // ---- bias table: E staged over the ring (free until tile 0), Q·Eᵀ on the MFMA, scattered
+  // into each row's clamped key window
+  float* tab = reinterpret_cast<float*>(sm + TAB_OFF) + w * WQ * TW;
+  stage_E(sm, (const bf16*)a.rel_E, nrel, NREL, tid);
+  __syncthreads();
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int q = qw + 16 * gq + li;
+    const int ks = (q - left) - ((q - left) & 3);
+    float* row = tab + (16 * gq + li) * TW;
+#pragma unroll
+    for (int jt = 0; jt < NREL / 16; ++jt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sm, jt * 16, s, lane), qf[gq][s], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = jt * 16 + 4 * g + r;
+        const float v = acc[r] * c2;
+        if (j == 0) {                              // keys <= q - left: idx 0 .. q - left - ks + 4
+          for (int i = 0; i <= q - left - ks + 4; ++i) row[i] = v;
+        } else if (j == nrel - 1) {                // keys >= q + right
+          for (int i = q + right - ks + 4; i < TKEYS; ++i) row[i] = v;
+        } else if (j < nrel - 1) {
+          row[j - left + q - ks + 4] = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  float blo[2], bhi[2];
+  int ksr[2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int q = qw + 16 * gq + li;
+    ksr[gq] = (q - left) - ((q - left) & 3);
+    blo[gq] = tab[(16 * gq + li) * TW];
+    bhi[gq] = tab[(16 * gq + li) * TW + TKEYS - 1];
+  }
+
+  char* sMask = sm + MASK_OFF;
+  const int nkt = (T + TK - 1) / TK;
+  const bool has_mask = a.key_mask != nullptr;
+  auto issue = [&](int kt) {
+    char* buf = sm + (kt & 1) * KV;
+    const int kb = kt * TK;
+    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w, lane);
+    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w + 1, lane);
+    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w, lane);
+    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w + 1, lane);
+    if (w == 0 && has_mask) glds_mask(a.key_mask, bT, kb, T, sMask + (kt & 1) * 256, lane);
+  };
+  issue(0);
+  if (nkt > 1) issue(1);
+  if (nkt > 1) {
+    if (w == 0 && has_mask) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  f32x4 o[2][4];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const char* tK = sm + (kt & 1) * KV;
+    const char* tV = tK + TILE;
+    const int* mk = reinterpret_cast<const int*>(sMask + (kt & 1) * 256);
+    const int kb = kt * TK;
+    bf16x8 kf[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) kf[t][ss] = frag_kc(tK, t * 16, ss, lane);
+    f32x4 s[2][4];
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s[gq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) s[gq][t] = mfma16(kf[t][ss], qf[gq][ss], s[gq][t]);
+      }
+    bf16x8 vf[4][2];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) vf[dt][u] = frag_tr_asm(tV, dt * 16, u, lane);
+    // keys past T or masked: this lane's 4 keys per t as additive fills (wave-uniform test)
+    const bool tail = kb + TK > T;
+    const bool masked_tile = has_mask && __ballot(mk[lane] == 0) != 0;
+    const bool fix = tail || masked_tile;
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq) {
+      const int q0g = qw + 16 * gq;
+      const bool all_lo = (kb + TK - 1) - q0g <= -left;
+      const bool all_hi = kb - (q0g + 15) >= right;
+      if (all_lo || all_hi) {
+        const float bc = all_lo ? blo[gq] : bhi[gq];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[gq][t][r] = fmaf(s[gq][t][r], c2, bc);
+      } else {
+        const float* row = tab + (16 * gq + li) * TW;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int off = min(max(kb + 16 * t + 4 * g - ksr[gq] + 4, 0), TKEYS - 4);
+          const f32x4 bt = *reinterpret_cast<const f32x4*>(row + off);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[gq][t][r] = fmaf(s[gq][t][r], c2, bt[r]);
+        }
+      }
+      if (fix) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int k0 = 16 * t + 4 * g;
+          int4 mw = has_mask ? *reinterpret_cast<const int4*>(mk + k0) : int4{1, 1, 1, 1};
+          const int mv[4] = {mw.x, mw.y, mw.z, mw.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float fill = (kb + k0 + r < T) ? NEG_MASK : -INFINITY;
+            s[gq][t][r] = (kb + k0 + r < T && mv[r] != 0) ? s[gq][t][r] : fill;
+          }
+        }
+      }
+      float tmax = fmaxf(fmaxf(fmaxf(s[gq][0][0], s[gq][0][1]), fmaxf(s[gq][0][2], s[gq][0][3])),
+                         fmaxf(fmaxf(s[gq][1][0], s[gq][1][1]), fmaxf(s[gq][1][2], s[gq][1][3])));
+      tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(s[gq][2][0], s[gq][2][1]), fmaxf(s[gq][2][2], s[gq][2][3])),
+                               fmaxf(fmaxf(s[gq][3][0], s[gq][3][1]), fmaxf(s[gq][3][2], s[gq][3][3]))));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      if (__ballot(tmax > m[gq]) != 0) {   // some row's max grew: rescale (alpha = 1 elsewhere)
+        const float mnew = fmaxf(m[gq], tmax);
+        const float alpha = __builtin_amdgcn_exp2f(m[gq] - mnew);
+        l[gq] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
+        m[gq] = mnew;
+      }
+      float psum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(s[gq][t][r] - m[gq]);
+          psum += pv;
+          s[gq][t][r] = pv;
+        }
+      l[gq] += psum;   // per-lane partial: reduced across the row's 4 lanes at the end
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16x8 pb = pack_acc(s[gq][2 * u], s[gq][2 * u + 1]);
+        const bf16x8 pl = pack_acc_lo(s[gq][2 * u], s[gq][2 * u + 1], pb);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pb, o[gq][dt]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pl, o[gq][dt]);
+      }
+    if (kt + 1 < nkt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (this wave's pieces)
+      __builtin_amdgcn_s_barrier();                     // ... every wave's, and tile kt fully read
+      if (kt + 2 < nkt) issue(kt + 2);
+    }
+  }
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    float lt = l[gq];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const int myq = qw + 16 * gq + li;
+    if (myq < T) {
+      const float inv_l = 1.0f / lt;
+      bf16* O = (bf16*)a.o + (int64_t)(bT + myq) * a.ldo + h * HD;
+      if (a.o_lo) {
+        bf16* Ol = (bf16*)a.o_lo + (int64_t)(bT + myq) * a.ldolo + h * HD;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          store_bf16x4_split(O + 16 * dt + 4 * g, Ol + 16 * dt + 4 * g, o[gq][dt] * inv_l);
+      } else {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) store_bf16x4(O + 16 * dt + 4 * g, o[gq][dt] * inv_l);
+      }
+      if (g == 0)
+        a.lse[(int64_t)(b * H + h) * T + myq] = m[gq] == NEG_MASK ? -INFINITY : (m[gq] + log2f(lt)) * LN2;
+    }
+  }
+}
+
 // ====================================== relative-key backward, v2: dQ (+ delta, + bins G)
 // 4 waves x 16 queries, K/V ring as in the forward.  delta = rowsum(dO*O) is computed here
 // from the wave's own dO/O fragments (no separate pass) and written for the dK/dV kernel.
@@ -1219,7 +1470,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel2_kernel(ste_attn_args 
     const bool blk_lo = (kb0 + KB - 1) - qb <= -left;
     const bool blk_hi = kb0 - (qb + TQ - 1) >= right;
     const bool blk_band = !(blk_lo || blk_hi);
-    {
+    if (!(STE_ABLATE & 1)) {
       bf16x8 qfr[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) qfr[s] = frag_kc(tQ, 16 * w, s, lane);
@@ -1238,7 +1489,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel2_kernel(ste_attn_args 
         }
       }
     }
-    __syncthreads();
+    if (!(STE_ABLATE & 1)) __syncthreads();
     // per-lane query vectors (queries 16n + 4g + r): -lse*log2e, delta, edge biases
     f32x4 nl2[4], dlt[4], lsev[4];
 #pragma unroll
@@ -1257,6 +1508,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel2_kernel(ste_attn_args 
         dp[n] = sc[n];
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
+          if (STE_ABLATE & 8) continue;
           sc[n] = mfma16(frag_kc(tQ, 16 * n, ss, lane), kf[gk][ss], sc[n]);
           dp[n] = mfma16(frag_kc(tD, 16 * n, ss, lane), vf[gk][ss], dp[n]);
         }
@@ -1269,7 +1521,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel2_kernel(ste_attn_args 
         for (int n = 0; n < 4; ++n) {
           const f32x4 eb = *reinterpret_cast<const f32x4*>(ev + 16 * n + 4 * g);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) sc[n][r] = __builtin_amdgcn_exp2f(fmaf(sc[n][r], c2, eb[r] + nl2[n][r]));
+          for (int r = 0; r < 4; ++r) sc[n][r] = (STE_ABLATE & 2) ? fmaf(sc[n][r], c2, eb[r] + nl2[n][r])
+                                                                  : __builtin_amdgcn_exp2f(fmaf(sc[n][r], c2, eb[r] + nl2[n][r]));
         }
       } else {
 #pragma unroll
@@ -1305,8 +1558,216 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel2_kernel(ste_attn_args 
         const bf16x8 pk = pack_acc(dp[2 * u], dp[2 * u + 1]);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
+          if (STE_ABLATE & 4) continue;
           dv[gk][dt] = mfma16(frag_tr(tD, dt * 16, u, lane), pv, dv[gk][dt]);
           dk[gk][dt] = mfma16(frag_tr(tQ, dt * 16, u, lane), pk, dk[gk][dt]);
+        }
+        if (STE_ABLATE & 4) { dv[gk][0] += pv[0]; dk[gk][0] += pk[0]; }
+      }
+    }
+    if (qt + 1 < nqt) {
+      if (!(STE_ABLATE & 16)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+      if (qt + 2 < nqt) issue(qt + 2);
+    }
+  }
+#pragma unroll
+  for (int gk = 0; gk < 2; ++gk) {
+    const int key = k0w + 16 * gk + li;
+    if (key < T) {
+      bf16* dK = (bf16*)a.dk + (int64_t)(bT + key) * a.lddk + h * HD;
+      bf16* dV = (bf16*)a.dv + (int64_t)(bT + key) * a.lddv + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        store_bf16x4(dK + 16 * dt + 4 * g, dk[gk][dt]);
+        store_bf16x4(dV + 16 * dt + 4 * g, dv[gk][dt]);
+      }
+    }
+  }
+}
+
+// v3 of the dK/dV kernel: the same algorithm as v2 with each Q/dO fragment (row and transposed)
+// read from LDS once per 32-query half and used for both key groups (v2 re-read them per key
+// group: LDS traffic equal to the MFMA time), transposed reads through the asm form (the
+// builtin makes hipcc drain the in-flight tile DMA at every read).
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args a) {
+  using namespace rel2;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T = a.T, H = a.H;
+  const int ntile = (T + KB - 1) / KB;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = id % ntile, bh = id / ntile, h = bh % H, b = bh / H, bT = b * T;
+  const int left = a.rel_left, right = a.rel_right, nrel = left + right + 1;
+  const bf16* Qb = (const bf16*)a.q + h * HD;
+  const bf16* Kb = (const bf16*)a.k + h * HD;
+  const bf16* Vb = (const bf16*)a.v + h * HD;
+  const bf16* dOb = (const bf16*)a.dout + h * HD;
+  const int kb0 = tile * KB, k0w = kb0 + w * 32;
+  const int64_t rowbase = (int64_t)(b * H + h) * T;
+  const float c2 = a.scale * LOG2E;
+
+  bf16x8 kf[2][2], vf[2][2];
+  bool kmask[2];
+#pragma unroll
+  for (int gk = 0; gk < 2; ++gk) {
+    const int key = k0w + 16 * gk + li;
+    const bool kv = key < T;
+    kmask[gk] = kv && a.key_mask != nullptr && a.key_mask[bT + key] == 0;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      kf[gk][s] = kv ? *reinterpret_cast<const bf16x8*>(Kb + (int64_t)(bT + key) * a.ldk + 32 * s + 8 * g) : bf16x8{};
+      vf[gk][s] = kv ? *reinterpret_cast<const bf16x8*>(Vb + (int64_t)(bT + key) * a.ldv + 32 * s + 8 * g) : bf16x8{};
+    }
+  }
+  const bool any_masked = __ballot(kmask[0] || kmask[1]) != 0;
+  char* sE = sm + KV_E_OFF;
+  float* qet = reinterpret_cast<float*>(sm + KV_QE_OFF);
+  float* elo = reinterpret_cast<float*>(sm + KV_EDGE_OFF);
+  float* ehi = elo + 64;
+  stage_E(sE, (const bf16*)a.rel_E, nrel, NREL, tid);
+
+  const int nqt = (T + TQ - 1) / TQ;
+  // wave w stages Q pieces 2w,2w+1 and dO pieces 2w,2w+1; wave 0 the lse words, wave 1 delta
+  auto issue = [&](int qt) {
+    char* buf = sm + (qt & 1) * QD;
+    const int qb = qt * TQ;
+    glds_tile_piece(Qb, a.ldq, bT, qb, T, buf, 2 * w, lane);
+    glds_tile_piece(Qb, a.ldq, bT, qb, T, buf, 2 * w + 1, lane);
+    glds_tile_piece(dOb, a.lddo, bT, qb, T, buf + TILE, 2 * w, lane);
+    glds_tile_piece(dOb, a.lddo, bT, qb, T, buf + TILE, 2 * w + 1, lane);
+    if (w < 2) {
+      const float* src = (w == 0 ? a.lse : a.delta) + rowbase + min(qb + lane, T - 1);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(buf + 2 * TILE + w * 256), 4, 0, 0);
+    }
+  };
+  issue(0);
+  if (nqt > 1) issue(1);
+  if (nqt > 1) {
+    if (w < 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();   // also publishes sE (plain stores)
+
+  f32x4 dk[2][4], dv[2][4];
+#pragma unroll
+  for (int gk = 0; gk < 2; ++gk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      dk[gk][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[gk][i] = dk[gk][i];
+    }
+
+  for (int qt = 0; qt < nqt; ++qt) {
+    const char* tQ = sm + (qt & 1) * QD;
+    const char* tD = tQ + TILE;
+    const float* sL = reinterpret_cast<const float*>(tQ + 2 * TILE);   // lse[64] | delta[64]
+    const int qb = qt * TQ;
+    // Q·Eᵀ of this query tile: wave w builds rows 16w..16w+15
+    const bool blk_lo = (kb0 + KB - 1) - qb <= -left;
+    const bool blk_hi = kb0 - (qb + TQ - 1) >= right;
+    const bool blk_band = !(blk_lo || blk_hi);
+    {
+      bf16x8 qfr[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) qfr[s] = frag_kc(tQ, 16 * w, s, lane);
+#pragma unroll
+      for (int jt = 0; jt < NREL / 16; ++jt) {
+        if (!blk_band && jt != 0 && jt != (nrel - 1) / 16) continue;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sE, jt * 16, s, lane), qfr[s], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = jt * 16 + 4 * g + r;
+          if (j < QEW) qet[(16 * w + li) * QEW + j] = acc[r];
+          if (j == 0) elo[16 * w + li] = acc[r] * c2;
+          if (j == nrel - 1) ehi[16 * w + li] = acc[r] * c2;
+        }
+      }
+    }
+    __syncthreads();
+    // per-lane query vectors (queries 16n + 4g + r): -lse*log2e, delta, edge biases
+    f32x4 nl2[4], dlt[4], lsev[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      lsev[n] = *reinterpret_cast<const f32x4*>(sL + 16 * n + 4 * g);
+      dlt[n] = *reinterpret_cast<const f32x4*>(sL + 64 + 16 * n + 4 * g);
+      nl2[n] = lsev[n] * -LOG2E;
+    }
+    // Two 32-query halves u; per half: S and dP of both key groups from Q/dO fragments read once,
+    // P and dS, then dV/dK from transposed Q/dO fragments read once for both key groups
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x4 sc[2][2], dp[2][2];
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) {
+        const int n = 2 * u + nn;
+        bf16x8 qa[2], da[2];
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          qa[ss] = frag_kc(tQ, 16 * n, ss, lane);
+          da[ss] = frag_kc(tD, 16 * n, ss, lane);
+        }
+#pragma unroll
+        for (int gk = 0; gk < 2; ++gk) {
+          sc[gk][nn] = mfma16(qa[0], kf[gk][0], f32x4{0.f, 0.f, 0.f, 0.f});
+          dp[gk][nn] = mfma16(da[0], vf[gk][0], f32x4{0.f, 0.f, 0.f, 0.f});
+          sc[gk][nn] = mfma16(qa[1], kf[gk][1], sc[gk][nn]);
+          dp[gk][nn] = mfma16(da[1], vf[gk][1], dp[gk][nn]);
+        }
+      }
+      bf16x8 pv[2], pk[2];
+#pragma unroll
+      for (int gk = 0; gk < 2; ++gk) {
+        const int k0g = k0w + 16 * gk, mykey = k0g + li;
+        const bool all_lo = (k0g + 15) - qb <= -left;
+        const bool all_hi = k0g - (qb + TQ - 1) >= right;
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn) {
+          const int n = 2 * u + nn;
+          if (all_lo || all_hi) {
+            const f32x4 eb = *reinterpret_cast<const f32x4*>((all_lo ? elo : ehi) + 16 * n + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r], c2, eb[r] + nl2[n][r]));
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int ql = 16 * n + 4 * g + r;
+              int d = mykey - (qb + ql);
+              d = d < -left ? -left : (d > right ? right : d);
+              sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r] + qet[ql * QEW + d + left], c2, nl2[n][r]));
+            }
+          }
+          if (any_masked && kmask[gk]) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sc[gk][nn][r] = lsev[n][r] == -INFINITY ? 1.0f / T : 0.f;
+          }
+          if (qb + TQ > T) {  // last query tile: rows past T (copies of row T-1) add nothing
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (qb + 16 * n + 4 * g + r >= T) sc[gk][nn][r] = 0.f;
+          }
+          dp[gk][nn] = sc[gk][nn] * (dp[gk][nn] - dlt[n]) * a.scale;   // dS * scale (for dK)
+        }
+        pv[gk] = pack_acc(sc[gk][0], sc[gk][1]);
+        pk[gk] = pack_acc(dp[gk][0], dp[gk][1]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 trd = frag_tr_asm(tD, dt * 16, u, lane);
+        const bf16x8 trq = frag_tr_asm(tQ, dt * 16, u, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int gk = 0; gk < 2; ++gk) {
+          dv[gk][dt] = mfma16(trd, pv[gk], dv[gk][dt]);
+          dk[gk][dt] = mfma16(trq, pk[gk], dk[gk][dt]);
         }
       }
     }
@@ -1395,6 +1856,27 @@ bool rel_v2() {
   return v == 1;
 }
 
+// STE_ATTN_FWD=3: the v3 relative-key forward (bias table; measured 5 % slower than v2 at c2,
+// kept for A/B work)
+bool rel_fwd_v3() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("STE_ATTN_FWD");
+    v = (e && e[0] == '3') ? 1 : 0;
+  }
+  return v == 1;
+}
+
+// STE_ATTN_BWD=2: the v2 relative-key dK/dV kernel (A/B comparisons in one process)
+bool rel_bwd_v3() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("STE_ATTN_BWD");
+    v = (e && e[0] == '2') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 int check(const ste_attn_args* a) {
   if (!a || a->B <= 0 || a->T <= 0 || a->H <= 0) return STE_ERR_ARG;
   if ((a->ldq & 7) || (a->ldk & 7) || (a->ldv & 7) || (a->ldo & 7)) return STE_ERR_SHAPE;
@@ -1416,7 +1898,10 @@ extern "C" int ste_attention_fwd(const ste_attn_args* a, void* stream) {
     dim3 g2((unsigned)(((a->T + rel2::BQ - 1) / rel2::BQ) * a->H * a->B));
     // always the hi/lo split of P: training and evaluation forwards then give bit-identical
     // outputs (the low half of O is written only when o_lo is given)
-    hipLaunchKernelGGL(attn_fwd_rel2_kernel<true>, g2, dim3(NT), rel2::FWD_LDS, s, *a);
+    if (rel_fwd_v3() && a->rel_left + a->rel_right + 4 <= rel3::TKEYS - 4)
+      hipLaunchKernelGGL(attn_fwd_rel3_kernel, g2, dim3(NT), rel3::FWD_LDS, s, *a);
+    else
+      hipLaunchKernelGGL(attn_fwd_rel2_kernel<true>, g2, dim3(NT), rel2::FWD_LDS, s, *a);
     STE_CHECK_LAUNCH();
     return 0;
   }
@@ -1440,7 +1925,8 @@ extern "C" int ste_attention_bwd(const ste_attn_args* a, void* stream) {
     hipLaunchKernelGGL(attn_bwd_dq_rel2_kernel, gq, dim3(NT), rel2::DQ_LDS, s, *a);
     STE_CHECK_LAUNCH();
     dim3 gk((unsigned)(((a->T + rel2::KB - 1) / rel2::KB) * a->H * a->B));
-    hipLaunchKernelGGL(attn_bwd_dkv_rel2_kernel, gk, dim3(NT), rel2::DKV_LDS, s, *a);
+    if (rel_bwd_v3()) hipLaunchKernelGGL(attn_bwd_dkv_rel3_kernel, gk, dim3(NT), rel2::DKV_LDS, s, *a);
+    else hipLaunchKernelGGL(attn_bwd_dkv_rel2_kernel, gk, dim3(NT), rel2::DKV_LDS, s, *a);
     STE_CHECK_LAUNCH();
     if (a->dE) {
       hipLaunchKernelGGL(attn_rel_dE2_kernel, dim3((unsigned)(a->B * a->H)), dim3(256), 0, s, *a);

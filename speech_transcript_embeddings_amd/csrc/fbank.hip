@@ -200,13 +200,27 @@ __global__ __launch_bounds__(128) void fbank_stats_kernel(const int32_t* __restr
   const int len = lengths[b];
   const int F = len >= FRAME ? 1 + (len - FRAME) / HOP : 0;
   const float* x = work + (int64_t)b * Fmax * NMEL + m;
+  // the sums must run frame by frame in order (numpy's rounding); loads go 16 frames ahead
+  constexpr int U = 16;
   float s = 0.f;
-  for (int f = 0; f < F; ++f) s = __fadd_rn(s, x[(int64_t)f * NMEL]);
+  for (int f0 = 0; f0 < F; f0 += U) {
+    float v[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) v[i] = f0 + i < F ? x[(int64_t)(f0 + i) * NMEL] : 0.f;
+#pragma unroll
+    for (int i = 0; i < U; ++i) s = __fadd_rn(s, v[i]);   // + 0 past F: exact
+  }
   const float mean = F > 0 ? __fdiv_rn(s, (float)F) : 0.f;
   float q = 0.f;
-  for (int f = 0; f < F; ++f) {
-    const float d = __fsub_rn(x[(int64_t)f * NMEL], mean);
-    q = __fadd_rn(q, __fmul_rn(d, d));
+  for (int f0 = 0; f0 < F; f0 += U) {
+    float v[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) v[i] = f0 + i < F ? x[(int64_t)(f0 + i) * NMEL] : mean;
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      const float d = __fsub_rn(v[i], mean);
+      if (f0 + i < F) q = __fadd_rn(q, __fmul_rn(d, d));
+    }
   }
   const float var = F > 1 ? __fdiv_rn(q, (float)(F - 1)) : 0.f;
   stats[(int64_t)b * 2 * NMEL + m] = mean;
