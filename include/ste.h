@@ -384,6 +384,67 @@ int ste_colsum(const void* x, int is_bf16, int64_t rows, int cols, int64_t ld, f
 int ste_scale_rows(float* x, const float* scale, int64_t rows, int cols, int64_t ld, void* stream);
 int ste_mask_i64_to_f32(const int64_t* m, float* f, int32_t* i32, int64_t n, void* stream);
 
+/* ------------------------------------------- wav2vec2 raw-waveform front end --
+ * EnhancedAudioTextModel(audio_model_name="facebook/wav2vec2-base"),
+ * whose encode_audio (ref:training/trainer_unfreeze.py:587-641) hands raw 16 kHz samples to
+ * transformers' Wav2Vec2Model (tf:models/wav2vec2/modeling_wav2vec2.py:1244-1375).  Activations
+ * are time-major [B*T, C]; the strided Conv1d layers and the grouped positional conv are
+ * ste_gemm launches on strided views (see csrc/w2v2.hip), these entries are the rest.
+ *
+ * conv0 (C_in = 1, no bias; :302-323): y fp32 [B*T0, C] = Σ_j w0[c, j]·wave[b, S0·t + j]
+ *   (w0 [C, K0], K0 <= 16, S0 <= 8, S0·(T0-1) + K0 <= N). */
+int ste_w2v_conv0_fwd(const float* wave, int64_t ldw, const float* w0, int B, int N, int T0, int C, int K0, int S0,
+                      float* y, void* stream);
+/* GroupNorm(num_groups = C) over time per (b, c) (biased variance, eps) + affine + GELU:
+ * h bf16 [B*T0, C]; mean/rstd fp32 [B*C] are kept for the backward. */
+int ste_w2v_gn_fwd(const float* y, const float* gamma, const float* beta, int B, int T0, int C, float eps,
+                   float* mean, float* rstd, void* h, void* stream);
+/* Backward of conv0 + GroupNorm + GELU given dh = dL/dh fp32 [B*T0, C]: dgamma/dbeta/dw0 +=
+ * (each may be NULL).  work fp32 of ste_w2v_gn_bwd_work(B, T0, C, K0) floats (deterministic
+ * partial sums, no atomics). */
+int64_t ste_w2v_gn_bwd_work(int B, int T0, int C, int K0);
+int ste_w2v_gn_bwd(const float* dh, const float* y, const float* mean, const float* rstd, const float* gamma,
+                   const float* beta, const float* wave, int64_t ldw, int B, int N, int T0, int C, int K0, int S0,
+                   float* dgamma, float* dbeta, float* dw0, float* work, int64_t work_floats, void* stream);
+/* out[i] += Σ_s part[s·n + i] (per-clip weight-gradient slabs of the strided conv GEMMs). */
+int ste_w2v_slab_sum(float* out, const float* part, int64_t n, int S, void* stream);
+/* col2im of a strided Conv1d input gradient: out[b, ti, c] = gelu'(z[b,ti,c]) ·
+ * Σ_{s·to + j = ti} dcol[b·To + to, j·C + c] (dcol fp32 row stride ldd; z bf16 or NULL for no
+ * activation; out bf16 if out_bf16 else fp32; [B*Ti, C]).  k = s = 1 applies gelu' alone. */
+int ste_w2v_conv_fold(const float* dcol, int64_t ldd, const void* z, int B, int Ti, int To, int C, int k, int s,
+                      void* out, int out_bf16, void* stream);
+/* [A][P][Q] -> [A][Q][P]: bf16 copy (conv weights [Co][Ci][k] -> the GEMM's [Co][k][Ci]), or with
+ * fp32_accumulate an fp32 += (the weight gradient back into the [Co][Ci][k] layout). */
+int ste_w2v_perm12(const void* src, void* dst, int A, int P, int Q, int fp32_accumulate, void* stream);
+/* Positional conv (weight-normed Conv1d(D, D, K, padding K/2, groups G) + SamePad + GELU,
+ * :326-379).  pos_pack: x fp32 [B*T, D] -> bf16 [G][B*Tp + K][D/G], Tp = T + K - 1, row b·Tp + u
+ * holding x[b, u - padl] (zero outside [0, T)); the forward GEMM reads it with row stride D/G.
+ * pos_elem: mode 0 out = src + gelu(cpad + bias); mode 1 out = src·gelu'(cpad + bias); mode 2
+ * out = (src + cpad)·maskf[row] (maskf may be NULL); cpad fp32 rows b·Tp + t, src/out [B*T, D]. */
+int ste_w2v_pos_pack(const float* x, int B, int T, int D, int G, int K, int padl, void* out, void* stream);
+int ste_w2v_pos_elem(int mode, const float* cpad, const float* bias, const float* src, const float* maskf, int B,
+                     int T, int D, int Tp, float* out, void* stream);
+/* weight_norm(dim=2) (nn.utils.parametrizations.weight_norm): v fp32 [D][Cg][K], g fp32 [K];
+ * writes norms[K] and the GEMM operands wr bf16 [G][Cg co][K][Cg ci] (forward) and wf bf16
+ * [G][Cg ci][K][Cg co] (taps reversed, the input gradient).  Backward from dW in the wr layout
+ * (fp32): dg[j] += s_j/n_j, dv += (g_j/n_j)·dW - (g_j s_j/n_j³)·v, s_j = Σ dW·v. */
+int ste_w2v_wnorm_fwd(const float* v, const float* g, int D, int Cg, int K, float* norms, void* wr, void* wf,
+                      void* stream);
+int ste_w2v_wnorm_bwd(const float* dwr, const float* v, const float* g, const float* norms, int D, int Cg, int K,
+                      float* dv, float* dg, void* stream);
+/* Frame mask of the conv stack (:997-1036): per clip L = Σ mask[b, :] (N if mask is NULL) pushed
+ * through floor((L - k)/s) + 1 per layer; maskf/mask32 [B*Tf] = t < L (either may be NULL).
+ * kernels/strides are HOST arrays of nconv <= 16 entries. */
+int ste_w2v_frame_mask(const int64_t* mask, int B, int N, int Tf, int nconv, const int* kernels, const int* strides,
+                       float* maskf, int32_t* mask32, void* stream);
+/* Wav2Vec2FeatureExtractor do_normalize: out[b, n] = (x - mean)/sqrt(var + 1e-7) over the first
+ * lengths[b] samples (population variance; lengths NULL = N), pad after. */
+int ste_w2v_wave_norm(const float* wave, int64_t ldw, const int32_t* lengths, int B, int N, float pad, float* out,
+                      void* stream);
+/* x[r, c] *= keep(seed, r·N + c)/(1-p) (the GEMM epilogue's dropout index) · maskf[r] (NULL = 1):
+ * backward of an output dropout + row mask, in place on a contiguous fp32 [M, N]. */
+int ste_w2v_drop_rows(float* x, int M, int N, float p, uint64_t seed, const float* maskf, void* stream);
+
 const char* ste_version(void);
 
 #ifdef __cplusplus

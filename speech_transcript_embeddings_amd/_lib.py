@@ -173,6 +173,28 @@ _SIGS = {
     "ste_spec_mask_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "ste_scale_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int64, c_void_p]),
     "ste_mask_i64_to_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "ste_w2v_conv0_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                  c_void_p]),
+    "ste_w2v_gn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
+                               c_void_p, c_void_p]),
+    "ste_w2v_gn_bwd_work": (c_int64, [c_int, c_int, c_int, c_int]),
+    "ste_w2v_gn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int,
+                               c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                               c_void_p]),
+    "ste_w2v_slab_sum": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "ste_w2v_conv_fold": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                  c_int, c_void_p]),
+    "ste_w2v_perm12": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "ste_w2v_pos_pack": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "ste_w2v_pos_elem": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                 c_void_p]),
+    "ste_w2v_wnorm_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ste_w2v_wnorm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                  c_void_p]),
+    "ste_w2v_frame_mask": (c_int, [c_void_p, c_int, c_int, c_int, c_int, C.POINTER(c_int), C.POINTER(c_int), c_void_p,
+                                   c_void_p, c_void_p]),
+    "ste_w2v_wave_norm": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p]),
+    "ste_w2v_drop_rows": (c_int, [c_void_p, c_int, c_int, c_float, c_uint64, c_void_p, c_void_p]),
     "ste_version": (C.c_char_p, []),
 }
 

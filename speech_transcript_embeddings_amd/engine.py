@@ -38,6 +38,14 @@ def _site_seed(base: int, site: int) -> int:
     return (x * 0xBF58476D1CE4E5B9) & _M64
 
 
+# parameter names of the post-LN layer (Engine._postln_fwd / _postln_bwd)
+XLMR_NAMES = dict(layer="text_encoder.encoder.layer.{i}.", q="attention.self.query", o="attention.output.dense",
+                  ln1="attention.output.LayerNorm", fi="intermediate.dense", fo="output.dense", ln2="output.LayerNorm")
+W2V2_NAMES = dict(layer="audio_encoder.encoder.layers.{i}.", q="attention.q_proj", o="attention.out_proj",
+                  ln1="layer_norm", fi="feed_forward.intermediate_dense", fo="feed_forward.output_dense",
+                  ln2="final_layer_norm")
+
+
 class Ctx(dict):
     """Saved activations of one forward (freed when backward finishes)."""
 
@@ -116,7 +124,16 @@ class Engine:
                                  dgamma=g, dbeta=self.s.g(name + ".bias"), **kw)
 
     # ================================================================ audio
+    @property
+    def raw_audio(self):
+        """wav2vec2 raw-waveform encoder (wav2vec2.py) instead of w2v-bert's fbank Conformer."""
+        from .modules import W2V2Config
+        return isinstance(self.acfg, W2V2Config)
+
     def audio_forward(self, feats, mask_i64, train, base_seed, ctx, save=True):
+        if self.raw_audio:
+            from . import wav2vec2
+            return wav2vec2.forward(self, feats, mask_i64, train, base_seed, ctx, save)
         c = self.acfg
         b, T, fin = feats.shape
         M = b * T
@@ -330,6 +347,9 @@ class Engine:
     def audio_backward(self, dh, ctx, layers_done=None):
         """layers_done() is called once every trainable Conformer layer's gradients are final
         (after the lowest trainable layer), so their all-reduce overlaps the frozen layers."""
+        if self.raw_audio:
+            from . import wav2vec2
+            return wav2vec2.backward(self, dh, ctx, layers_done)
         c = self.acfg
         b, T = ctx["a_b"], ctx["a_T"]
         maskf, mask32 = ctx["a_maskf"], ctx["a_mask32"]
@@ -389,69 +409,77 @@ class Engine:
         return x, xb
 
     def _xlmr_fwd(self, i, x, xb, nb, L, mask32, hp, ap, seed, save=True):
-        c = self.tcfg
+        return self._postln_fwd(self.tcfg, XLMR_NAMES, i, x, xb, nb, L, mask32, hp, ap, seed, save)
+
+    def _xlmr_bwd(self, i, sv, dx2, nb, L, mask32, hp, ap):
+        return self._postln_bwd(self.tcfg, XLMR_NAMES, i, sv, dx2, nb, L, mask32, hp, ap)
+
+    def _postln_fwd(self, c, nm, i, x, xb, nb, L, mask32, hp, ap, seed, save=True, act_p=0.0):
+        """One post-LN transformer layer: XLM-R (tf:…xlm_roberta…:186-398) and wav2vec2
+        (tf:models/wav2vec2/modeling_wav2vec2.py:466-608) share the math
+        LN(x + drop(O(attn(QKV x)))) -> LN(x1 + drop(W2·drop_act(gelu(W1 x1)))); `nm` maps the
+        parameter names (XLMR_NAMES / W2V2_NAMES)."""
         s = self.s
-        pre = f"text_encoder.encoder.layer.{i}."
+        pre = nm["layer"].format(i=i)
         M, D, F_ = x.shape[0], c.hidden_size, c.intermediate_size
         H = c.num_attention_heads
         eps = c.layer_norm_eps
-        tr = s.trainable_layer(pre + "attention.self.query.weight")
-        sv = {"tr": tr, "seed": seed}
-        qkv = ops.linear(xb, s.fused(pre + "attention.self.query.weight", 3, "w"),
-                         s.fused(pre + "attention.self.query.bias", 3, "p"), out_bf16=True)
+        tr = s.trainable_layer(pre + nm["q"] + ".weight")
+        sv = {"tr": tr, "seed": seed, "act_p": act_p}
+        qkv = ops.linear(xb, s.fused(pre + nm["q"] + ".weight", 3, "w"), s.fused(pre + nm["q"] + ".bias", 3, "p"),
+                         out_bf16=True)
         o = self._e(M, D, dtype=BF16)
         o_lo = self._e(M, D, dtype=BF16) if save else None
         lse = self._e(nb * H * L)
         ops.attention_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B=nb, T=L, H=H, o=o, lse=lse,
                           key_mask=mask32, scale=1.0 / math.sqrt(D // H), drop_p=ap, seed=_site_seed(seed, 1),
                           o_lo=o_lo)
-        y1 = ops.linear(o, s.w(pre + "attention.output.dense.weight"), s.p(pre + "attention.output.dense.bias"),
+        y1 = ops.linear(o, s.w(pre + nm["o"] + ".weight"), s.p(pre + nm["o"] + ".bias"),
                         residual=x, drop_p=hp, seed=_site_seed(seed, 2))
         x1 = self._e(M, D)
         x1b = self._e(M, D, dtype=BF16)
-        sv["st1"] = self._ln(y1, pre + "attention.output.LayerNorm", eps, y=x1, yb=x1b)
+        sv["st1"] = self._ln(y1, pre + nm["ln1"], eps, y=x1, yb=x1b)
         zt = self._e(M, F_, dtype=BF16) if save else None  # GELU pre-activation, for backward only
-        h = ops.linear(x1b, s.w(pre + "intermediate.dense.weight"), s.p(pre + "intermediate.dense.bias"),
-                       act=ACT_GELU, pre_out=zt, out_bf16=True)
-        y2 = ops.linear(h, s.w(pre + "output.dense.weight"), s.p(pre + "output.dense.bias"), residual=x1, drop_p=hp,
+        h = ops.linear(x1b, s.w(pre + nm["fi"] + ".weight"), s.p(pre + nm["fi"] + ".bias"),
+                       act=ACT_GELU, pre_out=zt, out_bf16=True, drop_p=act_p, seed=_site_seed(seed, 4))
+        y2 = ops.linear(h, s.w(pre + nm["fo"] + ".weight"), s.p(pre + nm["fo"] + ".bias"), residual=x1, drop_p=hp,
                         seed=_site_seed(seed, 3))
         x2 = self._e(M, D)
         x2b = self._e(M, D, dtype=BF16)
-        sv["st2"] = self._ln(y2, pre + "output.LayerNorm", eps, y=x2, yb=x2b)
+        sv["st2"] = self._ln(y2, pre + nm["ln2"], eps, y=x2, yb=x2b)
         sv.update(qkv=qkv, o=o, o_lo=o_lo, lse=lse, y1=y1, zt=zt, y2=y2)
         if tr:
             sv.update(xb=xb, x1b=x1b, h=h)
         return x2, x2b, sv
 
-    def _xlmr_bwd(self, i, sv, dx2, nb, L, mask32, hp, ap):
-        c = self.tcfg
+    def _postln_bwd(self, c, nm, i, sv, dx2, nb, L, mask32, hp, ap):
         s = self.s
-        pre = f"text_encoder.encoder.layer.{i}."
+        pre = nm["layer"].format(i=i)
         M, D = dx2.shape[0], c.hidden_size
         H = c.num_attention_heads
         tr = sv["tr"]
         seed = sv["seed"]
         dy2 = self._e(M, D)
         dy2b = self._e(M, D, dtype=BF16)
-        self._ln_bwd(dx2, sv["y2"], sv["st2"], pre + "output.LayerNorm", dx=dy2, dxb=dy2b, drop_p=hp,
-                     seed=_site_seed(seed, 3), dsum=s.g(pre + "output.dense.bias"))
-        dzt = self._dx(dy2b, pre + "output.dense.weight", act=ACT_GELU_BWD, z=sv["zt"], out_bf16=True,
-                            colsum=s.g(pre + "intermediate.dense.bias"))
+        self._ln_bwd(dx2, sv["y2"], sv["st2"], pre + nm["ln2"], dx=dy2, dxb=dy2b, drop_p=hp,
+                     seed=_site_seed(seed, 3), dsum=s.g(pre + nm["fo"] + ".bias"))
+        dzt = self._dx(dy2b, pre + nm["fo"] + ".weight", act=ACT_GELU_BWD, z=sv["zt"], out_bf16=True,
+                       colsum=s.g(pre + nm["fi"] + ".bias"), drop_p=sv["act_p"], seed=_site_seed(seed, 4))
         if tr:
-            self._dw(dy2b, sv["h"], pre + "output.dense.weight")
+            self._dw(dy2b, sv["h"], pre + nm["fo"] + ".weight")
         del dy2b
-        dx1 = self._dx(dzt, pre + "intermediate.dense.weight", residual=dy2)
+        dx1 = self._dx(dzt, pre + nm["fi"] + ".weight", residual=dy2)
         if tr:
-            self._dw(dzt, sv["x1b"], pre + "intermediate.dense.weight")
+            self._dw(dzt, sv["x1b"], pre + nm["fi"] + ".weight")
         del dzt, dy2
         dy1 = self._e(M, D)
         dy1b = self._e(M, D, dtype=BF16)
-        self._ln_bwd(dx1, sv["y1"], sv["st1"], pre + "attention.output.LayerNorm", dx=dy1, dxb=dy1b, drop_p=hp,
-                     seed=_site_seed(seed, 2), dsum=s.g(pre + "attention.output.dense.bias"))
+        self._ln_bwd(dx1, sv["y1"], sv["st1"], pre + nm["ln1"], dx=dy1, dxb=dy1b, drop_p=hp,
+                     seed=_site_seed(seed, 2), dsum=s.g(pre + nm["o"] + ".bias"))
         del dx1
-        do = self._dx(dy1b, pre + "attention.output.dense.weight", out_bf16=True)
+        do = self._dx(dy1b, pre + nm["o"] + ".weight", out_bf16=True)
         if tr:
-            self._dw(dy1b, sv["o"], pre + "attention.output.dense.weight")
+            self._dw(dy1b, sv["o"], pre + nm["o"] + ".weight")
         del dy1b
         qkv = sv["qkv"]
         dqkv = self._e(M, 3 * D, dtype=BF16)
@@ -460,10 +488,10 @@ class Engine:
                           dqkv[:, D:2 * D], dqkv[:, 2 * D:], B=nb, T=L, H=H, delta=delta, key_mask=mask32,
                           scale=1.0 / math.sqrt(D // H), drop_p=ap, seed=_site_seed(seed, 1), o_lo=sv["o_lo"])
         del do, delta
-        dx0 = self._dx(dqkv, pre + "attention.self.query.weight", 3, residual=dy1)
+        dx0 = self._dx(dqkv, pre + nm["q"] + ".weight", 3, residual=dy1)
         if tr:
-            self._dw(dqkv, sv["xb"], pre + "attention.self.query.weight", fused=3)
-            self._db(dqkv, pre + "attention.self.query.bias", fused=3)
+            self._dw(dqkv, sv["xb"], pre + nm["q"] + ".weight", fused=3)
+            self._db(dqkv, pre + nm["q"] + ".bias", fused=3)
         return dx0
 
     def text_backward(self, dh, ctx):
@@ -742,7 +770,12 @@ class Engine:
         tprojb = ops.cast_bf16(tproj.contiguous(), self._e(b, P, dtype=BF16))
         aprojb = ops.cast_bf16(aproj.contiguous(), self._e(b, P, dtype=BF16))
         tm32 = self._mask32(tmask, b * L) if tmask is not None else None
-        am32 = self._mask32(amask, b * T) if amask is not None else None
+        if amask is not None and self.raw_audio and amask.shape[-1] != T:
+            # a sample-level wav2vec2 mask [b, N]: the frame mask of the conv stack
+            from .wav2vec2 import frame_mask
+            am32 = frame_mask(self.acfg, amask, b, amask.shape[-1], T, self.s.device)[1]
+        else:
+            am32 = self._mask32(amask, b * T) if amask is not None else None
         # text -> audio
         aseqb = ops.linear(ahb, s.w("audio_seq_to_projection.weight"), s.p("audio_seq_to_projection.bias"),
                            out_bf16=True)
@@ -877,8 +910,10 @@ class Engine:
                 th, thb = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx, save)
         else:
             th, thb = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx, save)
-        ah, ahb = self.audio_forward(batch["input_values"].contiguous(), batch["attention_mask_audio"].contiguous(),
-                                     train, _site_seed(base_seed, 3), ctx, save)
+        amask = batch.get("attention_mask_audio")
+        ah, ahb = self.audio_forward(batch["input_values"].contiguous(),
+                                     None if amask is None else amask.contiguous(), train, _site_seed(base_seed, 3),
+                                     ctx, save)
         if side is not None:
             main.wait_stream(side)
         ctx["_thb"], ctx["_ahb"] = thb, ahb

@@ -21,7 +21,7 @@ from torch import nn
 from . import ops, torch_ops  # noqa: F401  (registers the ste:: custom ops)
 from .engine import Engine
 from .modules import (AttentivePooling, AudioConfig, AudioEncoder, CrossModalAttention, EnhancedProjection,
-                      TextConfig, TextEncoder, WordLevelAlignmentModule)
+                      TextConfig, TextEncoder, W2V2AudioEncoder, W2V2Config, WordLevelAlignmentModule)
 from .store import ParamStore
 
 logger = logging.getLogger(__name__)
@@ -31,11 +31,14 @@ _TEXT_CONFIGS = {
     "sentence-transformers/paraphrase-multilingual-mpnet-base-v2": TextConfig(),
     "xlm-roberta-base": TextConfig(),
 }
-_AUDIO_CONFIGS = {"facebook/w2v-bert-2.0": AudioConfig()}
+_AUDIO_CONFIGS = {"facebook/w2v-bert-2.0": AudioConfig(),
+                  # raw-waveform wav2vec2 (wav2vec2.py)
+                  "facebook/wav2vec2-base": W2V2Config(), "facebook/wav2vec2-base-960h": W2V2Config(),
+                  "facebook/wav2vec2-base-100h": W2V2Config()}
 
 
 def _resolve(name_or_cfg, table, default_cls):
-    if isinstance(name_or_cfg, (TextConfig, AudioConfig)):
+    if isinstance(name_or_cfg, (TextConfig, AudioConfig, W2V2Config)):
         return name_or_cfg
     if name_or_cfg in table:
         return table[name_or_cfg]
@@ -84,7 +87,8 @@ class EnhancedAudioTextModel(nn.Module):
                use_attentive_pooling, use_word_alignment, freeze_encoders, text_layers_to_unfreeze,
                audio_layers_to_unfreeze, spec_augment):
         self.text_encoder = TextEncoder(self.text_cfg)
-        self.audio_encoder = AudioEncoder(self.audio_cfg)
+        self.audio_encoder = (W2V2AudioEncoder if isinstance(self.audio_cfg, W2V2Config) else AudioEncoder)(
+            self.audio_cfg)
         self.text_hidden_dim = self.text_cfg.hidden_size
         self.audio_hidden_dim = self.audio_cfg.hidden_size
         self.projection_dim = projection_dim
@@ -156,6 +160,13 @@ class EnhancedAudioTextModel(nn.Module):
                         p.zero_()
                     elif n.endswith("masked_spec_embed"):
                         p.uniform_(0.0, 1.0, generator=g)
+                    elif n.endswith("parametrizations.weight.original1"):
+                        # wav2vec2 positional conv v (transformers' init: N(0, 2/(k·Cin/groups)))
+                        p.normal_(0.0, (2.0 / (p.shape[1] * p.shape[2])) ** 0.5, generator=g)
+                    elif n.endswith("parametrizations.weight.original0"):
+                        pass  # g = ‖v‖ per tap, set below once v is drawn
+                    elif ".conv_layers." in n and n.endswith("conv.weight"):
+                        nn.init.kaiming_normal_(p, generator=g)
                     else:
                         p.normal_(0.0, 0.02, generator=g)
                 elif leaf in ("in_proj_bias",) or (leaf == "bias" and "_attention" in n):
@@ -169,6 +180,10 @@ class EnhancedAudioTextModel(nn.Module):
                     else:
                         a = fan_in ** -0.5
                     p.uniform_(-a, a, generator=g)
+            params = dict(self.named_parameters())
+            for n, p in params.items():
+                if n.endswith("parametrizations.weight.original0"):
+                    p.copy_(params[n[:-1] + "1"].pow(2).sum(dim=(0, 1), keepdim=True).sqrt())
 
     # ---------------------------------------------------------------- API
     @staticmethod
@@ -186,6 +201,8 @@ class EnhancedAudioTextModel(nn.Module):
     def _embed(self, batch):
         for k in ("input_ids_pos", "attention_mask_pos", "input_ids_neg", "attention_mask_neg", "input_values",
                   "attention_mask_audio"):
+            if k == "attention_mask_audio" and batch.get(k) is None and self.engine.raw_audio:
+                continue  # wav2vec2: no sample mask = every frame valid
             if batch[k].device.type != "cuda":
                 raise RuntimeError(f"batch[{k!r}] must be on the GPU (libste.so has no CPU path)")
         self.store.sync_shadow()
@@ -217,11 +234,13 @@ class EnhancedAudioTextModel(nn.Module):
         return _EncodeFn.apply(self, "text", ids, mask, self.store.master[:1].detach().requires_grad_(True))
 
     def encode_audio(self, input_values, attention_mask=None):
-        """ref:587-641: (projection [B,P], last_hidden_state [B,T,H])."""
-        B, T, _ = input_values.shape
-        if attention_mask is None:
+        """ref:587-641: (projection [B,P], last_hidden_state [B,T,H]).  input_values: w2v-bert
+        features [B, T, 160], or raw samples [B, N] for a wav2vec2 audio encoder (whose
+        attention_mask may stay None, like wav2vec2-base's processor output)."""
+        B, T = input_values.shape[:2]
+        if attention_mask is None and not self.engine.raw_audio:
             attention_mask = torch.ones(B, T, dtype=torch.int64, device=input_values.device)
-        x, mask = input_values.contiguous(), attention_mask.contiguous()
+        x, mask = input_values.contiguous(), None if attention_mask is None else attention_mask.contiguous()
         if not torch.is_grad_enabled():
             return self._encode_nograd("audio", x, mask)
         return _EncodeFn.apply(self, "audio", x, mask, self.store.master[:1].detach().requires_grad_(True))
@@ -248,8 +267,8 @@ class EnhancedAudioTextModel(nn.Module):
             h, hb = e.text_forward(x, mask, self.training, _call_seed(self.training), ctx, save=False)
             m32, pool, proj = ctx["t_mask32"], "text_pooling", "text_projection"
         else:
-            B, L = x.shape[:2]
             h, hb = e.audio_forward(x, mask, self.training, _call_seed(self.training), ctx, save=False)
+            B, L = ctx["a_b"], ctx["a_T"]
             m32, pool, proj = ctx["a_mask32"], "audio_pooling", "audio_projection"
         _, pb = e._pool_fwd(pool, hb, m32, B, L, {})
         out = e._proj_fwd(proj, pb, B, self.training, _call_seed(self.training), {})
@@ -277,8 +296,8 @@ class _EncodeFn(torch.autograd.Function):
             h, hb = e.text_forward(x, mask, train, seed, ctx, save=True)
             m32, pool, proj = ctx["t_mask32"], "text_pooling", "text_projection"
         else:
-            B, L = x.shape[:2]
             h, hb = e.audio_forward(x, mask, train, seed, ctx, save=True)
+            B, L = ctx["a_b"], ctx["a_T"]
             m32, pool, proj = ctx["a_mask32"], "audio_pooling", "audio_projection"
         sv_pool, sv_proj = {}, {}
         _, pb = e._pool_fwd(pool, hb, m32, B, L, sv_pool)

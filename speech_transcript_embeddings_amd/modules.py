@@ -194,6 +194,149 @@ def _empty(*shape):
     return torch.empty(*shape)
 
 
+# --------------------------------------------------------- audio (wav2vec2, raw waveform)
+@dataclass
+class W2V2Config:
+    """wav2vec2-base (transformers Wav2Vec2Config defaults, configuration_wav2vec2.py): the
+    raw-waveform encoder of SURVEY §8f rank 4.  Implemented: feat_extract_norm="group",
+    conv_bias=False, do_stable_layer_norm=False (post-LN layers), GELU, no adapter."""
+    hidden_size: int = 768
+    num_hidden_layers: int = 12
+    num_attention_heads: int = 12
+    intermediate_size: int = 3072
+    conv_dim: tuple = (512, 512, 512, 512, 512, 512, 512)
+    conv_kernel: tuple = (10, 3, 3, 3, 3, 2, 2)
+    conv_stride: tuple = (5, 2, 2, 2, 2, 2, 2)
+    num_conv_pos_embeddings: int = 128
+    num_conv_pos_embedding_groups: int = 16
+    layer_norm_eps: float = 1e-5
+    hidden_dropout: float = 0.1
+    activation_dropout: float = 0.1
+    attention_dropout: float = 0.1
+    feat_proj_dropout: float = 0.0
+    layerdrop: float = 0.1
+    mask_time_prob: float = 0.05
+    mask_time_length: int = 10
+    mask_time_min_masks: int = 2
+    feat_extract_norm: str = "group"
+    conv_bias: bool = False
+    do_stable_layer_norm: bool = False
+
+    def __post_init__(self):
+        if self.feat_extract_norm != "group" or self.conv_bias or self.do_stable_layer_norm:
+            raise NotImplementedError("wav2vec2: only the base architecture (feat_extract_norm='group', "
+                                      "conv_bias=False, post-LN layers) is implemented")
+        self.conv_dim, self.conv_kernel, self.conv_stride = (tuple(self.conv_dim), tuple(self.conv_kernel),
+                                                             tuple(self.conv_stride))
+
+    def frames(self, n_samples: int) -> list:
+        """Sequence length after each conv layer: [N, T0, T1, ..., T_last]."""
+        out = [n_samples]
+        for k, s in zip(self.conv_kernel, self.conv_stride):
+            out.append((out[-1] - k) // s + 1)
+        return out
+
+
+class _W2VConv(nn.Module):
+    def __init__(self, cin, cout, k, s, group_norm):
+        super().__init__()
+        self.conv = nn.Conv1d(cin, cout, k, stride=s, bias=False)
+        if group_norm:
+            self.layer_norm = nn.GroupNorm(cout, cout, affine=True)
+
+
+class _W2VFeatureEncoder(nn.Module):
+    def __init__(self, c: W2V2Config):
+        super().__init__()
+        dims = (1,) + c.conv_dim
+        self.conv_layers = nn.ModuleList([_W2VConv(dims[i], dims[i + 1], c.conv_kernel[i], c.conv_stride[i], i == 0)
+                                          for i in range(len(c.conv_dim))])
+
+
+class _W2VFeatProj(nn.Module):
+    def __init__(self, c: W2V2Config):
+        super().__init__()
+        self.layer_norm = nn.LayerNorm(c.conv_dim[-1], eps=c.layer_norm_eps)
+        self.projection = nn.Linear(c.conv_dim[-1], c.hidden_size)
+
+
+class _WeightNormParams(nn.Module):
+    """nn.utils.parametrizations.weight_norm's parameter holder: state_dict keys
+    ...conv.parametrizations.weight.original0 (g [1,1,K]) / original1 (v [D, D/G, K])."""
+
+    def __init__(self, d, cg, k):
+        super().__init__()
+        import torch
+        self.original0 = nn.Parameter(torch.empty(1, 1, k))
+        self.original1 = nn.Parameter(torch.empty(d, cg, k))
+
+
+class _PosConv(nn.Module):
+    def __init__(self, c: W2V2Config):
+        super().__init__()
+        import torch
+        d, g, k = c.hidden_size, c.num_conv_pos_embedding_groups, c.num_conv_pos_embeddings
+        self.bias = nn.Parameter(torch.empty(d))
+        self.parametrizations = nn.Module()
+        self.parametrizations.weight = _WeightNormParams(d, d // g, k)
+
+
+class _PosConvEmbed(nn.Module):
+    def __init__(self, c: W2V2Config):
+        super().__init__()
+        self.conv = _PosConv(c)
+
+
+class _W2VAttn(nn.Module):
+    def __init__(self, d):
+        super().__init__()
+        # transformers' construction order (k, v, q, out); the ParamStore lays q|k|v out adjacently
+        self.k_proj, self.v_proj, self.q_proj = nn.Linear(d, d), nn.Linear(d, d), nn.Linear(d, d)
+        self.out_proj = nn.Linear(d, d)
+
+
+class _W2VFeedForward(nn.Module):
+    def __init__(self, d, f):
+        super().__init__()
+        self.intermediate_dense = nn.Linear(d, f)
+        self.output_dense = nn.Linear(f, d)
+
+
+class W2V2Layer(nn.Module):
+    """Wav2Vec2EncoderLayer (tf:models/wav2vec2/modeling_wav2vec2.py:575-608), post-LN."""
+
+    def __init__(self, c: W2V2Config):
+        super().__init__()
+        d, eps = c.hidden_size, c.layer_norm_eps
+        self.attention = _W2VAttn(d)
+        self.layer_norm = nn.LayerNorm(d, eps=eps)
+        self.feed_forward = _W2VFeedForward(d, c.intermediate_size)
+        self.final_layer_norm = nn.LayerNorm(d, eps=eps)
+
+
+class _W2VEncoder(nn.Module):
+    def __init__(self, c: W2V2Config):
+        super().__init__()
+        self.pos_conv_embed = _PosConvEmbed(c)
+        self.layer_norm = nn.LayerNorm(c.hidden_size, eps=c.layer_norm_eps)
+        self.layers = nn.ModuleList([W2V2Layer(c) for _ in range(c.num_hidden_layers)])
+
+
+class W2V2AudioEncoder(nn.Module):
+    """Wav2Vec2Model's parameter tree (tf:…/modeling_wav2vec2.py:1244-1263): state_dict keys
+    match transformers' (feature_extractor.conv_layers.*, feature_projection.*,
+    encoder.pos_conv_embed.conv.parametrizations.weight.original0/1, encoder.layers.*)."""
+
+    def __init__(self, c: W2V2Config):
+        super().__init__()
+        self.config = c
+        self.feature_extractor = _W2VFeatureEncoder(c)
+        self.feature_projection = _W2VFeatProj(c)
+        if c.mask_time_prob > 0:
+            self.masked_spec_embed = nn.Parameter(_empty(c.hidden_size))
+        self.encoder = _W2VEncoder(c)
+
+
 # ------------------------------------------------------------------------- heads
 class EnhancedProjection(nn.Module):
     """ref:66-99 (Linear -> GELU -> Dropout -> Linear -> LayerNorm)."""

@@ -36,6 +36,7 @@ def _fuse_groups(names):
     groups = {}
     sets = [("attention.self.query", "attention.self.key", "attention.self.value"),
             ("self_attn.linear_q", "self_attn.linear_k", "self_attn.linear_v"),
+            ("attention.q_proj", "attention.k_proj", "attention.v_proj"),
             ("_attention.key", "_attention.value")]
     nameset = set(names)
     for n in names:

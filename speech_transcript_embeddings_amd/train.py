@@ -482,7 +482,15 @@ class TrainStep:
         self.model.engine.layerdrop_gen = torch.Generator().manual_seed(int(seed.item()))
 
     def features(self, wav, lengths):
-        """GPU fbank for a batch of raw 16 kHz waveforms -> (input_values, attention_mask_audio)."""
+        """GPU fbank for a batch of raw 16 kHz waveforms -> (input_values, attention_mask_audio).
+        wav2vec2 audio encoder: Wav2Vec2FeatureExtractor's per-clip normalisation instead
+        (ste_w2v_wave_norm) and the sample mask of the clip lengths."""
+        if self.model.engine.raw_audio:
+            from .wav2vec2 import wave_normalize
+            B, n = wav.shape
+            lengths = lengths.to(device=wav.device, dtype=torch.int32)
+            mask = (torch.arange(n, device=wav.device).view(1, n) < lengths.view(B, 1)).to(torch.int64)
+            return wave_normalize(wav, lengths), mask
         n = int(wav.shape[1])
         T = ((1 + (n - 400) // 160) + 1) // 2
         return ops.fbank(wav, lengths, T, pad_value=self.pad_value, mask_mode=0)
