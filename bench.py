@@ -72,6 +72,9 @@ def parse(argv=None):
     ap.add_argument("--eval", action="store_true",
                     help="time the forward-only evaluation step (SURVEY §8f rank 1, ref evaluate() :1165-1284): "
                          "GPU fbank -> forward without saved activations -> similarity + InfoNCE value")
+    ap.add_argument("--audio-model", default="facebook/w2v-bert-2.0",
+                    help="facebook/wav2vec2-base: the raw-waveform wav2vec2 encoder (SURVEY §8f rank 4, "
+                         "not a BASELINE config: informational line, no CPU baseline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=4, help="BASELINE.md §3: B=4")
     ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU steps (median), after 2 warm-ups")
@@ -264,10 +267,12 @@ def main(argv=None):
     from speech_transcript_embeddings_amd.train import TrainStep, synthetic_batch
 
     glob, lbatch, micro, acc, scaling = batch_plan(args, world)
+    raw = "wav2vec2" in args.audio_model
     model = EnhancedAudioTextModel(use_word_alignment=args.align, text_layers_to_unfreeze=args.unfreeze,
                                    audio_layers_to_unfreeze=args.unfreeze, freeze_encoders=args.freeze,
                                    device=f"cuda:{local}", spec_augment=False,  # timed without SpecAugment
-                                   fp8_gemm=args.fp8)
+                                   fp8_gemm=args.fp8, audio_model_name=args.audio_model,
+                                   audio_embedding_dim=768 if raw else 1024)
     model.audio_cfg.layerdrop = 0.0
     step = TrainStep(model, warmup=100, total_steps=100000, accumulation_steps=acc,
                      in_batch_weight=args.in_batch_weight)
@@ -339,7 +344,10 @@ def main(argv=None):
     known = args.seconds == 10.0 and args.tokens == 64 and args.freeze == "partial" and \
         (args.unfreeze, args.align) in ((3, False), (5, True))
     gflop = (GFLOP_FWD_PER_PAIR if args.eval else GFLOP_PER_PAIR[args.unfreeze]) if known else None
-    if args.seconds == 10.0 and args.freeze == "partial" and args.tokens == 64:
+    if raw:
+        cname = "wav2vec2-base raw-waveform encoder (SURVEY §8f rank 4, not a BASELINE config)"
+        gflop = None
+    elif args.seconds == 10.0 and args.freeze == "partial" and args.tokens == 64:
         cname = {(3, False): "c2" if (world == 1 and glob == 64) else "c3", (5, True): "c4"}.get(
             (args.unfreeze, args.align), "custom")
     elif args.freeze == "none":
@@ -357,13 +365,15 @@ def main(argv=None):
         "data": "synthetic (SURVEY §8d waveforms + token ids), random-init weights",
         "config": {"workload": f"{cname}: global batch {glob} = {world} GPU x {acc} micro-batch(es) of {micro} pairs, "
                                f"each pair {args.seconds:g}s@16kHz audio + {L}-tok clean + {L}-tok corrupt; "
-                               f"w2v-bert-2.0 Conformer 24L + XLM-R-base 12L, "
-                               f"{'all layers trainable' if args.freeze == 'none' else f'{args.unfreeze}+{args.unfreeze} unfrozen'}"
-                               f"{', alignment head' if args.align else ''}; GPU fbank -> "
+                               + ("wav2vec2-base (conv stack + pos conv + 12L) + XLM-R-base 12L, " if raw else
+                                  "w2v-bert-2.0 Conformer 24L + XLM-R-base 12L, ")
+                               + f"{'all layers trainable' if args.freeze == 'none' else f'{args.unfreeze}+{args.unfreeze} unfrozen'}"
+                               f"{', alignment head' if args.align else ''}; {'GPU wave normalisation' if raw else 'GPU fbank'} -> "
                                + ("fwd (no saved activations, eval mode) -> similarity + InfoNCE value" if args.eval
                                   else "fwd -> InfoNCE -> bwd -> allreduce -> clip+AdamW"),
                    "global_batch": glob, "local_batch": lbatch, "micro_batch": micro, "accumulation_steps": acc,
-                   "seq_len_audio_frames": ((1 + (nsamp - 400) // 160) + 1) // 2,
+                   "seq_len_audio_frames": (model.audio_cfg.frames(nsamp)[-1] if raw else
+                                            ((1 + (nsamp - 400) // 160) + 1) // 2),
                    "seq_len_text": L, "parallelism": f"dp{world}"},
         "step_roofline_frac": round(pairs * gflop / (world * BF16_PEAK_TFLOPS * 1e3), 4) if gflop else None,
         "roofline": {"bound": "mfma", "kernel": dom, "launches_per_step": n_l // args.steps,
@@ -375,7 +385,7 @@ def main(argv=None):
         "hbm_kernels": hbm,
         "loss": round(loss, 5),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not raw:
         out["cpu_baseline"] = cpu_baseline(args)
     elif rank == 0:
         out["cpu_baseline"] = None

@@ -396,13 +396,14 @@ int ste_mask_i64_to_f32(const int64_t* m, float* f, int32_t* i32, int64_t n, voi
 int ste_w2v_conv0_fwd(const float* wave, int64_t ldw, const float* w0, int B, int N, int T0, int C, int K0, int S0,
                       float* y, void* stream);
 /* GroupNorm(num_groups = C) over time per (b, c) (biased variance, eps) + affine + GELU:
- * h bf16 [B*T0, C]; mean/rstd fp32 [B*C] are kept for the backward. */
+ * h bf16 [B*T0, C]; mean/rstd fp32 [B*C] are kept for the backward.  C % 4 == 0, C <= 1024.
+ * work: fp32 scratch of ste_w2v_gn_work(B, T0, C, K0) floats (fp64 partial sums per 512-row
+ * chunk; deterministic, no atomics), shared by the forward (K0 = 1) and the backward. */
+int64_t ste_w2v_gn_work(int B, int T0, int C, int K0);
 int ste_w2v_gn_fwd(const float* y, const float* gamma, const float* beta, int B, int T0, int C, float eps,
-                   float* mean, float* rstd, void* h, void* stream);
+                   float* mean, float* rstd, void* h, float* work, int64_t work_floats, void* stream);
 /* Backward of conv0 + GroupNorm + GELU given dh = dL/dh fp32 [B*T0, C]: dgamma/dbeta/dw0 +=
- * (each may be NULL).  work fp32 of ste_w2v_gn_bwd_work(B, T0, C, K0) floats (deterministic
- * partial sums, no atomics). */
-int64_t ste_w2v_gn_bwd_work(int B, int T0, int C, int K0);
+ * (each may be NULL). */
 int ste_w2v_gn_bwd(const float* dh, const float* y, const float* mean, const float* rstd, const float* gamma,
                    const float* beta, const float* wave, int64_t ldw, int B, int N, int T0, int C, int K0, int S0,
                    float* dgamma, float* dbeta, float* dw0, float* work, int64_t work_floats, void* stream);

@@ -175,9 +175,9 @@ _SIGS = {
     "ste_mask_i64_to_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "ste_w2v_conv0_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                   c_void_p]),
+    "ste_w2v_gn_work": (c_int64, [c_int, c_int, c_int, c_int]),
     "ste_w2v_gn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
-                               c_void_p, c_void_p]),
-    "ste_w2v_gn_bwd_work": (c_int64, [c_int, c_int, c_int, c_int]),
+                               c_void_p, c_void_p, c_int64, c_void_p]),
     "ste_w2v_gn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int,
                                c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                c_void_p]),

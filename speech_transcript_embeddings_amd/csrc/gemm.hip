@@ -1180,6 +1180,10 @@ int num_cus() {
   X(true, true, EF_BIAS | EF_C2 | EF_CBF16, STE_ACT_SWISH)   /* FFN intermediate   */ \
   X(true, true, EF_BIAS | EF_C2 | EF_CBF16, STE_ACT_GELU)    /* XLM-R intermediate */ \
   X(true, true, EF_BIAS | EF_CBF16, STE_ACT_SWISH)           /* FFN in, no backward */ \
+  X(true, true, EF_C2 | EF_CBF16, STE_ACT_GELU)              /* wav2vec2 conv layer */ \
+  X(true, true, EF_C2, STE_ACT_GELU)                         /* wav2vec2 last conv  */ \
+  X(true, true, EF_BIAS | EF_R | EF_DROP, STE_ACT_NONE)      /* post-LN O-proj / FFN out + dropout */ \
+  X(true, true, EF_BIAS | EF_C2 | EF_DROP | EF_CBF16, STE_ACT_GELU) /* wav2vec2 FFN in + act dropout */ \
   X(true, true, EF_BIAS | EF_CBF16, STE_ACT_GELU)                                     \
   X(true, true, EF_BIAS | EF_R, STE_ACT_NONE)                /* FFN out, O-proj    */ \
   X(true, true, EF_BIAS | EF_CBF16, STE_ACT_NONE)            /* QKV                */ \
@@ -1192,6 +1196,7 @@ int num_cus() {
   X(true, true, EF_Z | EF_COLSUM | EF_CBF16, STE_ACT_GELU_BWD)                        \
   X(true, true, EF_Z | EF_CBF16, STE_ACT_SWISH_BWD)          /* frozen layer: no db */ \
   X(true, true, EF_Z | EF_CBF16, STE_ACT_GELU_BWD)                                    \
+  X(true, true, EF_Z | EF_COLSUM | EF_DROP | EF_CBF16, STE_ACT_GELU_BWD) /* wav2vec2 act dropout */ \
   X(false, false, 0, STE_ACT_NONE)                           /* dW split-K slabs   */
 
 template <bool A_KC, bool B_KC>

@@ -52,86 +52,112 @@ __global__ __launch_bounds__(NT) void conv0_fwd_kernel(const float* __restrict__
 }
 
 // ------------------------------------------------------------------ GroupNorm(C, C)
-// per (b, c) statistics over time (biased variance, two passes in fp64)
-__global__ __launch_bounds__(NT) void gn_stats_kernel(const float* __restrict__ y, int T0, int C, float eps,
-                                                      float* __restrict__ mean, float* __restrict__ rstd) {
-  __shared__ double sred[NT];
-  __shared__ double smean[64];
-  const int b = blockIdx.y, cl = threadIdx.x & 63, r = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  const bool ok = c < C;
-  const float* yb = y + (int64_t)b * T0 * C + c;
-  double s = 0.0;
-  if (ok)
-    for (int t = r; t < T0; t += 4) s += (double)yb[(int64_t)t * C];
-  sred[threadIdx.x] = s;
-  __syncthreads();
-  if (r == 0) smean[cl] = (sred[cl] + sred[cl + 64] + sred[cl + 128] + sred[cl + 192]) / (double)T0;
-  __syncthreads();
-  const double mu = smean[cl];
-  double q = 0.0;
-  if (ok)
-    for (int t = r; t < T0; t += 4) {
-      const double d = (double)yb[(int64_t)t * C] - mu;
-      q += d * d;
-    }
-  __syncthreads();
-  sred[threadIdx.x] = q;
-  __syncthreads();
-  if (r == 0 && ok) {
-    const double var = (sred[cl] + sred[cl + 64] + sred[cl + 128] + sred[cl + 192]) / (double)T0;
-    mean[b * C + c] = (float)mu;
-    rstd[b * C + c] = (float)(1.0 / sqrt(var + (double)eps));
-  }
-}
+// Per (b, c) reductions over time, one pass: a block sums GN_ROWS rows of one clip for every
+// channel (16-B loads of 4 channels, fp64 partial sums, row groups combined in LDS) into
+// part[b][chunk][2][C]; a finalize kernel sums the chunks.
+//   MODE 0 (forward):  Σ y, Σ y²
+//   MODE 1 (backward): Σ dz, Σ dz·x̂ with x̂ = (y - mean)·rstd, dz = dh·gelu'(x̂·γ + β)
+constexpr int GN_ROWS = 512;
 
-// h = bf16(gelu((y - mean)·rstd·γ + β)), 4 channels per thread
-__global__ __launch_bounds__(NT) void gn_gelu_fwd_kernel(const float* __restrict__ y, const float* __restrict__ mean,
-                                                         const float* __restrict__ rstd, const float* __restrict__ g,
-                                                         const float* __restrict__ be, int T0, int C, int64_t n4,
-                                                         bf16* __restrict__ h) {
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
-    const int64_t e = i * 4;
-    const int64_t row = e / C;
-    const int c = (int)(e - row * C);
-    const int b = (int)(row / T0);
-    const f32x4 v = *reinterpret_cast<const f32x4*>(y + e);
-    f32x4 o;
+template <int MODE>
+__global__ __launch_bounds__(NT) void gn_partial_kernel(const float* __restrict__ y, const float* __restrict__ dh,
+                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                        const float* __restrict__ g, const float* __restrict__ be,
+                                                        int T0, int C, double* __restrict__ part) {
+  __shared__ double sred[NT * 8];
+  const int Q = C >> 2, groups = NT / Q;
+  const int b = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const int q = threadIdx.x % Q, rg = threadIdx.x / Q;
+  const int t0 = chunk * GN_ROWS, t1 = min(T0, t0 + GN_ROWS);
+  double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (rg < groups) {
+    const int c = q * 4;
+    f32x4 mu = {}, rs = {}, gc = {}, bc = {};
+    if (MODE == 1) {
+      mu = *reinterpret_cast<const f32x4*>(mean + b * C + c);
+      rs = *reinterpret_cast<const f32x4*>(rstd + b * C + c);
+      gc = *reinterpret_cast<const f32x4*>(g + c);
+      bc = *reinterpret_cast<const f32x4*>(be + c);
+    }
+    for (int t = t0 + rg; t < t1; t += groups) {
+      const int64_t off = ((int64_t)b * T0 + t) * C + c;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(y + off);
+      if (MODE == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          a[k] += (double)v[k];
+          a[4 + k] += (double)v[k] * (double)v[k];
+        }
+      } else {
+        const f32x4 d = *reinterpret_cast<const f32x4*>(dh + off);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float xh = (v[k] - mu[k]) * rs[k];
+          const float dz = d[k] * gelu_d(xh * gc[k] + bc[k]);
+          a[k] += (double)dz;
+          a[4 + k] += (double)dz * (double)xh;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sred[k * NT + threadIdx.x] = a[k];
+  __syncthreads();
+  if (rg == 0) {
+    for (int r = 1; r < groups; ++r)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] += sred[k * NT + r * Q + q];
+    double* p = part + ((int64_t)b * nchunk + chunk) * 2 * C + q * 4;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int bc = b * C + c + k;
-      o[k] = gelu_f((v[k] - mean[bc]) * rstd[bc] * g[c + k] + be[c + k]);
+      p[k] = a[k];
+      p[C + k] = a[4 + k];
     }
-    store_bf16x4(h + e, o);
   }
 }
 
-// backward, pass 1: per (b, c) s1 = Σ_t dz, s2 = Σ_t dz·x̂ with dz = dh·gelu'(z)
-__global__ __launch_bounds__(NT) void gn_bwd_reduce_kernel(const float* __restrict__ dh, const float* __restrict__ y,
-                                                           const float* __restrict__ mean,
-                                                           const float* __restrict__ rstd, const float* __restrict__ g,
-                                                           const float* __restrict__ be, int T0, int C,
-                                                           float* __restrict__ s1, float* __restrict__ s2) {
-  __shared__ double r1[NT], r2[NT];
-  const int b = blockIdx.y, cl = threadIdx.x & 63, r = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  double a1 = 0.0, a2 = 0.0;
-  if (c < C) {
-    const float mu = mean[b * C + c], rs = rstd[b * C + c], gc = g[c], bc = be[c];
-    const int64_t base = (int64_t)b * T0 * C + c;
-    for (int t = r; t < T0; t += 4) {
-      const float xh = (y[base + (int64_t)t * C] - mu) * rs;
-      const float dz = dh[base + (int64_t)t * C] * gelu_d(xh * gc + bc);
-      a1 += dz;
-      a2 += (double)dz * xh;
-    }
+// MODE 0: mean, rstd (biased variance) from Σy, Σy².  MODE 1: s1 = Σdz, s2 = Σdz·x̂ (fp32).
+template <int MODE>
+__global__ __launch_bounds__(NT) void gn_finalize_kernel(const double* __restrict__ part, int nchunk, int T0, int C,
+                                                         float eps, float* __restrict__ o1, float* __restrict__ o2) {
+  const int b = blockIdx.y, c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    const double* p = part + ((int64_t)b * nchunk + k) * 2 * C;
+    s1 += p[c];
+    s2 += p[C + c];
   }
-  r1[threadIdx.x] = a1;
-  r2[threadIdx.x] = a2;
-  __syncthreads();
-  if (r == 0 && c < C) {
-    s1[b * C + c] = (float)(r1[cl] + r1[cl + 64] + r1[cl + 128] + r1[cl + 192]);
-    s2[b * C + c] = (float)(r2[cl] + r2[cl + 64] + r2[cl + 128] + r2[cl + 192]);
+  if (MODE == 0) {
+    const double mu = s1 / T0;
+    const double var = fmax(s2 / T0 - mu * mu, 0.0);
+    o1[b * C + c] = (float)mu;
+    o2[b * C + c] = (float)(1.0 / sqrt(var + (double)eps));
+  } else {
+    o1[b * C + c] = (float)s1;
+    o2[b * C + c] = (float)s2;
+  }
+}
+
+// h = bf16(gelu((y - mean)·rstd·γ + β)): a block per 8 rows, 4 channels per thread
+__global__ __launch_bounds__(NT) void gn_gelu_fwd_kernel(const float* __restrict__ y, const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, const float* __restrict__ g,
+                                                         const float* __restrict__ be, int rows, int T0, int C,
+                                                         bf16* __restrict__ h) {
+  const int Q = C >> 2;
+  const int r0 = blockIdx.x * 8;
+  for (int i = threadIdx.x; i < 8 * Q; i += NT) {
+    const int row = r0 + i / Q, c = (i % Q) * 4;
+    if (row >= rows) break;
+    const int bc = (row / T0) * C + c;
+    const int64_t e = (int64_t)row * C + c;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(y + e);
+    const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + bc), rs = *reinterpret_cast<const f32x4*>(rstd + bc);
+    const f32x4 gc = *reinterpret_cast<const f32x4*>(g + c), bb = *reinterpret_cast<const f32x4*>(be + c);
+    f32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = gelu_f((v[k] - mu[k]) * rs[k] * gc[k] + bb[k]);
+    store_bf16x4(h + e, o);
   }
 }
 
@@ -200,13 +226,17 @@ __global__ __launch_bounds__(NT) void conv0_dw_kernel(const float* __restrict__ 
   }
 }
 
-// out[i] += Σ_s part[s·n + i]   (fixed order: deterministic)
+// ACC: out[i] += Σ_s part[s·n + i];  else out[g·n + i] = Σ_{s in group g of SG} part[s·n + i]
+// (fixed order: deterministic; the grouped form splits long sums over blockIdx.y)
+template <bool ACC>
 __global__ __launch_bounds__(NT) void slab_sum_kernel(float* __restrict__ out, const float* __restrict__ part,
-                                                      int64_t n, int S) {
+                                                      int64_t n, int S, int SG) {
+  const int s0 = ACC ? 0 : blockIdx.y * SG, s1 = ACC ? S : min(S, s0 + SG);
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     float a = 0.f;
-    for (int s = 0; s < S; ++s) a += part[(int64_t)s * n + i];
-    out[i] += a;
+    for (int s = s0; s < s1; ++s) a += part[(int64_t)s * n + i];
+    if (ACC) out[i] += a;
+    else out[(int64_t)blockIdx.y * n + i] = a;
   }
 }
 
@@ -214,21 +244,23 @@ __global__ __launch_bounds__(NT) void slab_sum_kernel(float* __restrict__ out, c
 // out[b, ti, c] = act'(z[b,ti,c]) · Σ_{to, j: s·to + j = ti} dcol[b·To + to, j·C + c]
 template <bool OUT_BF16>
 __global__ __launch_bounds__(NT) void conv_fold_kernel(const float* __restrict__ dcol, int64_t ldd,
-                                                       const bf16* __restrict__ z, int Ti, int To, int C, int k, int s,
-                                                       int64_t n4, void* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
-    const int64_t e = i * 4;
-    const int64_t row = e / C;
-    const int c = (int)(e - row * C);
-    const int b = (int)(row / Ti), ti = (int)(row - (int64_t)b * Ti);
+                                                       const bf16* __restrict__ z, int rows, int Ti, int To, int C,
+                                                       int k, int s, void* __restrict__ out) {
+  const int Q = C >> 2;
+  const int r0 = blockIdx.x * 8;
+  for (int i = threadIdx.x; i < 8 * Q; i += NT) {
+    const int row = r0 + i / Q, c = (i % Q) * 4;
+    if (row >= rows) break;
+    const int b = row / Ti, ti = row - b * Ti;
     int lo = ti - k + 1;
     lo = lo <= 0 ? 0 : (lo + s - 1) / s;
     const int hi = min(To - 1, ti / s);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int to = lo; to <= hi; ++to) {
       const int j = ti - s * to;
-      acc += *reinterpret_cast<const f32x4*>(dcol + ((int64_t)b * To + to) * ldd + (int64_t)j * C + c);
+      acc += *reinterpret_cast<const f32x4*>(dcol + ((int64_t)b * To + to) * ldd + j * C + c);
     }
+    const int64_t e = (int64_t)row * C + c;
     if (z) {
       const f32x4 zz = load_bf16x4(z + e);
 #pragma unroll
@@ -256,24 +288,22 @@ __global__ __launch_bounds__(NT) void perm12_kernel(const T* __restrict__ src, T
 // ------------------------------------------------------------------ positional conv
 // out [G][B·Tp + K][Cg] bf16: out[g][b·Tp + u][ci] = x[b, u - padl, g·Cg + ci] (0 outside [0,T))
 __global__ __launch_bounds__(NT) void pos_pack_kernel(const float* __restrict__ x, int B, int T, int D, int Cg, int Tp,
-                                                      int K, int padl, int64_t n8, bf16* __restrict__ out) {
+                                                      int K, int padl, int n8, bf16* __restrict__ out) {
   const int cg8 = Cg / 8;
-  const int64_t rows = (int64_t)B * Tp + K;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
-    const int ci = (int)(i % cg8) * 8;
-    const int64_t gr = i / cg8;
-    const int g = (int)(gr / rows);
-    const int64_t row = gr - (int64_t)g * rows;
+  const int rows = B * Tp + K;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < n8; i += gridDim.x * NT) {
+    const int gr = i / cg8, ci = (i - gr * cg8) * 8;
+    const int g = gr / rows, row = gr - g * rows;
     bf16x8 v = {};
-    if (row < (int64_t)B * Tp) {
-      const int b = (int)(row / Tp), t = (int)(row - (int64_t)b * Tp) - padl;
+    if (row < B * Tp) {
+      const int b = row / Tp, t = row - b * Tp - padl;
       if (t >= 0 && t < T) {
         const float* p = x + ((int64_t)b * T + t) * D + g * Cg + ci;
         const f32x4 a = *reinterpret_cast<const f32x4*>(p), c = *reinterpret_cast<const f32x4*>(p + 4);
         v = bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)c[0], (bf16)c[1], (bf16)c[2], (bf16)c[3]};
       }
     }
-    *reinterpret_cast<bf16x8*>(out + gr * Cg + ci) = v;
+    *reinterpret_cast<bf16x8*>(out + (int64_t)gr * Cg + ci) = v;
   }
 }
 
@@ -283,12 +313,12 @@ __global__ __launch_bounds__(NT) void pos_pack_kernel(const float* __restrict__ 
 template <int MODE>
 __global__ __launch_bounds__(NT) void pos_elem_kernel(const float* __restrict__ cpad, const float* __restrict__ bias,
                                                       const float* __restrict__ src, const float* __restrict__ maskf,
-                                                      int T, int D, int Tp, int64_t n4, float* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
-    const int64_t e = i * 4;
-    const int64_t row = e / D;
-    const int c = (int)(e - row * D);
-    const int b = (int)(row / T), t = (int)(row - (int64_t)b * T);
+                                                      int T, int D, int Tp, int n4, float* __restrict__ out) {
+  const int Q = D >> 2;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < n4; i += gridDim.x * NT) {
+    const int row = i / Q, c = (i - row * Q) * 4;
+    const int b = row / T, t = row - b * T;
+    const int64_t e = (int64_t)row * D + c;
     const f32x4 cv = *reinterpret_cast<const f32x4*>(cpad + ((int64_t)b * Tp + t) * D + c);
     const f32x4 sv = *reinterpret_cast<const f32x4*>(src + e);
     f32x4 o;
@@ -475,50 +505,87 @@ extern "C" int ste_w2v_conv0_fwd(const float* wave, int64_t ldw, const float* w0
   return 0;
 }
 
+namespace {
+struct GnPlan {
+  int nchunk;        // GN_ROWS-row chunks per clip (GroupNorm partial sums)
+  int tchunk, nc0;   // conv0 weight-gradient rows per block, blocks per clip
+  int64_t part_f, s12_f, dw_f, dw2_f;  // work sections, in floats
+};
+GnPlan gn_plan(int B, int T0, int C, int K0) {
+  GnPlan p;
+  p.nchunk = (T0 + GN_ROWS - 1) / GN_ROWS;
+  int nc0 = (1024 + B - 1) / B;
+  nc0 = max(1, min(nc0, (T0 + 31) / 32));
+  p.tchunk = ((T0 + nc0 - 1) / nc0 + 31) / 32 * 32;
+  p.nc0 = (T0 + p.tchunk - 1) / p.tchunk;
+  p.part_f = (int64_t)B * p.nchunk * 2 * C * 2;  // doubles
+  p.s12_f = (int64_t)2 * B * C;
+  p.dw_f = (int64_t)B * p.nc0 * C * K0;
+  p.dw2_f = (int64_t)((B * p.nc0 + 31) / 32) * C * K0;
+  return p;
+}
+bool gn_shape_ok(int B, int T0, int C) { return B > 0 && T0 > 0 && C > 0 && (C & 3) == 0 && C <= 4 * NT; }
+}  // namespace
+
+extern "C" int64_t ste_w2v_gn_work(int B, int T0, int C, int K0) {
+  if (!gn_shape_ok(B, T0, C)) return 0;
+  const GnPlan p = gn_plan(B, T0, C, K0);
+  return p.part_f + p.s12_f + p.dw_f + p.dw2_f;
+}
+
 extern "C" int ste_w2v_gn_fwd(const float* y, const float* gamma, const float* beta, int B, int T0, int C, float eps,
-                              float* mean, float* rstd, void* h, void* stream) {
-  if (B <= 0 || T0 <= 0 || C <= 0 || (C & 3)) return STE_ERR_SHAPE;
+                              float* mean, float* rstd, void* h, float* work, int64_t work_floats, void* stream) {
+  if (!gn_shape_ok(B, T0, C) || !work || work_floats < ste_w2v_gn_work(B, T0, C, 1)) return STE_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(gn_stats_kernel, dim3((C + 63) / 64, B), dim3(NT), 0, s, y, T0, C, eps, mean, rstd);
+  const GnPlan p = gn_plan(B, T0, C, 1);
+  double* part = reinterpret_cast<double*>(work);
+  hipLaunchKernelGGL(gn_partial_kernel<0>, dim3(p.nchunk, B), dim3(NT), 0, s, y, nullptr, nullptr, nullptr, nullptr,
+                     nullptr, T0, C, part);
   STE_CHECK_LAUNCH();
-  const int64_t n4 = (int64_t)B * T0 * C / 4;
-  hipLaunchKernelGGL(gn_gelu_fwd_kernel, dim3(grid_for(n4)), dim3(NT), 0, s, y, mean, rstd, gamma, beta, T0, C, n4,
+  hipLaunchKernelGGL(gn_finalize_kernel<0>, dim3((C + NT - 1) / NT, B), dim3(NT), 0, s, part, p.nchunk, T0, C, eps,
+                     mean, rstd);
+  STE_CHECK_LAUNCH();
+  const int rows = B * T0;
+  hipLaunchKernelGGL(gn_gelu_fwd_kernel, dim3((rows + 7) / 8), dim3(NT), 0, s, y, mean, rstd, gamma, beta, rows, T0, C,
                      (bf16*)h);
   STE_CHECK_LAUNCH();
   return 0;
-}
-
-extern "C" int64_t ste_w2v_gn_bwd_work(int B, int T0, int C, int K0) {
-  const int tchunk = 256;
-  const int nchunk = (T0 + tchunk - 1) / tchunk;
-  return (int64_t)2 * B * C + (int64_t)B * nchunk * C * K0;
 }
 
 extern "C" int ste_w2v_gn_bwd(const float* dh, const float* y, const float* mean, const float* rstd,
                               const float* gamma, const float* beta, const float* wave, int64_t ldw, int B, int N,
                               int T0, int C, int K0, int S0, float* dgamma, float* dbeta, float* dw0, float* work,
                               int64_t work_floats, void* stream) {
-  if (B <= 0 || T0 <= 0 || C <= 0 || K0 <= 0 || K0 > KMAX0 || S0 <= 0 || S0 > 8 || !work) return STE_ERR_SHAPE;
-  if (work_floats < ste_w2v_gn_bwd_work(B, T0, C, K0)) return STE_ERR_SHAPE;
+  if (!gn_shape_ok(B, T0, C) || K0 <= 0 || K0 > KMAX0 || S0 <= 0 || S0 > 8 || !work ||
+      (int64_t)S0 * (T0 - 1) + K0 > N || ldw < N)
+    return STE_ERR_SHAPE;
+  if (work_floats < ste_w2v_gn_work(B, T0, C, K0)) return STE_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
-  float* s1 = work;
-  float* s2 = work + (int64_t)B * C;
-  hipLaunchKernelGGL(gn_bwd_reduce_kernel, dim3((C + 63) / 64, B), dim3(NT), 0, s, dh, y, mean, rstd, gamma, beta, T0,
-                     C, s1, s2);
+  const GnPlan p = gn_plan(B, T0, C, K0);
+  double* part = reinterpret_cast<double*>(work);
+  float* s1 = work + p.part_f;
+  float* s2 = s1 + (int64_t)B * C;
+  hipLaunchKernelGGL(gn_partial_kernel<1>, dim3(p.nchunk, B), dim3(NT), 0, s, y, dh, mean, rstd, gamma, beta, T0, C,
+                     part);
+  STE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(gn_finalize_kernel<1>, dim3((C + NT - 1) / NT, B), dim3(NT), 0, s, part, p.nchunk, T0, C, 0.f, s1,
+                     s2);
   STE_CHECK_LAUNCH();
   if (dgamma || dbeta) {
     hipLaunchKernelGGL(gn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, s1, s2, B, C, dgamma, dbeta);
     STE_CHECK_LAUNCH();
   }
   if (dw0) {
-    const int tchunk = 256;
-    const int nchunk = (T0 + tchunk - 1) / tchunk;
-    float* part = work + (int64_t)2 * B * C;
-    hipLaunchKernelGGL(conv0_dw_kernel, dim3(nchunk, B), dim3(NT), 0, s, dh, y, mean, rstd, gamma, beta, s1, s2, wave,
-                       ldw, T0, C, K0, S0, tchunk, part);
+    float* dpart = s1 + p.s12_f;
+    float* dpart2 = dpart + p.dw_f;
+    hipLaunchKernelGGL(conv0_dw_kernel, dim3(p.nc0, B), dim3(NT), 0, s, dh, y, mean, rstd, gamma, beta, s1, s2, wave,
+                       ldw, T0, C, K0, S0, p.tchunk, dpart);
     STE_CHECK_LAUNCH();
     const int64_t n = (int64_t)C * K0;
-    hipLaunchKernelGGL(slab_sum_kernel, dim3(grid_for(n)), dim3(NT), 0, s, dw0, part, n, B * nchunk);
+    const int S = B * p.nc0, S2 = (S + 31) / 32;
+    hipLaunchKernelGGL(slab_sum_kernel<false>, dim3(grid_for(n), S2), dim3(NT), 0, s, dpart2, dpart, n, S, 32);
+    STE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(slab_sum_kernel<true>, dim3(grid_for(n)), dim3(NT), 0, s, dw0, dpart2, n, S2, 0);
     STE_CHECK_LAUNCH();
   }
   return 0;
@@ -526,7 +593,7 @@ extern "C" int ste_w2v_gn_bwd(const float* dh, const float* y, const float* mean
 
 extern "C" int ste_w2v_slab_sum(float* out, const float* part, int64_t n, int S, void* stream) {
   if (n <= 0 || S <= 0) return STE_ERR_SHAPE;
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, out, part, n, S);
+  hipLaunchKernelGGL(slab_sum_kernel<true>, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, out, part, n, S, 0);
   STE_CHECK_LAUNCH();
   return 0;
 }
@@ -534,15 +601,15 @@ extern "C" int ste_w2v_slab_sum(float* out, const float* part, int64_t n, int S,
 extern "C" int ste_w2v_conv_fold(const float* dcol, int64_t ldd, const void* z, int B, int Ti, int To, int C, int k,
                                  int s, void* out, int out_bf16, void* stream) {
   if (B <= 0 || Ti <= 0 || To <= 0 || C <= 0 || (C & 3) || k <= 0 || s <= 0 || ldd < (int64_t)k * C || (ldd & 3) ||
-      (int64_t)s * (To - 1) + k > Ti)
+      (int64_t)s * (To - 1) + k > Ti || (int64_t)B * Ti >= (1ll << 31))
     return STE_ERR_SHAPE;
-  const int64_t n4 = (int64_t)B * Ti * C / 4;
+  const int rows = B * Ti;
   if (out_bf16)
-    hipLaunchKernelGGL(conv_fold_kernel<true>, dim3(grid_for(n4)), dim3(NT), 0, (hipStream_t)stream, dcol, ldd,
-                       (const bf16*)z, Ti, To, C, k, s, n4, out);
+    hipLaunchKernelGGL(conv_fold_kernel<true>, dim3((rows + 7) / 8), dim3(NT), 0, (hipStream_t)stream, dcol, ldd,
+                       (const bf16*)z, rows, Ti, To, C, k, s, out);
   else
-    hipLaunchKernelGGL(conv_fold_kernel<false>, dim3(grid_for(n4)), dim3(NT), 0, (hipStream_t)stream, dcol, ldd,
-                       (const bf16*)z, Ti, To, C, k, s, n4, out);
+    hipLaunchKernelGGL(conv_fold_kernel<false>, dim3((rows + 7) / 8), dim3(NT), 0, (hipStream_t)stream, dcol, ldd,
+                       (const bf16*)z, rows, Ti, To, C, k, s, out);
   STE_CHECK_LAUNCH();
   return 0;
 }
@@ -563,7 +630,8 @@ extern "C" int ste_w2v_perm12(const void* src, void* dst, int A, int P, int Q, i
 extern "C" int ste_w2v_pos_pack(const float* x, int B, int T, int D, int G, int K, int padl, void* out, void* stream) {
   if (B <= 0 || T <= 0 || G <= 0 || D % G || (D / G) % 8 || K <= 0 || padl < 0 || padl >= K) return STE_ERR_SHAPE;
   const int Cg = D / G, Tp = T + K - 1;
-  const int64_t n8 = (int64_t)G * ((int64_t)B * Tp + K) * Cg / 8;
+  if ((int64_t)G * ((int64_t)B * Tp + K) * Cg / 8 >= (1ll << 31)) return STE_ERR_SHAPE;
+  const int n8 = G * (B * Tp + K) * Cg / 8;
   hipLaunchKernelGGL(pos_pack_kernel, dim3(grid_for(n8)), dim3(NT), 0, (hipStream_t)stream, x, B, T, D, Cg, Tp, K, padl,
                      n8, (bf16*)out);
   STE_CHECK_LAUNCH();
@@ -572,9 +640,10 @@ extern "C" int ste_w2v_pos_pack(const float* x, int B, int T, int D, int G, int 
 
 extern "C" int ste_w2v_pos_elem(int mode, const float* cpad, const float* bias, const float* src, const float* maskf,
                                 int B, int T, int D, int Tp, float* out, void* stream) {
-  if (B <= 0 || T <= 0 || D <= 0 || (D & 3) || Tp < T || mode < 0 || mode > 2 || (mode < 2 && !bias))
+  if (B <= 0 || T <= 0 || D <= 0 || (D & 3) || Tp < T || mode < 0 || mode > 2 || (mode < 2 && !bias) ||
+      (int64_t)B * T * D / 4 >= (1ll << 31))
     return STE_ERR_SHAPE;
-  const int64_t n4 = (int64_t)B * T * D / 4;
+  const int n4 = B * T * D / 4;
   hipStream_t s = (hipStream_t)stream;
   if (mode == 0)
     hipLaunchKernelGGL(pos_elem_kernel<0>, dim3(grid_for(n4)), dim3(NT), 0, s, cpad, bias, src, maskf, T, D, Tp, n4, out);

@@ -103,8 +103,11 @@ def forward(e, wave, mask_i64, train, base_seed, ctx, save=True):
               ptr(y0), _s())
     gn_mean, gn_rstd = e._e(B * C0), e._e(B * C0)
     h = e._e(B * T0, C0, dtype=BF16)
+    nwork = int(_lib.fn("ste_w2v_gn_work")(B, T0, C0, 1))
+    work = e._e(nwork)
     _lib.call("ste_w2v_gn_fwd", ptr(y0), ptr(s.p(FE + "0.layer_norm.weight")), ptr(s.p(FE + "0.layer_norm.bias")),
-              B, T0, C0, 1e-5, ptr(gn_mean), ptr(gn_rstd), ptr(h), _s())
+              B, T0, C0, 1e-5, ptr(gn_mean), ptr(gn_rstd), ptr(h), ptr(work), nwork, _s())
+    del work
     convs = [dict(h=h)]
     # ---- conv1.. : GEMM on the strided view of the previous output, GELU epilogue
     nl = len(c.conv_dim)
@@ -304,7 +307,7 @@ def backward(e, dh, ctx, layers_done=None):
         # ---- conv0 + GroupNorm + GELU (dz is dL/dh0 in fp32 here)
         C0, K0, S0 = c.conv_dim[0], c.conv_kernel[0], c.conv_stride[0]
         T0 = Ts[1]
-        nwork = int(_lib.fn("ste_w2v_gn_bwd_work")(B, T0, C0, K0))
+        nwork = int(_lib.fn("ste_w2v_gn_work")(B, T0, C0, K0))
         work = e._e(nwork)
         _lib.call("ste_w2v_gn_bwd", ptr(dz), ptr(sv["y0"]), ptr(sv["gn_mean"]), ptr(sv["gn_rstd"]),
                   ptr(s.p(FE + "0.layer_norm.weight")), ptr(s.p(FE + "0.layer_norm.bias")), ptr(sv["wave"]),
