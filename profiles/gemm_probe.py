@@ -1,0 +1,120 @@
+"""The encoder GEMMs of the c2 step, timed in isolation (HIP events): ste_gemm with the
+epilogue the step uses, ste_gemm with a plain bf16 output, and torch.mm (hipBLASLt) on the
+same operands — the A/B harness behind DESIGN §3's GEMM numbers.
+
+    python profiles/gemm_probe.py [--rows 31936] [--iters 20] [--only NAME]
+
+Shapes (M = b·T rows of c2 = 64 x 499): forward QKV / O / FFN-in / FFN-out, the input-gradient
+(dX = dY·W through the cached Wᵀ) and the weight-gradient (dW = dYᵀX, k-major operands,
+split-K) GEMMs of one Conformer layer."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=64 * 499)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    from speech_transcript_embeddings_amd import _lib, ops
+    M = a.rows
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(0)
+
+    def rnd(*s, dt=torch.bfloat16, sc=1.0):
+        return (torch.randn(*s, device=dev, generator=g) * sc).to(dt)
+
+    ws = torch.empty((80 << 20) // 4, device=dev)
+    D, F = 1024, 4096
+    x = rnd(M, D)
+    h = rnd(M, F)
+    res = rnd(M, D, dt=torch.float32)
+    cases = {}
+    for name, (k, n, epi) in {"qkv": (D, 3 * D, "bias_bf16"), "o_proj": (D, D, "bias_res"),
+                              "ffn_in": (D, F, "bias_swish_c2"), "ffn_out": (F, D, "bias_res"),
+                              "dx_ffn_out": (F, D, "dx_bf16"), "dx_qkv": (3 * D, D, "dx_bf16"),
+                              "dx_ffn_in_dz": (D, F, "dz_swish")}.items():
+        cases[name] = (k, n, epi)
+    out = {"rows": M}
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / a.iters
+
+    for name, (K, N, epi) in cases.items():
+        if a.only and a.only != name:
+            continue
+        A = x if K == D else (h if K == F else rnd(M, K))
+        W = rnd(N, K, sc=0.02)
+        bias = torch.randn(N, device=dev, generator=g) * 0.1
+        kw = {}
+        if epi == "bias_bf16":
+            kw = dict(bias=bias, out_bf16=True)
+        elif epi == "bias_res":
+            kw = dict(bias=bias, residual=res if N == D else rnd(M, N, dt=torch.float32))
+        elif epi == "bias_swish_c2":
+            kw = dict(bias=bias, act=_lib.ACT_SWISH, pre_out=torch.empty(M, N, device=dev, dtype=torch.bfloat16),
+                      out_bf16=True)
+        elif epi == "dx_bf16":
+            kw = dict(out_bf16=True)
+        elif epi == "dz_swish":
+            kw = dict(act=_lib.ACT_SWISH_BWD, z=rnd(M, N), out_bf16=True,
+                      colsum=torch.zeros(N, device=dev))
+        o_epi = torch.empty(M, N, device=dev, dtype=torch.bfloat16 if kw.get("out_bf16") else torch.float32)
+        o_plain = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        t_epi = timed(lambda: ops.linear(A, W, out=o_epi, **{k: v for k, v in kw.items() if k != "out_bf16"}))
+        t_plain = timed(lambda: ops.linear(A, W, out=o_plain))
+        Wt = W.t().contiguous()
+        t_blas = timed(lambda: torch.mm(A, Wt, out=o_plain))
+        fl = 2.0 * M * N * K
+        out[name] = {"M": M, "N": N, "K": K, "epilogue": epi,
+                     "ste_epilogue_us": round(t_epi, 1), "ste_epilogue_tflops": round(fl / t_epi / 1e6, 1),
+                     "ste_plain_us": round(t_plain, 1), "ste_plain_tflops": round(fl / t_plain / 1e6, 1),
+                     "hipblaslt_plain_us": round(t_blas, 1), "hipblaslt_plain_tflops": round(fl / t_blas / 1e6, 1)}
+        print(json.dumps({name: out[name]}), flush=True)
+    # weight gradients: dW[N,K] = dYᵀ·X over M rows (k-major operands, split-K slabs)
+    for name, (N, K) in {"dw_ffn_in": (F, D), "dw_ffn_out": (D, F), "dw_qkv": (3 * D, D), "dw_o": (D, D)}.items():
+        if a.only and a.only != name:
+            continue
+        dy = rnd(M, N)
+        X = x if K == D else h
+        dw = torch.zeros(N, K, device=dev)
+        t_ste = timed(lambda: ops.linear_dw(dy, X, out=dw, beta=1.0, ws=ws))
+        dwb = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+        t_blas = timed(lambda: torch.mm(dy.t(), X, out=dwb))
+        fl = 2.0 * M * N * K
+        out[name] = {"M": N, "N": K, "K": M, "kernel": ops.gemm_kernel_name(_dw_args(ops, dy, X, dw, ws)),
+                     "ste_us": round(t_ste, 1), "ste_tflops": round(fl / t_ste / 1e6, 1),
+                     "hipblaslt_us": round(t_blas, 1), "hipblaslt_tflops": round(fl / t_blas / 1e6, 1)}
+        print(json.dumps({name: out[name]}), flush=True)
+    print(json.dumps(out), flush=True)
+
+
+def _dw_args(ops, dy, x, dw, ws):
+    from speech_transcript_embeddings_amd._lib import GemmArgs, ptr
+    a = GemmArgs()
+    a.M, a.N, a.K, a.batch = dy.shape[1], x.shape[1], dy.shape[0], 1
+    a.A, a.lda, a.a_kc = ptr(dy), dy.stride(0), 0
+    a.B, a.ldb, a.b_kc = ptr(x), x.stride(0), 0
+    a.C, a.ldc = ptr(dw), dw.stride(0)
+    a.alpha, a.beta = 1.0, 1.0
+    a.ws, a.ws_bytes = ptr(ws), ws.numel() * 4
+    return a
+
+
+if __name__ == "__main__":
+    main()
