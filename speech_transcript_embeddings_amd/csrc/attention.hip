@@ -1375,6 +1375,292 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel2_kernel(ste_attn_args a
   }
 }
 
+// ====================================== relative-key backward, v3: dQ (+ delta, + bins G)
+// v2's schedule with 32 queries per wave: two 16-row groups share every K, V and transposed-K
+// fragment read (half the LDS traffic per MFMA, as in the forward), 128 queries per block.
+// The per-row Q·Eᵀ table and the G (distance-bin) table share one LDS row: an interior bin
+// d (-left < d < right) of a query is read for exactly one key (k = q + d), right before that
+// key's dS is written to the same slot; the clamped bins 0 and nrel-1 stay intact for the other
+// keys and their G sums live in registers.  Interior bins whose key was never visited (k < 0 or
+// past the last tile) are zeroed after the loop.  With the 80-float rows (bins 64..79 by one
+// 16x16x16 MFMA) the block needs 74 KB of LDS: two blocks per CU.
+namespace rel2 {
+constexpr int DQ3_WQ = 32;
+constexpr int DQ3_Q = 4 * DQ3_WQ;
+constexpr int GT3 = NREL;                                  // 80-float Q·Eᵀ / G rows
+constexpr int DQ3_T_OFF = MASK_OFF + 512;
+constexpr int DQ3_LDS = DQ3_T_OFF + 4 * DQ3_WQ * GT3 * 4;
+}  // namespace rel2
+
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a) {
+  using namespace rel2;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T = a.T, H = a.H;
+  const int ntile = (T + DQ3_Q - 1) / DQ3_Q;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = id % ntile, bh = id / ntile, h = bh % H, b = bh / H, bT = b * T;
+  const int left = a.rel_left, right = a.rel_right, nrel = left + right + 1;
+  const bf16* Qb = (const bf16*)a.q + h * HD;
+  const bf16* Kb = (const bf16*)a.k + h * HD;
+  const bf16* Vb = (const bf16*)a.v + h * HD;
+  const bf16* dOb = (const bf16*)a.dout + h * HD;
+  const bf16* Ob = (const bf16*)a.o + h * HD;
+  const bf16* Olb = a.o_lo ? (const bf16*)a.o_lo + h * HD : nullptr;
+  const int qw = tile * DQ3_Q + w * DQ3_WQ;
+  const float c2 = a.scale * LOG2E;
+
+  bf16x8 qf[2][2], df[2][2];
+  float dl[2], nl2[2], pm[2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int myq = qw + 16 * gq + li;
+    const bool qv = myq < T;
+    const int64_t off = (int64_t)(bT + myq);
+    float dpart = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      qf[gq][s] = qv ? *reinterpret_cast<const bf16x8*>(Qb + off * a.ldq + 32 * s + 8 * g) : bf16x8{};
+      df[gq][s] = qv ? *reinterpret_cast<const bf16x8*>(dOb + off * a.lddo + 32 * s + 8 * g) : bf16x8{};
+      const bf16x8 of = qv ? *reinterpret_cast<const bf16x8*>(Ob + off * a.ldo + 32 * s + 8 * g) : bf16x8{};
+      const bf16x8 ol = (qv && Olb) ? *reinterpret_cast<const bf16x8*>(Olb + off * a.ldolo + 32 * s + 8 * g)
+                                    : bf16x8{};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dpart += (float)df[gq][s][e] * ((float)of[e] + (float)ol[e]);
+    }
+    dpart += __shfl_xor(dpart, 16, 64);
+    dpart += __shfl_xor(dpart, 32, 64);
+    dl[gq] = dpart;
+    const int64_t rowid = (int64_t)(b * H + h) * T + myq;
+    if (qv && g == 0) a.delta[rowid] = dpart;
+    const float lse = qv ? a.lse[rowid] : 0.f;
+    nl2[gq] = -lse * LOG2E;
+    pm[gq] = lse == -INFINITY ? 1.0f / T : 0.f;
+  }
+
+  float* tb = reinterpret_cast<float*>(sm + DQ3_T_OFF) + w * DQ3_WQ * GT3;
+  stage_E(sm, (const bf16*)a.rel_E, nrel, NREL, tid);
+  __syncthreads();
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int jt = 0; jt < NREL / 16; ++jt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sm, jt * 16, s, lane), qf[gq][s], acc);
+      *reinterpret_cast<f32x4*>(tb + (16 * gq + li) * GT3 + jt * 16 + 4 * g) = acc;
+    }
+  __syncthreads();
+  float blo[2], bhi[2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    blo[gq] = tb[(16 * gq + li) * GT3] * c2 + nl2[gq];
+    bhi[gq] = tb[(16 * gq + li) * GT3 + nrel - 1] * c2 + nl2[gq];
+  }
+
+  char* sMask = sm + MASK_OFF;
+  const int nkt = (T + TK - 1) / TK;
+  const bool has_mask = a.key_mask != nullptr;
+  auto issue = [&](int kt) {
+    char* buf = sm + (kt & 1) * KV;
+    const int kb = kt * TK;
+    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w, lane);
+    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w + 1, lane);
+    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w, lane);
+    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w + 1, lane);
+    if (w == 0 && has_mask) glds_mask(a.key_mask, bT, kb, T, sMask + (kt & 1) * 256, lane);
+  };
+  issue(0);
+  if (nkt > 1) issue(1);
+  if (nkt > 1) {
+    if (w == 0 && has_mask) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  f32x4 dq[2][4];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dq[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float glo[2] = {0.f, 0.f}, ghi[2] = {0.f, 0.f};
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const char* tK = sm + (kt & 1) * KV;
+    const char* tV = tK + TILE;
+    const int* mk = reinterpret_cast<const int*>(sMask + (kt & 1) * 256);
+    const int kb = kt * TK;
+    f32x4 sc[2][4], dp[2][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int gq = 0; gq < 2; ++gq) sc[gq][t] = dp[gq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 kf = frag_kc(tK, t * 16, ss, lane);
+        const bf16x8 vf = frag_kc(tV, t * 16, ss, lane);
+#pragma unroll
+        for (int gq = 0; gq < 2; ++gq) {
+          sc[gq][t] = mfma16(kf, qf[gq][ss], sc[gq][t]);
+          dp[gq][t] = mfma16(vf, df[gq][ss], dp[gq][t]);
+        }
+      }
+    }
+    bf16x8 ktr[4][2];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) ktr[dt][u] = frag_tr_asm(tK, dt * 16, u, lane);
+    const bool lane_in = kb + lane < T;
+    const uint64_t in_bits = __ballot(lane_in);
+    const uint64_t ok_bits = __ballot(lane_in && (!has_mask || mk[lane] != 0));
+    const bool all_valid = ok_bits == ~0ull;
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq) {
+      const int q0g = qw + 16 * gq, myq = q0g + li;
+      float* row = tb + (16 * gq + li) * GT3 + left;
+      const bool all_lo = (kb + TK - 1) - q0g <= -left;
+      const bool all_hi = kb - (q0g + 15) >= right;
+      const bool band = !(all_lo || all_hi);
+      if (!band) {
+        const float cb = all_lo ? blo[gq] : bhi[gq];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sc[gq][t][r] = __builtin_amdgcn_exp2f(fmaf(sc[gq][t][r], c2, cb));
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            int d = kb + 16 * t + 4 * g + r - myq;
+            d = d < -left ? -left : (d > right ? right : d);
+            sc[gq][t][r] = __builtin_amdgcn_exp2f(fmaf(sc[gq][t][r] + row[d], c2, nl2[gq]));
+          }
+      }
+      if (!all_valid) {
+        const uint64_t inl = in_bits >> (4 * g), okl = ok_bits >> (4 * g);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int bit = 16 * t + r;
+            const float fill = ((inl >> bit) & 1) ? pm[gq] : 0.f;
+            sc[gq][t][r] = ((okl >> bit) & 1) ? sc[gq][t][r] : fill;
+          }
+      }
+      float bsum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ds = sc[gq][t][r] * (dp[gq][t][r] - dl[gq]);
+          sc[gq][t][r] = ds;
+          bsum += ds;
+        }
+      if (!band) {
+        if (all_lo) glo[gq] += bsum; else ghi[gq] += bsum;
+      } else {
+        // branch-free: clamped bins sum in registers, interior bins go to the slot this key's
+        // bias was just read from, the rest to the spare slot GT3-1 (re-zeroed after the loop)
+        float* spare = row + (GT3 - 1 - left);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int d = kb + 16 * t + 4 * g + r - myq;
+            const bool lo = d <= -left, hi = d >= right;
+            glo[gq] += lo ? sc[gq][t][r] : 0.f;
+            ghi[gq] += hi ? sc[gq][t][r] : 0.f;
+            *((lo || hi) ? spare : row + d) = sc[gq][t][r];
+          }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16x8 pb = pack_acc(sc[gq][2 * u], sc[gq][2 * u + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) dq[gq][dt] = mfma16(ktr[dt][u], pb, dq[gq][dt]);
+      }
+    if (kt + 1 < nkt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < nkt) issue(kt + 2);
+    }
+  }
+  // finish the G rows: register sums of the clamped bins, zeros for interior bins whose key
+  // lies outside [0, nkt·64) (never visited, still holding Q·E)
+  const int kend = nkt * TK;
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    glo[gq] += __shfl_xor(glo[gq], 16, 64);
+    glo[gq] += __shfl_xor(glo[gq], 32, 64);
+    ghi[gq] += __shfl_xor(ghi[gq], 16, 64);
+    ghi[gq] += __shfl_xor(ghi[gq], 32, 64);
+    const int myq = qw + 16 * gq + li;
+    float* row = tb + (16 * gq + li) * GT3;
+    for (int j = 1 + g; j < nrel - 1; j += 4) {
+      const int k = myq + j - left;
+      if (k < 0 || k >= kend) row[j] = 0.f;
+    }
+    if (g == 1) row[GT3 - 1] = 0.f;      // the spare slot
+    if (g == 0) {
+      row[0] = glo[gq];
+      row[nrel - 1] = ghi[gq];
+    }
+  }
+  __syncthreads();                       // ring free: restage E (80 rows) for dQ += G·E
+  stage_E(sm, (const bf16*)a.rel_E, nrel, NREL, tid);
+  __syncthreads();
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const float* row = tb + (16 * gq + li) * GT3;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const f32x4 g0 = *reinterpret_cast<const f32x4*>(row + 32 * u + 4 * g);
+      const f32x4 g1 = *reinterpret_cast<const f32x4*>(row + 32 * u + 16 + 4 * g);
+      const bf16x8 pb = pack_acc(g0, g1);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[gq][dt] = mfma16(frag_tr(sm, dt * 16, u, lane), pb, dq[gq][dt]);
+    }
+    // bins 64..79: one 16x16x16 product (A: E rows 64+4g.., B: this row's G values)
+    const f32x4 gt4 = *reinterpret_cast<const f32x4*>(row + 64 + 4 * g);
+    bf16x4 gb;
+    gb[0] = (bf16)gt4[0]; gb[1] = (bf16)gt4[1]; gb[2] = (bf16)gt4[2]; gb[3] = (bf16)gt4[3];
+    const int q = li >> 2, pq = li & 3;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const s16x4 ea = ds_read_tr16(sm + tr_off(64 + 4 * g + q, dt * 4 + pq));
+      dq[gq][dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ea, __builtin_bit_cast(s16x4, gb), dq[gq][dt], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int myq = qw + 16 * gq + li;
+    if (myq >= T) continue;
+    const int64_t rowid = (int64_t)(b * H + h) * T + myq;
+    const float* row = tb + (16 * gq + li) * GT3;
+    if (a.dE) {
+      float* G = a.gwork + rowid * NREL;
+#pragma unroll
+      for (int c = 0; c < NREL / 16; ++c) {
+        const int j = c * 16 + 4 * g;
+        *reinterpret_cast<f32x4*>(G + j) = *reinterpret_cast<const f32x4*>(row + j);
+      }
+    }
+    bf16* dQ = (bf16*)a.dq + (int64_t)(bT + myq) * a.lddq + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) store_bf16x4(dQ + 16 * dt + 4 * g, dq[gq][dt] * a.scale);
+  }
+}
+
 // ================================================= relative-key backward, v2: dK and dV
 // 4 waves x 32 keys (two 16-key groups sharing every Q/dO fragment read), 128 keys per
 // block, iterating over query tiles of 64 whose Q, dO, lse and delta are staged by
@@ -1388,6 +1674,8 @@ constexpr int KV_E_OFF = 2 * QD;
 constexpr int KV_QE_OFF = KV_E_OFF + NREL * 128;
 constexpr int KV_EDGE_OFF = KV_QE_OFF + 64 * QEW * 4;   // elo[64], ehi[64]
 constexpr int DKV_LDS = KV_EDGE_OFF + 512;
+constexpr int KV_EDGE3_OFF = KV_QE_OFF + 64 * NREL * 4;   // v3: Q·Eᵀ rows of NREL floats
+constexpr int DKV3_LDS = KV_EDGE3_OFF + 512;
 }  // namespace rel2
 
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel2_kernel(ste_attn_args a) {
@@ -1625,8 +1913,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
   }
   const bool any_masked = __ballot(kmask[0] || kmask[1]) != 0;
   char* sE = sm + KV_E_OFF;
-  float* qet = reinterpret_cast<float*>(sm + KV_QE_OFF);
-  float* elo = reinterpret_cast<float*>(sm + KV_EDGE_OFF);
+  float* qet3 = reinterpret_cast<float*>(sm + KV_QE_OFF);
+  float* elo = reinterpret_cast<float*>(sm + KV_EDGE3_OFF);
   float* ehi = elo + 64;
   stage_E(sE, (const bf16*)a.rel_E, nrel, NREL, tid);
 
@@ -1676,19 +1964,20 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
       bf16x8 qfr[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) qfr[s] = frag_kc(tQ, 16 * w, s, lane);
+      // rows of NREL floats, one 16-B store per lane and bin tile (no per-element predicates);
+      // the edge bins are copied to elo/ehi by the row's g == 0 lane after its own stores
+      float* qrow = qet3 + (16 * w + li) * NREL;
 #pragma unroll
       for (int jt = 0; jt < NREL / 16; ++jt) {
         if (!blk_band && jt != 0 && jt != (nrel - 1) / 16) continue;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sE, jt * 16, s, lane), qfr[s], acc);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = jt * 16 + 4 * g + r;
-          if (j < QEW) qet[(16 * w + li) * QEW + j] = acc[r];
-          if (j == 0) elo[16 * w + li] = acc[r] * c2;
-          if (j == nrel - 1) ehi[16 * w + li] = acc[r] * c2;
-        }
+        *reinterpret_cast<f32x4*>(qrow + jt * 16 + 4 * g) = acc;
+      }
+      if (g == 0) {
+        elo[16 * w + li] = qrow[0] * c2;
+        ehi[16 * w + li] = qrow[nrel - 1] * c2;
       }
     }
     __syncthreads();
@@ -1741,7 +2030,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
               const int ql = 16 * n + 4 * g + r;
               int d = mykey - (qb + ql);
               d = d < -left ? -left : (d > right ? right : d);
-              sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r] + qet[ql * QEW + d + left], c2, nl2[n][r]));
+              sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r] + qet3[ql * NREL + d + left], c2, nl2[n][r]));
             }
           }
           if (any_masked && kmask[gk]) {
@@ -1867,6 +2156,16 @@ bool rel_fwd_v3() {
   return v == 1;
 }
 
+// STE_ATTN_DQ=2: the v2 relative-key dQ kernel (A/B comparisons in one process)
+bool rel_dq_v3() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("STE_ATTN_DQ");
+    v = (e && e[0] == '2') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 // STE_ATTN_BWD=2: the v2 relative-key dK/dV kernel (A/B comparisons in one process)
 bool rel_bwd_v3() {
   static int v = -1;
@@ -1921,11 +2220,16 @@ extern "C" int ste_attention_bwd(const ste_attn_args* a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int64_t nrow = (int64_t)a->B * a->T * a->H;
   if (a->rel_E && a->drop_p == 0.f && rel_v2()) {
-    dim3 gq((unsigned)(((a->T + rel2::DQ_Q - 1) / rel2::DQ_Q) * a->H * a->B));
-    hipLaunchKernelGGL(attn_bwd_dq_rel2_kernel, gq, dim3(NT), rel2::DQ_LDS, s, *a);
+    if (rel_dq_v3() && a->rel_left + a->rel_right + 1 < rel2::GT3) {   // bin GT3-1 is the spare slot
+      dim3 gq((unsigned)(((a->T + rel2::DQ3_Q - 1) / rel2::DQ3_Q) * a->H * a->B));
+      hipLaunchKernelGGL(attn_bwd_dq_rel3_kernel, gq, dim3(NT), rel2::DQ3_LDS, s, *a);
+    } else {
+      dim3 gq((unsigned)(((a->T + rel2::DQ_Q - 1) / rel2::DQ_Q) * a->H * a->B));
+      hipLaunchKernelGGL(attn_bwd_dq_rel2_kernel, gq, dim3(NT), rel2::DQ_LDS, s, *a);
+    }
     STE_CHECK_LAUNCH();
     dim3 gk((unsigned)(((a->T + rel2::KB - 1) / rel2::KB) * a->H * a->B));
-    if (rel_bwd_v3()) hipLaunchKernelGGL(attn_bwd_dkv_rel3_kernel, gk, dim3(NT), rel2::DKV_LDS, s, *a);
+    if (rel_bwd_v3()) hipLaunchKernelGGL(attn_bwd_dkv_rel3_kernel, gk, dim3(NT), rel2::DKV3_LDS, s, *a);
     else hipLaunchKernelGGL(attn_bwd_dkv_rel2_kernel, gk, dim3(NT), rel2::DKV_LDS, s, *a);
     STE_CHECK_LAUNCH();
     if (a->dE) {
