@@ -39,6 +39,13 @@ constexpr float NEG_MASK = -3.4028234663852886e38f;
 
 STE_DEV int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
+// clamp(d, lo, hi) in one VALU op (hipcc emits max + min for run-time bounds)
+STE_DEV int med3i(int d, int lo, int hi) {
+  int r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(d), "v"(lo), "v"(hi));
+  return r;
+}
+
 STE_DEV void tile_ld(bf16x8 (&r)[2], const bf16* base, int64_t ld, int bT, int row0, int T, int tid) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -76,13 +83,22 @@ STE_DEV bf16x8 pack_acc(f32x4 a, f32x4 b) {
   return v;
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // low halves of the same accumulator pair: (bf16)(x - hi) for the hi/lo split of P
 STE_DEV bf16x8 pack_acc_lo(f32x4 a, f32x4 b, bf16x8 hi) {
+  // hi back to fp32 straight from the packed words (low half << 16, high half masked), one
+  // v_pk_add_f32 per pair
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 hu = __builtin_bit_cast(u32x4, hi);
+  const f32x4 x[2] = {a, b};
   bf16x8 v;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[i] = (bf16)(a[i] - (float)hi[i]);
-    v[i + 4] = (bf16)(b[i] - (float)hi[i + 4]);
+  for (int w = 0; w < 4; ++w) {
+    const f32x2 h = {__builtin_bit_cast(float, hu[w] << 16), __builtin_bit_cast(float, hu[w] & 0xffff0000u)};
+    const f32x2 d = f32x2{x[w >> 1][2 * (w & 1)], x[w >> 1][2 * (w & 1) + 1]} - h;
+    v[2 * w] = (bf16)d[0];
+    v[2 * w + 1] = (bf16)d[1];
   }
   return v;
 }
@@ -214,7 +230,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(ste_attn_args a) {
           else if (all_hi) bias = qe_hi;
           else {
             int d = kb + kl - myq;
-            d = d < -left ? -left : (d > right ? right : d);
+            d = med3i(d, -left, right);
             bias = qe[li * NREL + d + left];
           }
         }
@@ -388,7 +404,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(ste_attn_args a) {
       for (int r = 0; r < 4; ++r) {
         const int kl = 16 * t + 4 * g + r, key = kb + kl;
         int d = key - myq;
-        d = d < -left ? -left : (d > right ? right : d);
+        d = med3i(d, -left, right);
         float bias = 0.f;
         if (REL) bias = all_lo ? qe_lo : (all_hi ? qe_hi : qe[li * NREL + d + left]);
         float v = (s[t][r] + bias) * a.scale;
@@ -545,7 +561,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(ste_attn_args a) {
         float bias = 0.f;
         if (REL) {
           int d = mykey - q;
-          d = d < -left ? -left : (d > right ? right : d);
+          d = med3i(d, -left, right);
           bias = sQE[ql * NREL + d + left];
         }
         float v = (s[n][r] + bias) * a.scale;
@@ -725,15 +741,15 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = jt * 16 + 4 * g + r;
-        if (j < QEW) qe[(16 * gq + li) * QEW + j] = acc[r];
+        if (j < QEW) qe[(16 * gq + li) * QEW + j] = acc[r] * c2;   // pre-scaled: s·c2 + qe
       }
     }
   __syncthreads();
   float blo[2], bhi[2];
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq) {
-    blo[gq] = qe[(16 * gq + li) * QEW] * c2;
-    bhi[gq] = qe[(16 * gq + li) * QEW + nrel - 1] * c2;
+    blo[gq] = qe[(16 * gq + li) * QEW];
+    bhi[gq] = qe[(16 * gq + li) * QEW + nrel - 1];
   }
 
   char* sMask = sm + MASK_OFF;
@@ -780,15 +796,22 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
     const uint64_t in_bits = __ballot(lane_in);
     const uint64_t ok_bits = __ballot(lane_in && (!has_mask || mk[lane] != 0));
     const bool all_valid = ok_bits == ~0ull;
+    // the lane's 16 keys (16t + 4g + r) as 16-bit patterns: bit 4t + r
+    uint32_t okp = 0xFFFFu, inp = 0xFFFFu;
+    if (!all_valid) {
+      okp = inp = 0u;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        okp |= (uint32_t)((ok_bits >> (16 * t + 4 * g)) & 0xFull) << (4 * t);
+        inp |= (uint32_t)((in_bits >> (16 * t + 4 * g)) & 0xFull) << (4 * t);
+      }
+    }
     f32x4 s[2][4];
 #pragma unroll
     for (int gq = 0; gq < 2; ++gq)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        s[gq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) s[gq][t] = mfma16(kf[t][ss], qf[gq][ss], s[gq][t]);
-      }
+      for (int t = 0; t < 4; ++t)   // first product from an inline-zero accumulator (no v_mov)
+        s[gq][t] = mfma16(kf[t][1], qf[gq][1], mfma16(kf[t][0], qf[gq][0], f32x4{0.f, 0.f, 0.f, 0.f}));
     bf16x8 vf[4][2];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
@@ -799,32 +822,38 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
       const int q0g = qw + 16 * gq, myq = q0g + li;
       const bool all_lo = (kb + TK - 1) - q0g <= -left;
       const bool all_hi = kb - (q0g + 15) >= right;
+      // packed fp32 (v_pk_fma_f32) on the accumulator register pairs
+      const f32x2 c22 = {c2, c2};
       if (all_lo || all_hi) {
         const float bc = all_lo ? blo[gq] : bhi[gq];
+        const f32x2 bc2 = {bc, bc};
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) s[gq][t][r] = fmaf(s[gq][t][r], c2, bc);
+        for (int t = 0; t < 4; ++t) {
+          const f32x2 x0 = __builtin_elementwise_fma(f32x2{s[gq][t][0], s[gq][t][1]}, c22, bc2);
+          const f32x2 x1 = __builtin_elementwise_fma(f32x2{s[gq][t][2], s[gq][t][3]}, c22, bc2);
+          s[gq][t] = f32x4{x0[0], x0[1], x1[0], x1[1]};
+        }
       } else {
         const float* qrow = qe + (16 * gq + li) * QEW + left;
+        const int d0 = kb + 4 * g - myq;
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t) {
+          float qv[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            int d = kb + 16 * t + 4 * g + r - myq;
-            d = d < -left ? -left : (d > right ? right : d);
-            s[gq][t][r] = (s[gq][t][r] + qrow[d]) * c2;
-          }
+          for (int r = 0; r < 4; ++r) qv[r] = qrow[med3i(d0 + 16 * t + r, -left, right)];
+          const f32x2 x0 = __builtin_elementwise_fma(f32x2{s[gq][t][0], s[gq][t][1]}, c22, f32x2{qv[0], qv[1]});
+          const f32x2 x1 = __builtin_elementwise_fma(f32x2{s[gq][t][2], s[gq][t][3]}, c22, f32x2{qv[2], qv[3]});
+          s[gq][t] = f32x4{x0[0], x0[1], x1[0], x1[1]};
+        }
       }
-      if (!all_valid) {  // bit kl of the ballots: key kb+kl in range / unmasked
-        const uint64_t inl = in_bits >> (4 * g), okl = ok_bits >> (4 * g);
+      if (!all_valid) {  // key kb+16t+4g+r in range (inp) / unmasked (okp)
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int bit = 16 * t + r;
-            const float fill = ((inl >> bit) & 1) ? NEG_MASK : -INFINITY;
-            s[gq][t][r] = ((okl >> bit) & 1) ? s[gq][t][r] : fill;
+            const int bit = 4 * t + r;
+            const float fill = ((inp >> bit) & 1u) ? NEG_MASK : -INFINITY;
+            s[gq][t][r] = ((okp >> bit) & 1u) ? s[gq][t][r] : fill;
           }
       }
       float tmax = -INFINITY;
@@ -836,15 +865,18 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mnew = fmaxf(m[gq], tmax);
       const float alpha = __builtin_amdgcn_exp2f(m[gq] - mnew);
-      float psum = 0.f;
+      const f32x2 mn2 = {mnew, mnew};
+      f32x2 ps2 = {0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(s[gq][t][r] - mnew);
-          psum += pv;
-          s[gq][t][r] = pv;
-        }
+      for (int t = 0; t < 4; ++t) {
+        const f32x2 x0 = f32x2{s[gq][t][0], s[gq][t][1]} - mn2;
+        const f32x2 x1 = f32x2{s[gq][t][2], s[gq][t][3]} - mn2;
+        const f32x2 p0 = {__builtin_amdgcn_exp2f(x0[0]), __builtin_amdgcn_exp2f(x0[1])};
+        const f32x2 p1 = {__builtin_amdgcn_exp2f(x1[0]), __builtin_amdgcn_exp2f(x1[1])};
+        ps2 += p0 + p1;
+        s[gq][t] = f32x4{p0[0], p0[1], p1[0], p1[1]};
+      }
+      float psum = ps2[0] + ps2[1];
       psum += __shfl_xor(psum, 16, 64);
       psum += __shfl_xor(psum, 32, 64);
       l[gq] = l[gq] * alpha + psum;
@@ -1289,7 +1321,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel2_kernel(ste_attn_args a
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           int d = kb + 16 * t + 4 * g + r - myq;
-          d = d < -left ? -left : (d > right ? right : d);
+          d = med3i(d, -left, right);
           sc[t][r] = __builtin_amdgcn_exp2f(fmaf(sc[t][r] + qrow[d], c2, nl2));
         }
     }
@@ -1497,15 +1529,14 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
 #pragma unroll
-      for (int gq = 0; gq < 2; ++gq) sc[gq][t] = dp[gq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         const bf16x8 kf = frag_kc(tK, t * 16, ss, lane);
         const bf16x8 vf = frag_kc(tV, t * 16, ss, lane);
 #pragma unroll
         for (int gq = 0; gq < 2; ++gq) {
-          sc[gq][t] = mfma16(kf, qf[gq][ss], sc[gq][t]);
-          dp[gq][t] = mfma16(vf, df[gq][ss], dp[gq][t]);
+          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+          sc[gq][t] = mfma16(kf, qf[gq][ss], ss ? sc[gq][t] : z);
+          dp[gq][t] = mfma16(vf, df[gq][ss], ss ? dp[gq][t] : z);
         }
       }
     }
@@ -1518,6 +1549,15 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
     const uint64_t in_bits = __ballot(lane_in);
     const uint64_t ok_bits = __ballot(lane_in && (!has_mask || mk[lane] != 0));
     const bool all_valid = ok_bits == ~0ull;
+    uint32_t okp = 0xFFFFu, inp = 0xFFFFu;   // bit 4t + r: the lane's key kb+16t+4g+r
+    if (!all_valid) {
+      okp = inp = 0u;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        okp |= (uint32_t)((ok_bits >> (16 * t + 4 * g)) & 0xFull) << (4 * t);
+        inp |= (uint32_t)((in_bits >> (16 * t + 4 * g)) & 0xFull) << (4 * t);
+      }
+    }
 #pragma unroll
     for (int gq = 0; gq < 2; ++gq) {
       const int q0g = qw + 16 * gq, myq = q0g + li;
@@ -1537,19 +1577,18 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             int d = kb + 16 * t + 4 * g + r - myq;
-            d = d < -left ? -left : (d > right ? right : d);
+            d = med3i(d, -left, right);
             sc[gq][t][r] = __builtin_amdgcn_exp2f(fmaf(sc[gq][t][r] + row[d], c2, nl2[gq]));
           }
       }
       if (!all_valid) {
-        const uint64_t inl = in_bits >> (4 * g), okl = ok_bits >> (4 * g);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int bit = 16 * t + r;
-            const float fill = ((inl >> bit) & 1) ? pm[gq] : 0.f;
-            sc[gq][t][r] = ((okl >> bit) & 1) ? sc[gq][t][r] : fill;
+            const int bit = 4 * t + r;
+            const float fill = ((inp >> bit) & 1u) ? pm[gq] : 0.f;
+            sc[gq][t][r] = ((okp >> bit) & 1u) ? sc[gq][t][r] : fill;
           }
       }
       float bsum = 0.f;
@@ -1819,7 +1858,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel2_kernel(ste_attn_args 
           for (int r = 0; r < 4; ++r) {
             const int ql = 16 * n + 4 * g + r;
             int d = mykey - (qb + ql);
-            d = d < -left ? -left : (d > right ? right : d);
+            d = med3i(d, -left, right);
             sc[n][r] = __builtin_amdgcn_exp2f(fmaf(sc[n][r] + qet[ql * QEW + d + left], c2, nl2[n][r]));
           }
       }
@@ -2029,7 +2068,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
             for (int r = 0; r < 4; ++r) {
               const int ql = 16 * n + 4 * g + r;
               int d = mykey - (qb + ql);
-              d = d < -left ? -left : (d > right ? right : d);
+              d = med3i(d, -left, right);
               sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r] + qet3[ql * NREL + d + left], c2, nl2[n][r]));
             }
           }
