@@ -883,11 +883,10 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
       m[gq] = mnew;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int gq = 0; gq < 2; ++gq)
+      // this group's PV right after its softmax: its MFMAs run while the VALU does the next
+      // group's softmax (the transposed V reads were issued before the first softmax)
+      if (gq == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const bf16x8 pb = pack_acc(s[gq][2 * u], s[gq][2 * u + 1]);
@@ -899,6 +898,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
           for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pl, o[gq][dt]);
         }
       }
+    }
     if (kt + 1 < nkt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (this wave's pieces)
       __builtin_amdgcn_s_barrier();                     // ... every wave's, and tile kt fully read
