@@ -125,6 +125,7 @@ class ParamStore:
         self._wt = {}          # (name, count) -> (Wᵀ bf16, param versions, opt_epoch) (see wt())
         self._wq = {}          # (name, count) -> ((W e4m3, E8M0 scales), versions, opt_epoch) (see wq())
         self.opt_epoch = 0     # fused optimizer steps so far (each refreshes the shadow of every trained weight)
+        self._prebuilt = None  # (event, stream, streams that waited): Wᵀ rebuilt by refresh_transposes
         self.sync_shadow(force=True)
 
     # ------------------------------------------------------------------ views
@@ -197,12 +198,43 @@ class ParamStore:
         trained = s.segment in ("enc", "head")
         ent = self._wt.get(key)
         if ent is not None and ent[1] == versions and (not trained or ent[2] == self.opt_epoch):
+            self._wait_prebuilt()
             return ent[0]
         src = self.fused(name, count, "w") if count > 1 else self.w(name)
         dst = ent[0] if ent is not None else None
         dst = ops.transpose16(src, dst)
         self._wt[key] = (dst, versions, self.opt_epoch)
         return dst
+
+    def refresh_transposes(self, stream):
+        """Rebuild on `stream` every cached Wᵀ of a weight the fused optimizer just updated
+        (26 transposes per c2 step), right after the optimizer step, so they overlap the next
+        forward instead of sitting on the backward's critical path.  A stream that later takes
+        one of them from wt() first waits for this work (one event)."""
+        if stream is None or self.device.type != "cuda":
+            return
+        stale = [k for k, ent in self._wt.items()
+                 if ent[2] != self.opt_epoch and self.slots[k[0]].segment in ("enc", "head")]
+        if not stale:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        stream.wait_stream(cur)               # the optimizer's shadow writes
+        with torch.cuda.stream(stream):
+            for name, count in stale:
+                self.wt(name, count)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        self._prebuilt = (ev, stream, set())
+
+    def _wait_prebuilt(self):
+        pb = getattr(self, "_prebuilt", None)
+        if pb is None:
+            return
+        ev, stream, waited = pb
+        cur = torch.cuda.current_stream(self.device)
+        if cur.cuda_stream != stream.cuda_stream and cur.cuda_stream not in waited:
+            cur.wait_event(ev)
+            waited.add(cur.cuda_stream)
 
     def trainable_layer(self, name: str) -> bool:
         return self.slots[name].segment in ("enc", "head")

@@ -566,6 +566,9 @@ class TrainStep:
         self.gradsync.finish()
         self.opt.step(self.sched.factor())  # reference order: optimizer.step() then scheduler.step()
         self.sched.step()
+        # the updated weights' cached Wᵀ (dX GEMM operands) rebuild on the side stream, under
+        # the next forward
+        self.model.store.refresh_transposes(self.model.engine._side_stream())
         self._micro = 0
         self._ids = []
 
