@@ -160,6 +160,14 @@ typedef struct {
 } ste_ln_bwd_args;
 int ste_layernorm_bwd(const ste_ln_bwd_args* a, void* stream);
 
+/* Two chained LayerNorms in one pass over the rows (a Conformer layer's final_layer_norm and
+ * the next layer's ffn1_layer_norm, tf:…wav2vec2_bert…:381-394, 359-362): forward
+ * y2 = LN_b(LN_a(x)) with LN_a's output (which a must also write, a->y) kept in registers for
+ * LN_b (b->x is not read); backward in reverse: b's input gradient, in registers, is a's dy
+ * (a->dy is not read; b->dx optional).  cols <= 1024; every other option per LN as above. */
+int ste_layernorm_fwd_pair(const ste_ln_fwd_args* a, const ste_ln_fwd_args* b, void* stream);
+int ste_layernorm_bwd_pair(const ste_ln_bwd_args* a, const ste_ln_bwd_args* b, void* stream);
+
 /* ------------------------------------------------------------- Attention --
  * Multi-head self-attention core, softmax(QKᵀ·scale + relbias + mask)·V, fused
  * (scores never reach HBM).  Replaces:

@@ -116,6 +116,8 @@ _SIGS = {
     "ste_rows_accumulate": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_float, c_void_p]),
     "ste_layernorm_fwd": (c_int, [C.POINTER(LnFwdArgs), c_void_p]),
     "ste_layernorm_bwd": (c_int, [C.POINTER(LnBwdArgs), c_void_p]),
+    "ste_layernorm_fwd_pair": (c_int, [C.POINTER(LnFwdArgs), C.POINTER(LnFwdArgs), c_void_p]),
+    "ste_layernorm_bwd_pair": (c_int, [C.POINTER(LnBwdArgs), C.POINTER(LnBwdArgs), c_void_p]),
     "ste_attention_fwd": (c_int, [C.POINTER(AttnArgs), c_void_p]),
     "ste_attention_bwd": (c_int, [C.POINTER(AttnArgs), c_void_p]),
     "ste_glu_dwconv_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),

@@ -27,148 +27,178 @@ STE_DEV void load_row(const void* base, bool is_bf16, int64_t ld, int row, int c
   }
 }
 
+// One row of the forward: v holds the row's input values on entry and its output values
+// (after row scale, activation, dropout) on exit; every requested output is written.
+template <int MAXC>
+STE_DEV void ln_fwd_row(const ste_ln_fwd_args& a, int row, int lane, float (&v)[MAXC * 4]) {
+  const float inv_n = 1.0f / (float)a.cols;
+  const uint32_t thresh = (uint32_t)(a.drop_p * 4294967296.0);
+  const float inv_keep = a.drop_p > 0.f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC * 4; ++i) s += v[i];
+  const float mean = wave_sum(s) * inv_n;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int col = (lane + c * 64) * 4;
+    if (col < a.cols) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { float d = v[c * 4 + e] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) * inv_n + a.eps);
+  if (lane == 0) { a.mean[row] = mean; a.rstd[row] = rstd; }
+  const float rs = a.row_scale ? a.row_scale[row] : 1.0f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int col = (lane + c * 64) * 4;
+    if (col >= a.cols) continue;
+    f32x4 g = *reinterpret_cast<const f32x4*>(a.gamma + col);
+    f32x4 b = *reinterpret_cast<const f32x4*>(a.beta + col);
+    f32x4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = ((v[c * 4 + e] - mean) * rstd * g[e] + b[e]) * rs;
+      if (a.act == STE_ACT_SWISH) t = swish_f(t);
+      if (a.drop_p > 0.f) t *= drop_scale(a.seed, (uint64_t)row * a.cols + col + e, thresh, inv_keep);
+      y[e] = t;
+      v[c * 4 + e] = t;
+    }
+    if (a.y) *reinterpret_cast<f32x4*>(a.y + (int64_t)row * a.ldy + col) = y;
+    if (a.yb) store_bf16x4((bf16*)a.yb + (int64_t)row * a.ldyb + col, y);
+    if (a.q8) {  // MX-fp8 copy: 8 lanes x 4 columns = one 32-column block
+      float am = fmaxf(fmaxf(fabsf(y[0]), fabsf(y[1])), fmaxf(fabsf(y[2]), fabsf(y[3])));
+      am = fmaxf(am, __shfl_xor(am, 1));
+      am = fmaxf(am, __shfl_xor(am, 2));
+      am = fmaxf(am, __shfl_xor(am, 4));
+      const int ex = mx8_exp(am);
+      const float inv = ldexpf(1.0f, -ex);
+      uint32_t w = 0;
+      w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(y[0] * inv, -448.f), 448.f),
+                                          fminf(fmaxf(y[1] * inv, -448.f), 448.f), w, false);
+      w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(y[2] * inv, -448.f), 448.f),
+                                          fminf(fmaxf(y[3] * inv, -448.f), 448.f), w, true);
+      *reinterpret_cast<uint32_t*>((uint8_t*)a.q8 + (int64_t)row * a.ldq8 + col) = w;
+      if ((lane & 7) == 0) ((uint8_t*)a.q8s)[(int64_t)row * (a.cols >> 5) + (col >> 5)] = (uint8_t)(ex + 127);
+    }
+  }
+}
+
 template <int MAXC>
 __global__ __launch_bounds__(NT) void ln_fwd_kernel(ste_ln_fwd_args a) {
   const int lane = threadIdx.x & 63;
   const int wave = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * (NT / 64);
-  const float inv_n = 1.0f / (float)a.cols;
-  const uint32_t thresh = (uint32_t)(a.drop_p * 4294967296.0);
-  const float inv_keep = a.drop_p > 0.f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
   for (int row = wave; row < a.rows; row += nwaves) {
     float v[MAXC * 4];
     load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, v);
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < MAXC * 4; ++i) s += v[i];
-    const float mean = wave_sum(s) * inv_n;
-    float q = 0.f;
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      int col = (lane + c * 64) * 4;
-      if (col < a.cols) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { float d = v[c * 4 + e] - mean; q += d * d; }
-      }
-    }
-    const float rstd = rsqrtf(wave_sum(q) * inv_n + a.eps);
-    if (lane == 0) { a.mean[row] = mean; a.rstd[row] = rstd; }
-    const float rs = a.row_scale ? a.row_scale[row] : 1.0f;
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      int col = (lane + c * 64) * 4;
-      if (col >= a.cols) continue;
-      f32x4 g = *reinterpret_cast<const f32x4*>(a.gamma + col);
-      f32x4 b = *reinterpret_cast<const f32x4*>(a.beta + col);
-      f32x4 y;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float t = ((v[c * 4 + e] - mean) * rstd * g[e] + b[e]) * rs;
-        if (a.act == STE_ACT_SWISH) t = swish_f(t);
-        if (a.drop_p > 0.f) t *= drop_scale(a.seed, (uint64_t)row * a.cols + col + e, thresh, inv_keep);
-        y[e] = t;
-      }
-      if (a.y) *reinterpret_cast<f32x4*>(a.y + (int64_t)row * a.ldy + col) = y;
-      if (a.yb) store_bf16x4((bf16*)a.yb + (int64_t)row * a.ldyb + col, y);
-      if (a.q8) {  // MX-fp8 copy: 8 lanes x 4 columns = one 32-column block
-        float am = fmaxf(fmaxf(fabsf(y[0]), fabsf(y[1])), fmaxf(fabsf(y[2]), fabsf(y[3])));
-        am = fmaxf(am, __shfl_xor(am, 1));
-        am = fmaxf(am, __shfl_xor(am, 2));
-        am = fmaxf(am, __shfl_xor(am, 4));
-        const int ex = mx8_exp(am);
-        const float inv = ldexpf(1.0f, -ex);
-        uint32_t w = 0;
-        w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(y[0] * inv, -448.f), 448.f),
-                                            fminf(fmaxf(y[1] * inv, -448.f), 448.f), w, false);
-        w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(y[2] * inv, -448.f), 448.f),
-                                            fminf(fmaxf(y[3] * inv, -448.f), 448.f), w, true);
-        *reinterpret_cast<uint32_t*>((uint8_t*)a.q8 + (int64_t)row * a.ldq8 + col) = w;
-        if ((lane & 7) == 0) ((uint8_t*)a.q8s)[(int64_t)row * (a.cols >> 5) + (col >> 5)] = (uint8_t)(ex + 127);
-      }
-    }
+    ln_fwd_row<MAXC>(a, row, lane, v);
   }
 }
 
-template <int MAXC, bool REDUCE>
-__global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
-  __shared__ float red[REDUCE ? NT / 64 : 1][REDUCE ? MAXC * 4 * 64 : 1];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wave = blockIdx.x * (NT / 64) + wid;
+// Two chained LayerNorms over the same rows, y2 = LN_b(LN_a(x)) (a Conformer layer's final LN
+// and the next layer's FFN1 LN): LN_a's output stays in registers for LN_b, saving LN_b's read
+// of it and a launch.  b.x is not read.
+template <int MAXC>
+__global__ __launch_bounds__(NT) void ln_fwd_pair_kernel(ste_ln_fwd_args a, ste_ln_fwd_args b) {
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * (NT / 64);
+  for (int row = wave; row < a.rows; row += nwaves) {
+    float v[MAXC * 4];
+    load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, v);
+    ln_fwd_row<MAXC>(a, row, lane, v);
+    ln_fwd_row<MAXC>(b, row, lane, v);
+  }
+}
+
+// Column-sum accumulators of one backward (gamma, beta, and the dxb copy's column sums).
+template <int MAXC>
+struct LnAcc {
+  float dg[MAXC * 4], db[MAXC * 4], dsm[MAXC * 4];
+  STE_DEV void zero() {
+#pragma unroll
+    for (int i = 0; i < MAXC * 4; ++i) { dg[i] = 0.f; db[i] = 0.f; dsm[i] = 0.f; }
+  }
+};
+
+// One row of the backward: x holds the input row, g the incoming gradient; on exit g holds
+// this LN's input gradient (dx, dres included); requested outputs are written.
+template <int MAXC>
+STE_DEV void ln_bwd_row(const ste_ln_bwd_args& a, int row, int lane, float (&x)[MAXC * 4], float (&g)[MAXC * 4],
+                        LnAcc<MAXC>& acc) {
   const float inv_n = 1.0f / (float)a.cols;
   const uint32_t thresh = (uint32_t)(a.drop_p * 4294967296.0);
   const float inv_keep = a.drop_p > 0.f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
   const uint32_t in_thresh = (uint32_t)(a.in_drop_p * 4294967296.0);
   const float in_inv_keep = a.in_drop_p > 0.f ? 1.0f / (1.0f - a.in_drop_p) : 1.0f;
-  float dg[MAXC * 4], db[MAXC * 4], dsm[MAXC * 4];
+  const float mean = a.mean[row], rstd = a.rstd[row];
+  const float rs = a.row_scale ? a.row_scale[row] : 1.0f;
+  float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-  for (int i = 0; i < MAXC * 4; ++i) { dg[i] = 0.f; db[i] = 0.f; dsm[i] = 0.f; }
-
-  for (int row = wave; row < a.rows; row += nwaves) {
-    float x[MAXC * 4], g[MAXC * 4];
-    load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, x);
-    load_row<MAXC>(a.dy, a.dy_bf16, a.lddy, row, a.cols, lane, g);
-    const float mean = a.mean[row], rstd = a.rstd[row];
-    const float rs = a.row_scale ? a.row_scale[row] : 1.0f;
-    float s1 = 0.f, s2 = 0.f;
+  for (int c = 0; c < MAXC; ++c) {
+    int col = (lane + c * 64) * 4;
+    if (col >= a.cols) continue;
+    f32x4 gm = *reinterpret_cast<const f32x4*>(a.gamma + col);
+    f32x4 bt = {0.f, 0.f, 0.f, 0.f};
+    if (a.act == STE_ACT_SWISH) bt = *reinterpret_cast<const f32x4*>(a.beta + col);
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      int col = (lane + c * 64) * 4;
-      if (col >= a.cols) continue;
-      f32x4 gm = *reinterpret_cast<const f32x4*>(a.gamma + col);
-      f32x4 bt = {0.f, 0.f, 0.f, 0.f};
-      if (a.act == STE_ACT_SWISH) bt = *reinterpret_cast<const f32x4*>(a.beta + col);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int i = c * 4 + e;
-        const float xh = (x[i] - mean) * rstd;
-        float gi = g[i];
-        if (a.in_drop_p > 0.f) gi *= drop_scale(a.in_seed, (uint64_t)row * a.cols + col + e, in_thresh, in_inv_keep);
-        if (a.act == STE_ACT_SWISH) gi *= swish_d((xh * gm[e] + bt[e]) * rs);
-        gi *= rs;
-        dg[i] += gi * xh;
-        db[i] += gi;
-        const float gg = gi * gm[e];
-        g[i] = gg;
-        x[i] = xh;
-        s1 += gg;
-        s2 += gg * xh;
-      }
-    }
-    s1 = wave_sum(s1) * inv_n;
-    s2 = wave_sum(s2) * inv_n;
-    const float ors = a.out_row_scale ? a.out_row_scale[row] : 1.0f;
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      int col = (lane + c * 64) * 4;
-      if (col >= a.cols) continue;
-      f32x4 d;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int i = c * 4 + e;
-        d[e] = rstd * (g[i] - s1 - x[i] * s2);
-      }
-      if (a.dres) d += *reinterpret_cast<const f32x4*>(a.dres + (int64_t)row * a.lddres + col);
-      if (a.dx) *reinterpret_cast<f32x4*>(a.dx + (int64_t)row * a.lddx + col) = d;
-      if (a.dxb || a.dsum) {
-        f32x4 o = d * (a.out_scale * ors);
-        if (a.drop_p > 0.f) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] *= drop_scale(a.seed, (uint64_t)row * a.cols + col + e, thresh, inv_keep);
-        }
-        if (a.dxb) store_bf16x4((bf16*)a.dxb + (int64_t)row * a.lddxb + col, o);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dsm[c * 4 + e] += o[e];
-      }
+    for (int e = 0; e < 4; ++e) {
+      const int i = c * 4 + e;
+      const float xh = (x[i] - mean) * rstd;
+      float gi = g[i];
+      if (a.in_drop_p > 0.f) gi *= drop_scale(a.in_seed, (uint64_t)row * a.cols + col + e, in_thresh, in_inv_keep);
+      if (a.act == STE_ACT_SWISH) gi *= swish_d((xh * gm[e] + bt[e]) * rs);
+      gi *= rs;
+      acc.dg[i] += gi * xh;
+      acc.db[i] += gi;
+      const float gg = gi * gm[e];
+      g[i] = gg;
+      x[i] = xh;
+      s1 += gg;
+      s2 += gg * xh;
     }
   }
-  if (!REDUCE) return;
-  // three column sums through one LDS array: [wave][c*256 + lane*4 + e] -> column (lane + c*64)*4 + e
+  s1 = wave_sum(s1) * inv_n;
+  s2 = wave_sum(s2) * inv_n;
+  const float ors = a.out_row_scale ? a.out_row_scale[row] : 1.0f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int col = (lane + c * 64) * 4;
+    if (col >= a.cols) continue;
+    f32x4 d;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = c * 4 + e;
+      d[e] = rstd * (g[i] - s1 - x[i] * s2);
+    }
+    if (a.dres) d += *reinterpret_cast<const f32x4*>(a.dres + (int64_t)row * a.lddres + col);
+    if (a.dx) *reinterpret_cast<f32x4*>(a.dx + (int64_t)row * a.lddx + col) = d;
+    if (a.dxb || a.dsum) {
+      f32x4 o = d * (a.out_scale * ors);
+      if (a.drop_p > 0.f) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] *= drop_scale(a.seed, (uint64_t)row * a.cols + col + e, thresh, inv_keep);
+      }
+      if (a.dxb) store_bf16x4((bf16*)a.dxb + (int64_t)row * a.lddxb + col, o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc.dsm[c * 4 + e] += o[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) g[c * 4 + e] = d[e];
+  }
+}
+
+// the block's column sums of one backward through one reused LDS array, one atomic per column
+template <int MAXC>
+STE_DEV void ln_flush(const ste_ln_bwd_args& a, const LnAcc<MAXC>& acc, float (*red)[MAXC * 4 * 64], int lane,
+                      int wid) {
   float* const outs[3] = {a.dgamma, a.dbeta, a.dsum};
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     if (!outs[k]) continue;  // uniform
-    const float* src = k == 0 ? dg : (k == 1 ? db : dsm);
+    const float* src = k == 0 ? acc.dg : (k == 1 ? acc.db : acc.dsm);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < MAXC * 4; ++i) red[wid][(i >> 2) * 256 + lane * 4 + (i & 3)] = src[i];
@@ -182,6 +212,49 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
       for (int w = 0; w < NT / 64; ++w) sum += red[w][j];
       atomicAdd(outs[k] + col, sum);
     }
+  }
+}
+
+template <int MAXC, bool REDUCE>
+__global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
+  __shared__ float red[REDUCE ? NT / 64 : 1][REDUCE ? MAXC * 4 * 64 : 1];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wave = blockIdx.x * (NT / 64) + wid;
+  const int nwaves = gridDim.x * (NT / 64);
+  LnAcc<MAXC> acc;
+  acc.zero();
+  for (int row = wave; row < a.rows; row += nwaves) {
+    float x[MAXC * 4], g[MAXC * 4];
+    load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, x);
+    load_row<MAXC>(a.dy, a.dy_bf16, a.lddy, row, a.cols, lane, g);
+    ln_bwd_row<MAXC>(a, row, lane, x, g, acc);
+  }
+  if constexpr (REDUCE) ln_flush<MAXC>(a, acc, red, lane, wid);
+}
+
+// Backward of the forward pair, in reverse: LN_b's backward (a.dy ignored: its dy is b.dy)
+// produces d(LN_a output) in registers, which is LN_a's incoming gradient.  b.dx may be NULL
+// (the intermediate gradient never touches HBM).
+template <int MAXC, bool REDUCE>
+__global__ __launch_bounds__(NT) void ln_bwd_pair_kernel(ste_ln_bwd_args a, ste_ln_bwd_args b) {
+  __shared__ float red[REDUCE ? NT / 64 : 1][REDUCE ? MAXC * 4 * 64 : 1];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wave = blockIdx.x * (NT / 64) + wid;
+  const int nwaves = gridDim.x * (NT / 64);
+  LnAcc<MAXC> acc_a, acc_b;
+  acc_a.zero();
+  acc_b.zero();
+  for (int row = wave; row < a.rows; row += nwaves) {
+    float x[MAXC * 4], g[MAXC * 4];
+    load_row<MAXC>(b.x, b.x_bf16, b.ldx, row, b.cols, lane, x);
+    load_row<MAXC>(b.dy, b.dy_bf16, b.lddy, row, b.cols, lane, g);
+    ln_bwd_row<MAXC>(b, row, lane, x, g, acc_b);
+    load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, x);
+    ln_bwd_row<MAXC>(a, row, lane, x, g, acc_a);
+  }
+  if constexpr (REDUCE) {
+    ln_flush<MAXC>(b, acc_b, red, lane, wid);
+    ln_flush<MAXC>(a, acc_a, red, lane, wid);
   }
 }
 
@@ -203,6 +276,40 @@ extern "C" int ste_layernorm_fwd(const ste_ln_fwd_args* a, void* stream) {
   if (a->cols <= 256) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(NT), 0, s, *a);
   else if (a->cols <= 1024) hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(NT), 0, s, *a);
   else hipLaunchKernelGGL(ln_fwd_kernel<8>, grid, dim3(NT), 0, s, *a);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_layernorm_fwd_pair(const ste_ln_fwd_args* a, const ste_ln_fwd_args* b, void* stream) {
+  if (!a || !b || a->rows <= 0 || a->cols <= 0 || (a->cols & 3) || a->cols > 1024 || b->rows != a->rows ||
+      b->cols != a->cols || !a->mean || !a->rstd || !b->mean || !b->rstd)
+    return STE_ERR_ARG;
+  for (const ste_ln_fwd_args* t : {a, b})
+    if (t->q8 && (!t->q8s || (t->cols & 127) || t->ldq8 < t->cols || (t->ldq8 & 3) || (((uintptr_t)t->q8) & 3)))
+      return STE_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(grid_for(a->rows));
+  if (a->cols <= 256) hipLaunchKernelGGL(ln_fwd_pair_kernel<1>, grid, dim3(NT), 0, s, *a, *b);
+  else hipLaunchKernelGGL(ln_fwd_pair_kernel<4>, grid, dim3(NT), 0, s, *a, *b);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_layernorm_bwd_pair(const ste_ln_bwd_args* a, const ste_ln_bwd_args* b, void* stream) {
+  if (!a || !b || a->rows <= 0 || a->cols <= 0 || (a->cols & 3) || a->cols > 1024 || b->rows != a->rows ||
+      b->cols != a->cols)
+    return STE_ERR_ARG;
+  if ((a->act == STE_ACT_SWISH && !a->beta) || (b->act == STE_ACT_SWISH && !b->beta)) return STE_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const bool reduce = a->dgamma || a->dbeta || a->dsum || b->dgamma || b->dbeta || b->dsum;
+  const dim3 grid(grid_for(a->rows, reduce ? 512 : 1024));
+  if (a->cols <= 256) {
+    if (reduce) hipLaunchKernelGGL((ln_bwd_pair_kernel<1, true>), grid, dim3(NT), 0, s, *a, *b);
+    else hipLaunchKernelGGL((ln_bwd_pair_kernel<1, false>), grid, dim3(NT), 0, s, *a, *b);
+  } else {
+    if (reduce) hipLaunchKernelGGL((ln_bwd_pair_kernel<4, true>), grid, dim3(NT), 0, s, *a, *b);
+    else hipLaunchKernelGGL((ln_bwd_pair_kernel<4, false>), grid, dim3(NT), 0, s, *a, *b);
+  }
   STE_CHECK_LAUNCH();
   return 0;
 }

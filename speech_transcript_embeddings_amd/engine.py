@@ -65,6 +65,9 @@ class Engine:
         # layerdrop draws (tf:…wav2vec2_bert…:519-522): the global torch RNG unless a trainer sets a
         # generator (TrainStep broadcasts one seed so every data-parallel rank drops the same layers)
         self.layerdrop_gen = None
+        # a Conformer layer's final LN and the next layer's FFN1 LN as one fused pass (forward and
+        # backward, ste_layernorm_*_pair); STE_LN_PAIR=0: separate launches (A/B runs)
+        self.ln_pair = os.environ.get("STE_LN_PAIR", "1") != "0"
 
     @property
     def fp8(self):
@@ -157,23 +160,31 @@ class Engine:
             spec = torch.from_numpy(sm.astype("int32").reshape(-1)).to(self.s.device)
             ops.spec_mask_fwd(x, spec, maskf, self.s.p("audio_encoder.masked_spec_embed"))
         ctx.update(a_b=b, a_T=T, a_maskf=maskf, a_mask32=mask32, a_xin=xin, a_a0=a0, a_st0=st0, a_spec=spec)
-        layers = []
         xb = None
         nl = c.num_hidden_layers
-        for i in range(nl):
-            if train and c.layerdrop > 0 and float(torch.rand([], generator=self.layerdrop_gen)) < c.layerdrop:
-                layers.append(None)
-                continue
+        # layerdrop draws (one per layer, in layer order, as transformers does) made up front so
+        # each layer knows the next one that runs (its FFN1 LN fuses with this layer's final LN)
+        run = [not (train and c.layerdrop > 0 and float(torch.rand([], generator=self.layerdrop_gen)) < c.layerdrop)
+               for _ in range(nl)]
+        order = [i for i in range(nl) if run[i]]
+        layers = [None] * nl
+        pre1 = None
+        for k, i in enumerate(order):
             last = i == nl - 1
-            x, xb, sv = self._conformer_fwd(i, x, b, T, maskf, mask32, train, _site_seed(base_seed, 100 + i), last,
-                                            save)
-            layers.append(sv if save else None)
+            nxt = order[k + 1] if (self.ln_pair and k + 1 < len(order)) else None
+            x, xb, sv, pre1 = self._conformer_fwd(i, x, b, T, maskf, mask32, train, _site_seed(base_seed, 100 + i),
+                                                  last, save, pre1=pre1, nxt=nxt)
+            layers[i] = sv if save else None
         if xb is None:  # the last layer was dropped (only the last layer writes the bf16 copy)
             xb = ops.cast_bf16(x, self._e(M, D, dtype=BF16))
         ctx["a_layers"] = layers
         return x, xb
 
-    def _conformer_fwd(self, i, x, b, T, maskf, mask32, train, seed, want_bf16, save=True):
+    def _conformer_fwd(self, i, x, b, T, maskf, mask32, train, seed, want_bf16, save=True, pre1=None, nxt=None):
+        """One Conformer layer.  pre1 = (a1, a1in, stats): this layer's FFN1 LN, already computed
+        by the previous layer's fused final-LN pair; nxt = index of the next layer that runs
+        (None: none, or no fusion): its FFN1 LN is computed here, fused with this final LN.
+        -> (x5, x5 bf16 or None, saved activations, pre1 of layer nxt)."""
         c = self.acfg
         s = self.s
         pre = f"audio_encoder.encoder.layers.{i}."
@@ -215,8 +226,20 @@ class Engine:
             sv[st] = self._ln(xin, name, eps, yb=y, q8=q, **kw)
             return y, q
 
+        def ln_in_out(name, tr_, **kw):
+            """ln_in's outputs for a LayerNorm computed by a fused pair: (keyword set, a, ain)."""
+            if not fp8:
+                y = self._e(M, D, dtype=BF16)
+                return dict(yb=y, **kw), y, y
+            y = self._e(M, D, dtype=BF16) if (tr_ and save) else None
+            q = (self._e(M, D, dtype=torch.uint8), self._e(M, D // 32, dtype=torch.uint8))
+            return dict(yb=y, q8=q, **kw), y, q
+
         # -- FFN1 (half-step)
-        a1, a1in = ln_in(x, pre + "ffn1_layer_norm", "st1")
+        if pre1 is not None:
+            a1, a1in, sv["st1"] = pre1
+        else:
+            a1, a1in = ln_in(x, pre + "ffn1_layer_norm", "st1")
         z1 = self._e(M, F_, dtype=BF16) if save else None  # swish pre-activation, for backward only
         h1, h1in = ffn_in(a1in, pre + "ffn1.intermediate_dense.weight", pre + "ffn1.intermediate_dense.bias", z1)
         x1 = lin(h1in, pre + "ffn1.output_dense.weight", s.p(pre + "ffn1.output_dense.bias"), alpha=0.5,
@@ -250,24 +273,48 @@ class Engine:
                  residual=x3)
         x5 = self._e(M, D)
         x5b = self._e(M, D, dtype=BF16) if want_bf16 else None
-        sv["st6"] = self._ln(x4, pre + "final_layer_norm", eps, y=x5, yb=x5b)
+        pre_next = None
+        if nxt is None:
+            sv["st6"] = self._ln(x4, pre + "final_layer_norm", eps, y=x5, yb=x5b)
+        else:
+            # this final LN fused with layer nxt's FFN1 LN (x5 stays in registers for the second)
+            prej = f"audio_encoder.encoder.layers.{nxt}.ffn1_layer_norm"
+            trj = s.trainable_layer(f"audio_encoder.encoder.layers.{nxt}.ffn1_layer_norm.weight")
+            second, a1j, a1inj = ln_in_out(prej, trj, gamma=s.p(prej + ".weight"), beta=s.p(prej + ".bias"), eps=eps)
+            sv["st6"], st1j = ops.layernorm_fwd_pair(
+                dict(x=x4, gamma=s.p(pre + "final_layer_norm.weight"), beta=s.p(pre + "final_layer_norm.bias"), eps=eps,
+                     y=x5, yb=x5b), second)
+            pre_next = (a1j, a1inj, st1j)
         sv.update(x=x, z1=z1, x1=x1, qkv=qkv, o=o, o_lo=o_lo, lse=lse, x2=x2, pw1=pw1, cv=cv, x3=x3, z2=z2, x4=x4, p_conv=p_conv)
         if tr:
             sv.update(a1=a1, h1=h1, a2=a2, a3=a3, sw=sw, a5=a5, h2=h2)
-        return x5, x5b, sv
+        return x5, x5b, sv, pre_next
 
-    def _conformer_bwd(self, i, sv, dx5, b, T, maskf, mask32):
+    def _ln_bwd_kw(self, x, stats, name, **kw):
+        """layernorm_bwd keyword set of the named LN (the pair kernels' argument form)."""
+        return dict(x=x, mean=stats[0], rstd=stats[1], gamma=self.s.p(name + ".weight"), beta=self.s.p(name + ".bias"),
+                    dgamma=self.s.g(name + ".weight"), dbeta=self.s.g(name + ".bias"), **kw)
+
+    def _conformer_bwd(self, i, sv, dx5, b, T, maskf, mask32, pending=None):
+        """Backward of one Conformer layer.  pending: the FFN1-LN backward of the layer above
+        (keyword set, dy included), fused here with this layer's final-LN backward; dx5 is then
+        None.  -> (d input or None, this layer's own FFN1-LN backward as a pending keyword set
+        when fusion is on, else None)."""
         c = self.acfg
         s = self.s
         pre = f"audio_encoder.encoder.layers.{i}."
-        M, D, F_ = dx5.shape[0], c.hidden_size, c.intermediate_size
+        M, D, F_ = sv["x4"].shape[0], c.hidden_size, c.intermediate_size
         H = c.num_attention_heads
         tr = sv["tr"]
         # final LN
         dx4 = self._e(M, D)
         dx4b = self._e(M, D, dtype=BF16)
-        self._ln_bwd(dx5, sv["x4"], sv["st6"], pre + "final_layer_norm", dx=dx4, dxb=dx4b, out_scale=0.5,
-                     dsum=s.g(pre + "ffn2.output_dense.bias"))
+        if pending is None:
+            self._ln_bwd(dx5, sv["x4"], sv["st6"], pre + "final_layer_norm", dx=dx4, dxb=dx4b, out_scale=0.5,
+                         dsum=s.g(pre + "ffn2.output_dense.bias"))
+        else:
+            ops.layernorm_bwd_pair(self._ln_bwd_kw(sv["x4"], sv["st6"], pre + "final_layer_norm", dx=dx4, dxb=dx4b,
+                                                   out_scale=0.5, dsum=s.g(pre + "ffn2.output_dense.bias")), pending)
         # FFN2
         dz2 = self._dx(dx4b, pre + "ffn2.output_dense.weight", act=ACT_SWISH_BWD, z=sv["z2"],
                             out_bf16=True, colsum=s.g(pre + "ffn2.intermediate_dense.bias"))
@@ -340,8 +387,17 @@ class Engine:
         if tr:
             self._dw(dz1, sv["a1"], pre + "ffn1.intermediate_dense.weight")
         del dz1
+        kw = self._ln_bwd_kw(sv["x"], sv["st1"], pre + "ffn1_layer_norm", dy=da1, dres=dx1)
+        if self.ln_pair:
+            return None, kw
         dx0 = self._e(M, D)
-        self._ln_bwd(da1, sv["x"], sv["st1"], pre + "ffn1_layer_norm", dres=dx1, dx=dx0)
+        ops.layernorm_bwd(dx=dx0, **kw)
+        return dx0, None
+
+    def _flush_ln(self, pending):
+        """Run a pending FFN1-LN backward on its own -> its input gradient."""
+        dx0 = self._e(*pending["x"].shape)
+        ops.layernorm_bwd(dx=dx0, **pending)
         return dx0
 
     def audio_backward(self, dh, ctx, layers_done=None):
@@ -356,13 +412,18 @@ class Engine:
         lo = next((i for i in range(c.num_hidden_layers)
                    if self.s.trainable_layer(f"audio_encoder.encoder.layers.{i}.ffn1_layer_norm.weight")), None)
         dx = dh
+        pending = None
         for i in reversed(range(c.num_hidden_layers)):
             sv = ctx["a_layers"][i]
             if sv is not None:
-                dx = self._conformer_bwd(i, sv, dx, b, T, maskf, mask32)
+                dx, pending = self._conformer_bwd(i, sv, dx, b, T, maskf, mask32, pending)
                 ctx["a_layers"][i] = None
             if layers_done is not None and i == lo:
+                if pending is not None:   # the lowest trainable layer's FFN1-LN gradients must be final
+                    dx, pending = self._flush_ln(pending), None
                 layers_done()
+        if pending is not None:
+            dx = self._flush_ln(pending)
         s = self.s
         if ctx.get("a_spec") is not None:  # SpecAugment rows: gradient to masked_spec_embed, not the projection
             ops.spec_mask_bwd(dx, ctx["a_spec"], maskf, s.g("audio_encoder.masked_spec_embed"))

@@ -167,16 +167,21 @@ def linear_dw(dy, x, **kw):
 
 
 # -------------------------------------------------------------- LayerNorm
-def layernorm_fwd(x, gamma, beta, eps, *, y=None, yb=None, mean=None, rstd=None, row_scale=None,
-                  act=_lib.ACT_NONE, drop_p=0.0, seed=0, q8=None):
-    rows, cols = x.shape
+def _ln_fwd_struct(x, gamma, beta, eps, y=None, yb=None, mean=None, rstd=None, row_scale=None, act=_lib.ACT_NONE,
+                   drop_p=0.0, seed=0, q8=None, rows=None, cols=None):
+    """-> (LnFwdArgs, mean, rstd, algorithmic bytes).  x may be None (pair kernels: the second
+    LN's input is the first one's output in registers); then rows/cols are given."""
+    if x is not None:
+        rows, cols = x.shape
+    dev = gamma.device
     if mean is None:
-        mean = torch.empty(rows, device=x.device, dtype=F32)
+        mean = torch.empty(rows, device=dev, dtype=F32)
     if rstd is None:
-        rstd = torch.empty(rows, device=x.device, dtype=F32)
+        rstd = torch.empty(rows, device=dev, dtype=F32)
     a = LnFwdArgs()
     a.rows, a.cols = rows, cols
-    a.x, a.ldx, a.x_bf16 = ptr(x), _ld(x), int(x.dtype == BF16)
+    if x is not None:
+        a.x, a.ldx, a.x_bf16 = ptr(x), _ld(x), int(x.dtype == BF16)
     a.gamma, a.beta, a.eps = ptr(gamma), ptr(beta), float(eps)
     if y is not None:
         a.y, a.ldy = ptr(y), _ld(y)
@@ -188,19 +193,38 @@ def layernorm_fwd(x, gamma, beta, eps, *, y=None, yb=None, mean=None, rstd=None,
     if q8 is not None:  # (e4m3 [rows, cols], E8M0 [rows, cols/32]): MX-fp8 copy for ste_gemm_mx8
         a.q8, a.q8s, a.ldq8 = ptr(q8[0]), ptr(q8[1]), _ld(q8[0])
     # algorithmic bytes: read x, write every requested output, 8 B/row of statistics
-    nbytes = rows * cols * (x.element_size() + (4 if y is not None else 0) + (2 if yb is not None else 0) +
-                            (1 + 1 / 32 if q8 is not None else 0)) + 8 * rows + 8 * cols
+    nbytes = rows * cols * ((x.element_size() if x is not None else 0) + (4 if y is not None else 0) +
+                            (2 if yb is not None else 0) + (1 + 1 / 32 if q8 is not None else 0)) + 8 * rows + 8 * cols
+    return a, mean, rstd, nbytes
+
+
+def layernorm_fwd(x, gamma, beta, eps, *, y=None, yb=None, mean=None, rstd=None, row_scale=None,
+                  act=_lib.ACT_NONE, drop_p=0.0, seed=0, q8=None):
+    a, mean, rstd, nbytes = _ln_fwd_struct(x, gamma, beta, eps, y, yb, mean, rstd, row_scale, act, drop_p, seed, q8)
     _traced("layernorm_fwd", nbytes, lambda: call("ste_layernorm_fwd", C.byref(a), _s()))
     return mean, rstd
 
 
-def layernorm_bwd(dy, x, mean, rstd, gamma, *, beta=None, dx=None, dxb=None, dres=None, dgamma=None, dbeta=None,
-                  row_scale=None, act=_lib.ACT_NONE, drop_p=0.0, seed=0, out_scale=1.0, in_drop_p=0.0, in_seed=0,
-                  out_row_scale=None, dsum=None):
+def layernorm_fwd_pair(first: dict, second: dict):
+    """y2 = LN_2(LN_1(x)) in one pass (ste_layernorm_fwd_pair): `first` / `second` are
+    layernorm_fwd keyword sets (x, gamma, beta, eps, y/yb/q8 ...); `second` has no x.  Returns
+    ((mean1, rstd1), (mean2, rstd2))."""
+    a, m1, r1, nb1 = _ln_fwd_struct(**first)
+    b, m2, r2, nb2 = _ln_fwd_struct(None, rows=a.rows, cols=a.cols, **second)
+    _traced("layernorm_fwd", nb1 + nb2, lambda: call("ste_layernorm_fwd_pair", C.byref(a), C.byref(b), _s()))
+    return (m1, r1), (m2, r2)
+
+
+def _ln_bwd_struct(dy, x, mean, rstd, gamma, beta=None, dx=None, dxb=None, dres=None, dgamma=None, dbeta=None,
+                   row_scale=None, act=_lib.ACT_NONE, drop_p=0.0, seed=0, out_scale=1.0, in_drop_p=0.0, in_seed=0,
+                   out_row_scale=None, dsum=None):
+    """-> (LnBwdArgs, algorithmic bytes).  dy may be None (the first LN of a backward pair
+    takes its gradient from the second one's, in registers)."""
     rows, cols = x.shape
     a = LnBwdArgs()
     a.rows, a.cols = rows, cols
-    a.dy, a.lddy, a.dy_bf16 = ptr(dy), _ld(dy), int(dy.dtype == BF16)
+    if dy is not None:
+        a.dy, a.lddy, a.dy_bf16 = ptr(dy), _ld(dy), int(dy.dtype == BF16)
     a.x, a.ldx, a.x_bf16 = ptr(x), _ld(x), int(x.dtype == BF16)
     a.mean, a.rstd, a.gamma, a.beta = ptr(mean), ptr(rstd), ptr(gamma), ptr(beta)
     a.row_scale, a.act = ptr(row_scale), int(act)
@@ -215,10 +239,28 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, *, beta=None, dx=None, dxb=None, dre
     a.in_drop_p, a.in_seed = float(in_drop_p), int(in_seed) & (2**64 - 1)
     a.out_row_scale, a.dsum = ptr(out_row_scale), ptr(dsum)
     # algorithmic bytes: read dy, x (and dres), write dx / dxb, 8 B/row of statistics
-    nbytes = rows * cols * (dy.element_size() + x.element_size() + (4 if dres is not None else 0) +
-                            (4 if dx is not None else 0) + (2 if dxb is not None else 0)) + 8 * rows + 16 * cols
+    nbytes = rows * cols * ((dy.element_size() if dy is not None else 0) + x.element_size() +
+                            (4 if dres is not None else 0) + (4 if dx is not None else 0) +
+                            (2 if dxb is not None else 0)) + 8 * rows + 16 * cols
+    return a, nbytes
+
+
+def layernorm_bwd(dy, x, mean, rstd, gamma, *, beta=None, dx=None, dxb=None, dres=None, dgamma=None, dbeta=None,
+                  row_scale=None, act=_lib.ACT_NONE, drop_p=0.0, seed=0, out_scale=1.0, in_drop_p=0.0, in_seed=0,
+                  out_row_scale=None, dsum=None):
+    a, nbytes = _ln_bwd_struct(dy, x, mean, rstd, gamma, beta, dx, dxb, dres, dgamma, dbeta, row_scale, act, drop_p,
+                               seed, out_scale, in_drop_p, in_seed, out_row_scale, dsum)
     _traced("layernorm_bwd", nbytes, lambda: call("ste_layernorm_bwd", C.byref(a), _s()))
     return dx, dxb
+
+
+def layernorm_bwd_pair(first: dict, second: dict):
+    """Backward of layernorm_fwd_pair in one pass (ste_layernorm_bwd_pair): `second` (the later
+    LN, with its dy) runs first and its input gradient feeds `first` in registers (`first` has
+    no dy; second's dx output is optional).  Keyword sets as layernorm_bwd."""
+    a, nb1 = _ln_bwd_struct(None, **first)
+    b, nb2 = _ln_bwd_struct(**second)
+    _traced("layernorm_bwd", nb1 + nb2, lambda: call("ste_layernorm_bwd_pair", C.byref(a), C.byref(b), _s()))
 
 
 # -------------------------------------------------------------- attention
