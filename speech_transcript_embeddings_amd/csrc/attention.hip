@@ -180,7 +180,9 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(ste_attn_args a) {
   const uint32_t thresh = (uint32_t)(a.drop_p * 4294967296.0);
   const float inv_keep = DROP ? 1.0f / (1.0f - a.drop_p) : 1.0f;
   const uint64_t drow = ((uint64_t)(b * H + h) * T + myq) * (uint64_t)T;
-  const bool split = true;   // P = hi + lo in the PV product (see attn_fwd_rel2_kernel)
+  // P = hi + lo in the PV product when the backward will need O to ~fp32 (o_lo requested, see
+  // attn_fwd_rel2_kernel); forward-only calls keep the single bf16 product
+  const bool split = a.o_lo != nullptr;
 
   float m = -INFINITY, l = 0.f;
   f32x4 o[4];
@@ -697,7 +699,8 @@ STE_DEV bf16x8 frag_tr_asm(const char* t, int cb, int u, int lane) {
   return join_tr(ds_read_tr16_asm(t + tr_off(r0, quad)), ds_read_tr16_asm(t + tr_off(r0 + 16, quad)));
 }
 
-// SPLIT (the launcher always sets it): the PV product runs on P = bf16(P) + bf16(P - bf16(P)),
+// SPLIT (set by the launcher when o_lo is requested, i.e. when a backward follows): the PV
+// product runs on P = bf16(P) + bf16(P - bf16(P)),
 // so O carries ~16 mantissa bits of P.  The backward
 // recomputes P in fp32 and needs delta = Σ_k P_k dP_k = dO·O with THAT P: with near-uniform
 // attention the bf16 rounding of P alone moves O by ~1e-4·|mean V|, which the cancellation in
@@ -2234,12 +2237,14 @@ extern "C" int ste_attention_fwd(const ste_attn_args* a, void* stream) {
   const bool rel = a->rel_E != nullptr, drop = a->drop_p > 0.f;
   if (rel && !drop && rel_v2()) {
     dim3 g2((unsigned)(((a->T + rel2::BQ - 1) / rel2::BQ) * a->H * a->B));
-    // always the hi/lo split of P: training and evaluation forwards then give bit-identical
-    // outputs (the low half of O is written only when o_lo is given)
+    // the hi/lo split of P only when a backward follows (o_lo given); a forward-only call (no_grad
+    // evaluation) saves the second PV product
     if (rel_fwd_v3() && a->rel_left + a->rel_right + 4 <= rel3::TKEYS - 4)
       hipLaunchKernelGGL(attn_fwd_rel3_kernel, g2, dim3(NT), rel3::FWD_LDS, s, *a);
-    else
+    else if (a->o_lo)
       hipLaunchKernelGGL(attn_fwd_rel2_kernel<true>, g2, dim3(NT), rel2::FWD_LDS, s, *a);
+    else
+      hipLaunchKernelGGL(attn_fwd_rel2_kernel<false>, g2, dim3(NT), rel2::FWD_LDS, s, *a);
     STE_CHECK_LAUNCH();
     return 0;
   }

@@ -2,8 +2,9 @@
 (trainer_unfreeze.py:1165-1284) on the HIP path.
 
 * no_grad embeddings (engine.forward(save=False): no saved activations, FFN GEMMs without the
-  pre-activation copy) are bit-identical to the autograd path's, and match the reference's
-  golden embeddings / loss (same 2e-2 bound as test_model_gpu.py);
+  pre-activation copy, attention PV on bf16 P instead of the hi/lo split the backward needs)
+  match the autograd path's within 5e-3 relative and the reference's golden embeddings / loss
+  (same 2e-2 bound as test_model_gpu.py);
 * evaluate() returns the reference's metric keys, computed from the golden s_pos / s_neg with
   the reference's formulas (to_human_readable prob scale, mean / median / std, size-weighted
   loss), over a loader with a None batch (skipped, as in the reference);
@@ -33,9 +34,9 @@ def test_no_grad_embeddings_match_autograd_path_and_golden(tag):
         n_align = model.last_alignment_scores
     assert not any(t.requires_grad for t in n_out)
     for a, b in zip(g_out, n_out):
-        assert torch.equal(a, b)
+        assert rel(b, a.cpu().numpy()) < 5e-3
     if g_align is not None:
-        assert torch.equal(g_align, n_align)
+        assert rel(n_align, g_align.cpu().numpy()) < 5e-3
     for name, t in zip(["txt_pos", "txt_neg", "aud"], n_out):
         assert rel(t, z[name]) < 2e-2, name
 
