@@ -272,6 +272,17 @@ int ste_xattn1_fwd(const float* q, const void* k, const void* v, int64_t ldkv, c
 int ste_xattn1_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs, const float* dout,
                    int B, int S, int P, int nh, float scale, float drop_p, uint64_t seed, float* dq, float* dk,
                    float* dv, int64_t lddkv, void* stream);  /* dk/dv: fp32 rows of stride lddkv, += */
+/* nq (1 or 2) query sets sharing one K/V (the positive and corrupted transcripts' text->audio
+ * calls, ref:training/trainer_unfreeze.py:525-542): query qi of sample b is row qi*B+b of q / out /
+ * dout / dq and of probs [(qi*B+b)*nh + head]*S; query set qi drops with seed_qi, exactly as an
+ * xattn1 call on that set alone.  dk/dv are accumulated once for both sets.  P/nh % 8 == 0,
+ * ldkv % 8 == 0, k/v/out/dq/dk/dv 16-B aligned. */
+int ste_xattn_fwd(const float* q, const void* k, const void* v, int64_t ldkv, const int32_t* mask, int B, int S, int P,
+                  int nh, int nq, float scale, float drop_p, uint64_t seed0, uint64_t seed1, float* probs, float* out,
+                  void* stream);
+int ste_xattn_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs, const float* dout,
+                  int B, int S, int P, int nh, int nq, float scale, float drop_p, uint64_t seed0, uint64_t seed1,
+                  float* dq, float* dk, float* dv, int64_t lddkv, void* stream);
 
 /* WordLevelAlignmentModule attention core (ref:training/trainer_unfreeze.py:214-310, the
  * nn.MultiheadAttention(P, nh=4, batch_first) of :237-242 with key_padding_mask, probs

@@ -192,128 +192,205 @@ __global__ __launch_bounds__(NT) void weighted_pool_bwd_kernel(const float* weig
 
 // ---------------------------------------------------- single-query cross attention
 // scores/probs layout: [B][nh][S]
-__global__ __launch_bounds__(NT) void xattn1_fwd_kernel(const float* q, const bf16* k, const bf16* v, int64_t ldkv,
-                                                      const int32_t* mask, int S, int P, int nh, float scale,
-                                                      float drop_p, uint64_t seed, float* probs, float* out) {
-  extern __shared__ float sp[];  // nh * S
-  __shared__ float sq[1024];
-  __shared__ float red[8];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int dh = P / nh;
-  for (int c = tid; c < P; c += NT) sq[c] = q[(int64_t)b * P + c];
+// CrossModalAttention with NQ single-vector queries per sample sharing the same keys/values
+// (the positive and the corrupted transcript's text->audio calls, ref:525-542, read one audio
+// K/V): one block per (sample, head), so B*nh blocks fill the chip.  Query qi of sample b is
+// row qi*B + b of q / out / dout / dq and of the probs ((qi*B + b)*nh + head)*S; its dropout
+// uses seed qi and the index (b*nh + head)*S + s (the per-call layout of one query set).
+// Rows of K/V are read with 16-B (8 x bf16) loads; the PV / dK / dV passes put 4 columns on a
+// lane and spread the key rows over the block's row groups.
+template <int NQ>
+__global__ __launch_bounds__(NT) void xattn_fwd_kernel(const float* q, const bf16* k, const bf16* v, int64_t ldkv,
+                                                     const int32_t* mask, int B, int S, int P, int nh, float scale,
+                                                     float drop_p, uint64_t seed0, uint64_t seed1, float* probs,
+                                                     float* out) {
+  extern __shared__ float sp[];  // NQ * S
+  __shared__ float sq[NQ][256];
+  __shared__ float red[NQ][NT / 64];
+  __shared__ f32x4 racc[NT];
+  const int b = blockIdx.x, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int dh = P / nh, c0 = hh * dh;
+  for (int c = tid; c < NQ * dh; c += NT) sq[c / dh][c % dh] = q[(int64_t)((c / dh) * B + b) * P + c0 + c % dh];
   __syncthreads();
-  for (int i = tid; i < nh * S; i += NT) {
-    const int hh = i / S, s = i % S;
-    const bf16* kr = k + (int64_t)(b * S + s) * ldkv + hh * dh;
-    float acc = 0.f;
-    for (int d = 0; d < dh; d += 4) {
-      f32x4 x = load_bf16x4(kr + d);
-      acc += x[0] * sq[hh * dh + d] + x[1] * sq[hh * dh + d + 1] + x[2] * sq[hh * dh + d + 2] + x[3] * sq[hh * dh + d + 3];
+  // scores
+  for (int s = tid; s < S; s += NT) {
+    const bf16* kr = k + (int64_t)(b * S + s) * ldkv + c0;
+    float acc[NQ];
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) acc[qi] = 0.f;
+    for (int d = 0; d < dh; d += 8) {
+      const bf16x8 x = *reinterpret_cast<const bf16x8*>(kr + d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int qi = 0; qi < NQ; ++qi) acc[qi] += (float)x[e] * sq[qi][d + e];
     }
-    acc *= scale;
-    if (mask && mask[b * S + s] == 0) acc = -1e9f;
-    sp[i] = acc;
+    const bool masked = mask && mask[b * S + s] == 0;
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) sp[qi * S + s] = masked ? -1e9f : acc[qi] * scale;
   }
   __syncthreads();
-  // softmax per head: wave w handles heads w, w+4, ...
+  // softmax per query over the block
+  float mx[NQ], sm[NQ];
+#pragma unroll
+  for (int qi = 0; qi < NQ; ++qi) {
+    float m = -INFINITY;
+    for (int s = tid; s < S; s += NT) m = fmaxf(m, sp[qi * S + s]);
+    m = wave_max(m);
+    if (lane == 0) red[qi][w] = m;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int qi = 0; qi < NQ; ++qi) {
+    mx[qi] = fmaxf(fmaxf(red[qi][0], red[qi][1]), fmaxf(red[qi][2], red[qi][3]));
+    float t = 0.f;
+    for (int s = tid; s < S; s += NT) t += __expf(sp[qi * S + s] - mx[qi]);
+    sm[qi] = wave_sum(t);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int qi = 0; qi < NQ; ++qi)
+    if (lane == 0) red[qi][w] = sm[qi];
+  __syncthreads();
   const uint32_t thresh = (uint32_t)(drop_p * 4294967296.0);
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
-  for (int hh = w; hh < nh; hh += NT / 64) {
-    float* row = sp + hh * S;
-    float mx = -INFINITY;
-    for (int s = lane; s < S; s += 64) mx = fmaxf(mx, row[s]);
-    mx = wave_max(mx);
-    float sum = 0.f;
-    for (int s = lane; s < S; s += 64) { float e = __expf(row[s] - mx); row[s] = e; sum += e; }
-    sum = wave_sum(sum);
-    const float inv = 1.f / sum;
-    for (int s = lane; s < S; s += 64) {
-      float p = row[s] * inv;
-      probs[((int64_t)b * nh + hh) * S + s] = p;
-      if (drop_p > 0.f) p *= drop_scale(seed, ((uint64_t)b * nh + hh) * S + s, thresh, inv_keep);
-      row[s] = p;
+#pragma unroll
+  for (int qi = 0; qi < NQ; ++qi) {
+    const float inv = 1.f / (red[qi][0] + red[qi][1] + red[qi][2] + red[qi][3]);
+    const uint64_t sd = qi ? seed1 : seed0;
+    float* pr = probs + ((int64_t)(qi * B + b) * nh + hh) * S;
+    for (int s = tid; s < S; s += NT) {
+      float pv = __expf(sp[qi * S + s] - mx[qi]) * inv;
+      pr[s] = pv;
+      if (drop_p > 0.f) pv *= drop_scale(sd, ((uint64_t)b * nh + hh) * S + s, thresh, inv_keep);
+      sp[qi * S + s] = pv;
     }
   }
   __syncthreads();
-  for (int c = tid; c < P; c += NT) {
-    const int hh = c / dh;
-    float acc = 0.f;
-    for (int s = 0; s < S; ++s) acc += sp[hh * S + s] * (float)v[(int64_t)(b * S + s) * ldkv + c];
-    out[(int64_t)b * P + c] = acc;
+  // out = P·V: lane (row group rg, column quad cq)
+  const int nq4 = dh >> 2, RG = NT / nq4;
+  const int cq = tid % nq4, rg = tid / nq4;
+  f32x4 acc[NQ];
+#pragma unroll
+  for (int qi = 0; qi < NQ; ++qi) acc[qi] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (rg < RG)
+    for (int s = rg; s < S; s += RG) {
+      const f32x4 vv = load_bf16x4(v + (int64_t)(b * S + s) * ldkv + c0 + 4 * cq);
+#pragma unroll
+      for (int qi = 0; qi < NQ; ++qi) acc[qi] += vv * sp[qi * S + s];
+    }
+#pragma unroll
+  for (int qi = 0; qi < NQ; ++qi) {
+    racc[tid] = acc[qi];
+    __syncthreads();
+    if (tid < nq4) {
+      f32x4 t = racc[tid];
+      for (int r = 1; r < RG; ++r) t += racc[r * nq4 + tid];
+      *reinterpret_cast<f32x4*>(out + (int64_t)(qi * B + b) * P + c0 + 4 * tid) = t;
+    }
+    __syncthreads();
   }
 }
 
-// dk, dv are fp32 and ACCUMULATED (+=); dq is written.
-// One block per (batch, head): the heads are independent, so B*nh blocks fill the chip
-// (one block per batch row left most CUs idle and serialised S*P work per block).
-// Waves take key rows s = w, w+4, ...; lanes take the head's columns (coalesced rows).
-__global__ __launch_bounds__(NT) void xattn1_bwd_kernel(const float* q, const bf16* k, const bf16* v, int64_t ldkv,
-                                                      const float* probs, const float* dout, int S, int P, int nh,
-                                                      float scale, float drop_p, uint64_t seed, float* dq, float* dk,
-                                                      float* dv, int64_t lddkv) {
-  extern __shared__ float sds[];  // S: dp, then ds
-  __shared__ float sq[256], sdo[256], red[NT / 64][256];
+// dk, dv are fp32 and ACCUMULATED (+=) once for all NQ queries; dq is written.
+template <int NQ>
+__global__ __launch_bounds__(NT) void xattn_bwd_kernel(const float* q, const bf16* k, const bf16* v, int64_t ldkv,
+                                                     const float* probs, const float* dout, int B, int S, int P,
+                                                     int nh, float scale, float drop_p, uint64_t seed0,
+                                                     uint64_t seed1, float* dq, float* dk, float* dv, int64_t lddkv) {
+  extern __shared__ float sds[];  // NQ * S: dp, then ds
+  __shared__ float sq[NQ][256], sdo[NQ][256], red[NQ][NT / 64];
+  __shared__ f32x4 racc[NT];
   const int b = blockIdx.x, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int dh = P / nh, c0 = hh * dh;
   const uint32_t thresh = (uint32_t)(drop_p * 4294967296.0);
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
-  const float* pr = probs + ((int64_t)b * nh + hh) * S;
   const uint64_t drop_base = ((uint64_t)b * nh + hh) * S;
-  for (int c = tid; c < dh; c += NT) { sq[c] = q[(int64_t)b * P + c0 + c]; sdo[c] = dout[(int64_t)b * P + c0 + c]; }
+  for (int c = tid; c < NQ * dh; c += NT) {
+    const int qi = c / dh, cc = c % dh;
+    sq[qi][cc] = q[(int64_t)(qi * B + b) * P + c0 + cc];
+    sdo[qi][cc] = dout[(int64_t)(qi * B + b) * P + c0 + cc];
+  }
   __syncthreads();
-  // dp[s] = v[s]·dout_h  (wave per row, lanes over columns)
-  for (int s = w; s < S; s += NT / 64) {
+  // dp[qi][s] = v[s]·dout_qi (times the dropout scale)
+  for (int s = tid; s < S; s += NT) {
     const bf16* vr = v + (int64_t)(b * S + s) * ldkv + c0;
-    float acc = 0.f;
-    for (int c = lane; c < dh; c += 64) acc += (float)vr[c] * sdo[c];
-    acc = wave_sum(acc);
-    if (lane == 0) {
-      if (drop_p > 0.f) acc *= drop_scale(seed, drop_base + s, thresh, inv_keep);
-      sds[s] = acc;
+    float acc[NQ];
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) acc[qi] = 0.f;
+    for (int d = 0; d < dh; d += 8) {
+      const bf16x8 x = *reinterpret_cast<const bf16x8*>(vr + d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int qi = 0; qi < NQ; ++qi) acc[qi] += (float)x[e] * sdo[qi][d + e];
+    }
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) {
+      if (drop_p > 0.f) acc[qi] *= drop_scale(qi ? seed1 : seed0, drop_base + s, thresh, inv_keep);
+      sds[qi * S + s] = acc[qi];
     }
   }
   __syncthreads();
-  float part = 0.f;
-  for (int s = tid; s < S; s += NT) part += pr[s] * sds[s];
-  part = wave_sum(part);
-  if (lane == 0) red[w][0] = part;
-  __syncthreads();
-  float rowsum = 0.f;
+  float rs[NQ];
 #pragma unroll
-  for (int i = 0; i < NT / 64; ++i) rowsum += red[i][0];
+  for (int qi = 0; qi < NQ; ++qi) {
+    const float* pr = probs + ((int64_t)(qi * B + b) * nh + hh) * S;
+    float part = 0.f;
+    for (int s = tid; s < S; s += NT) part += pr[s] * sds[qi * S + s];
+    part = wave_sum(part);
+    if (lane == 0) red[qi][w] = part;
+  }
   __syncthreads();
-  for (int s = tid; s < S; s += NT) sds[s] = pr[s] * (sds[s] - rowsum) * scale;
-  __syncthreads();
-  // dq[c] = Σ_s ds[s] k[s][c];  dk[s][c] += ds[s] q[c];  dv[s][c] += p'[s] dout[c]
-  float dqa[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int s = w; s < S; s += NT / 64) {
-    const float ds = sds[s];
-    float pd = pr[s];
-    if (drop_p > 0.f) pd *= drop_scale(seed, drop_base + s, thresh, inv_keep);
-    const bf16* kr = k + (int64_t)(b * S + s) * ldkv + c0;
-    float* dkr = dk + (int64_t)(b * S + s) * lddkv + c0;
-    float* dvr = dv + (int64_t)(b * S + s) * lddkv + c0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = lane + 64 * i;
-      if (c < dh) {
-        dqa[i] += ds * (float)kr[c];
-        dkr[c] += ds * sq[c];
-        dvr[c] += pd * sdo[c];
+  for (int qi = 0; qi < NQ; ++qi) rs[qi] = red[qi][0] + red[qi][1] + red[qi][2] + red[qi][3];
+#pragma unroll
+  for (int qi = 0; qi < NQ; ++qi) {
+    const float* pr = probs + ((int64_t)(qi * B + b) * nh + hh) * S;
+    for (int s = tid; s < S; s += NT) sds[qi * S + s] = pr[s] * (sds[qi * S + s] - rs[qi]) * scale;
+  }
+  __syncthreads();
+  // dq[qi] = Σ_s ds k[s];  dk[s] += Σ_qi ds q_qi;  dv[s] += Σ_qi p' dout_qi  (4 columns per lane)
+  const int nq4 = dh >> 2, RG = NT / nq4;
+  const int cq = tid % nq4, rg = tid / nq4, cc = 4 * cq;
+  f32x4 dqa[NQ];
+#pragma unroll
+  for (int qi = 0; qi < NQ; ++qi) dqa[qi] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (rg < RG) {
+    f32x4 qv[NQ], dov[NQ];
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) {
+      qv[qi] = f32x4{sq[qi][cc], sq[qi][cc + 1], sq[qi][cc + 2], sq[qi][cc + 3]};
+      dov[qi] = f32x4{sdo[qi][cc], sdo[qi][cc + 1], sdo[qi][cc + 2], sdo[qi][cc + 3]};
+    }
+    for (int s = rg; s < S; s += RG) {
+      const f32x4 kk = load_bf16x4(k + (int64_t)(b * S + s) * ldkv + c0 + cc);
+      f32x4 dkv = {0.f, 0.f, 0.f, 0.f}, dvv = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qi = 0; qi < NQ; ++qi) {
+        const float ds = sds[qi * S + s];
+        float pd = probs[((int64_t)(qi * B + b) * nh + hh) * S + s];
+        if (drop_p > 0.f) pd *= drop_scale(qi ? seed1 : seed0, drop_base + s, thresh, inv_keep);
+        dqa[qi] += kk * ds;
+        dkv += qv[qi] * ds;
+        dvv += dov[qi] * pd;
       }
+      f32x4* dkr = reinterpret_cast<f32x4*>(dk + (int64_t)(b * S + s) * lddkv + c0 + cc);
+      f32x4* dvr = reinterpret_cast<f32x4*>(dv + (int64_t)(b * S + s) * lddkv + c0 + cc);
+      *dkr += dkv;
+      *dvr += dvv;
     }
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = lane + 64 * i;
-    if (c < dh) red[w][c] = dqa[i];
-  }
-  __syncthreads();
-  for (int c = tid; c < dh; c += NT) {
-    float acc = 0.f;
-#pragma unroll
-    for (int i = 0; i < NT / 64; ++i) acc += red[i][c];
-    dq[(int64_t)b * P + c0 + c] = acc;
+  for (int qi = 0; qi < NQ; ++qi) {
+    racc[tid] = dqa[qi];
+    __syncthreads();
+    if (tid < nq4) {
+      f32x4 t = racc[tid];
+      for (int r = 1; r < RG; ++r) t += racc[r * nq4 + tid];
+      *reinterpret_cast<f32x4*>(dq + (int64_t)(qi * B + b) * P + c0 + 4 * tid) = t;
+    }
+    __syncthreads();
   }
 }
 
@@ -564,26 +641,60 @@ extern "C" int ste_weighted_pool_bwd(const float* weights, const float* dpooled,
   return 0;
 }
 
+namespace {
+bool xattn_shape_ok(int B, int S, int P, int nh, int nq) {
+  if (B <= 0 || S <= 0 || nh <= 0 || P > 1024 || P % nh) return false;
+  const int dh = P / nh;
+  return dh % 8 == 0 && dh <= 256 && nq * S <= 16384;
+}
+}  // namespace
+
+extern "C" int ste_xattn_fwd(const float* q, const void* k, const void* v, int64_t ldkv, const int32_t* mask, int B,
+                             int S, int P, int nh, int nq, float scale, float drop_p, uint64_t seed0, uint64_t seed1,
+                             float* probs, float* out, void* stream) {
+  if (!xattn_shape_ok(B, S, P, nh, nq) || (nq != 1 && nq != 2) || (ldkv & 7) ||
+      (((uintptr_t)k | (uintptr_t)v | (uintptr_t)out) & 15))
+    return STE_ERR_SHAPE;
+  const size_t lds = (size_t)nq * S * sizeof(float);
+  if (nq == 1)
+    hipLaunchKernelGGL(xattn_fwd_kernel<1>, dim3(B, nh), dim3(NT), lds, (hipStream_t)stream, q, (const bf16*)k,
+                       (const bf16*)v, ldkv, mask, B, S, P, nh, scale, drop_p, seed0, seed1, probs, out);
+  else
+    hipLaunchKernelGGL(xattn_fwd_kernel<2>, dim3(B, nh), dim3(NT), lds, (hipStream_t)stream, q, (const bf16*)k,
+                       (const bf16*)v, ldkv, mask, B, S, P, nh, scale, drop_p, seed0, seed1, probs, out);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_xattn_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
+                             const float* dout, int B, int S, int P, int nh, int nq, float scale, float drop_p,
+                             uint64_t seed0, uint64_t seed1, float* dq, float* dk, float* dv, int64_t lddkv,
+                             void* stream) {
+  if (!xattn_shape_ok(B, S, P, nh, nq) || (nq != 1 && nq != 2) || (ldkv & 7) || lddkv < P || (lddkv & 3) ||
+      (((uintptr_t)k | (uintptr_t)v | (uintptr_t)dq | (uintptr_t)dk | (uintptr_t)dv) & 15))
+    return STE_ERR_SHAPE;
+  const size_t lds = (size_t)nq * S * sizeof(float);
+  if (nq == 1)
+    hipLaunchKernelGGL(xattn_bwd_kernel<1>, dim3(B, nh), dim3(NT), lds, (hipStream_t)stream, q, (const bf16*)k,
+                       (const bf16*)v, ldkv, probs, dout, B, S, P, nh, scale, drop_p, seed0, seed1, dq, dk, dv, lddkv);
+  else
+    hipLaunchKernelGGL(xattn_bwd_kernel<2>, dim3(B, nh), dim3(NT), lds, (hipStream_t)stream, q, (const bf16*)k,
+                       (const bf16*)v, ldkv, probs, dout, B, S, P, nh, scale, drop_p, seed0, seed1, dq, dk, dv, lddkv);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int ste_xattn1_fwd(const float* q, const void* k, const void* v, int64_t ldkv, const int32_t* mask, int B,
                               int S, int P, int nh, float scale, float drop_p, uint64_t seed, float* probs, float* out,
                               void* stream) {
-  if (B <= 0 || S <= 0 || P > 1024 || P % nh || (P / nh) % 4 || nh * S > 16384) return STE_ERR_SHAPE;
-  hipLaunchKernelGGL(xattn1_fwd_kernel, dim3(B), dim3(NT), nh * S * sizeof(float), (hipStream_t)stream, q,
-                     (const bf16*)k, (const bf16*)v, ldkv, mask, S, P, nh, scale, drop_p, seed, probs, out);
-  STE_CHECK_LAUNCH();
-  return 0;
+  return ste_xattn_fwd(q, k, v, ldkv, mask, B, S, P, nh, 1, scale, drop_p, seed, seed, probs, out, stream);
 }
 
 extern "C" int ste_xattn1_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
                               const float* dout, int B, int S, int P, int nh, float scale, float drop_p, uint64_t seed,
                               float* dq, float* dk, float* dv, int64_t lddkv, void* stream) {
-  if (B <= 0 || S <= 0 || P > 1024 || P % nh || (P / nh) % 4 || P / nh > 256 || S > 16384 || lddkv < P)
-    return STE_ERR_SHAPE;
-  hipLaunchKernelGGL(xattn1_bwd_kernel, dim3(B, nh), dim3(NT), S * sizeof(float), (hipStream_t)stream, q,
-                     (const bf16*)k, (const bf16*)v, ldkv, probs, dout, S, P, nh, scale, drop_p, seed, dq, dk, dv,
-                     lddkv);
-  STE_CHECK_LAUNCH();
-  return 0;
+  return ste_xattn_bwd(q, k, v, ldkv, probs, dout, B, S, P, nh, 1, scale, drop_p, seed, seed, dq, dk, dv, lddkv,
+                       stream);
 }
 
 extern "C" int ste_l2norm_fwd(const float* x, int rows, int cols, float* y, float* norms, void* stream) {

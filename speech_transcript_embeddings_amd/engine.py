@@ -678,11 +678,9 @@ class Engine:
             probs_t = self._e(nb * nh * T)
             att_t = self._e(nb, P)
             seed_t = _site_seed(base_seed, 203)
-            for half in range(2):  # pos rows, neg rows: same audio keys
-                r0 = half * b
-                ops.xattn1_fwd(qt[r0:r0 + b], kva[:, :P], kva[:, P:], ctx["a_mask32"], b, T, nh,
-                               probs_t[r0 * nh * T:(r0 + b) * nh * T], att_t[r0:r0 + b], drop_p=p_x,
-                               seed=_site_seed(seed_t, half))
+            # pos rows, neg rows: one launch over the shared audio keys (each half keeps its own seed)
+            ops.xattn_fwd(qt, kva[:, :P], kva[:, P:], ctx["a_mask32"], b, T, nh, probs_t, att_t,
+                          (_site_seed(seed_t, 0), _site_seed(seed_t, 1)), drop_p=p_x)
             att_tb = ops.cast_bf16(att_t, self._e(nb, P, dtype=BF16))
             ops.linear(att_tb, s.w("text_to_audio_attention.out_proj.weight"),
                        s.p("text_to_audio_attention.out_proj.bias"), out=tcat[:, P:])
@@ -754,12 +752,9 @@ class Engine:
             self._db(datt, "text_to_audio_attention.out_proj.bias")
             dqt = self._e(nb, P)
             dkv = self._z(ab * T, 2 * P)
-            for half in range(2):
-                r0 = half * b
-                ops.xattn1_bwd(hs["qt"][r0:r0 + b], hs["kva"][:, :P], hs["kva"][:, P:],
-                               hs["probs_t"][r0 * nh * T:(r0 + b) * nh * T], dq_in[r0:r0 + b], b, T, nh,
-                               dqt[r0:r0 + b], dkv[:, :P], dkv[:, P:], drop_p=hs["p_x"],
-                               seed=_site_seed(hs["seed_t"], half))
+            ops.xattn_bwd(hs["qt"], hs["kva"][:, :P], hs["kva"][:, P:], hs["probs_t"], dq_in, b, T, nh, dqt,
+                          dkv[:, :P], dkv[:, P:], (_site_seed(hs["seed_t"], 0), _site_seed(hs["seed_t"], 1)),
+                          drop_p=hs["p_x"])
             dqtb = ops.cast_bf16(dqt, self._e(nb, P, dtype=BF16))
             ops.linear_dx(dqtb, s.w("text_to_audio_attention.query.weight"), out=d_tproj, beta=1.0)
             self._dw(dqtb, hs["tprojb"], "text_to_audio_attention.query.weight")

@@ -373,6 +373,24 @@ def xattn1_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, drop_p=0.0, seed=0):
          float((P // nh) ** -0.5), float(drop_p), int(seed) & (2**64 - 1), ptr(dq), ptr(dk), ptr(dv), _ld(dk), _s())
 
 
+def xattn_fwd(q, k, v, mask, B, S, nh, probs, out, seeds, drop_p=0.0):
+    """len(seeds) query sets sharing K/V: q / out rows qi*B + b, probs [(qi*B + b)*nh + h]*S."""
+    P = q.shape[-1]
+    nq = len(seeds)
+    assert q.shape[0] == nq * B and out.shape[0] == nq * B and probs.numel() >= nq * B * nh * S
+    call("ste_xattn_fwd", ptr(q), ptr(k), ptr(v), _ld(k), ptr(mask), B, S, P, nh, nq, float((P // nh) ** -0.5),
+         float(drop_p), int(seeds[0]) & (2**64 - 1), int(seeds[-1]) & (2**64 - 1), ptr(probs), ptr(out), _s())
+
+
+def xattn_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, seeds, drop_p=0.0):
+    P = q.shape[-1]
+    nq = len(seeds)
+    assert _ld(dk) == _ld(dv) and q.shape[0] == nq * B and dq.shape[0] == nq * B and dout.shape[0] == nq * B
+    call("ste_xattn_bwd", ptr(q), ptr(k), ptr(v), _ld(k), ptr(probs), ptr(dout), B, S, P, nh, nq,
+         float((P // nh) ** -0.5), float(drop_p), int(seeds[0]) & (2**64 - 1), int(seeds[-1]) & (2**64 - 1),
+         ptr(dq), ptr(dk), ptr(dv), _ld(dk), _s())
+
+
 def align_attn_fwd(q, kv, kmask, B, L, T, nh, probs, out, drop_p=0.0, seed=0):
     P = kv.shape[-1] // 2
     call("ste_align_attn_fwd", ptr(q), _ld(q), ptr(kv), _ld(kv), ptr(kmask), B, L, T, P, nh, float(drop_p),

@@ -570,6 +570,48 @@ def test_xattn1(ops, drop_p):
     assert rel_err(dv, vr.grad) < 1e-5
 
 
+@pytest.mark.parametrize("B,S,P,nh,drop_p", [(3, 40, 256, 8, 0.0), (4, 499, 768, 8, 0.1)])
+def test_xattn_two_query_sets(ops, B, S, P, nh, drop_p):
+    """Positive + corrupted transcript queries over one audio K/V in one launch (engine's
+    text->audio call, ref:training/trainer_unfreeze.py:525-542): each set equals its own
+    single-query attention with its own dropout seed; dK/dV are the sum over both sets."""
+    torch.manual_seed(S)
+    q = torch.randn(2 * B, P, device=DEV)
+    kv = torch.randn(B * S, 2 * P, device=DEV).bfloat16()
+    k, v = kv[:, :P], kv[:, P:]
+    mask = torch.ones(B * S, dtype=torch.int32, device=DEV)
+    mask[S - 9:S] = 0
+    probs = torch.empty(2 * B * nh * S, device=DEV)
+    out = torch.empty(2 * B, P, device=DEV)
+    seeds = (1234, 777)
+    ops.xattn_fwd(q, k, v, mask, B, S, nh, probs, out, seeds, drop_p=drop_p)
+    d = P // nh
+    qr = q.clone().requires_grad_()
+    kr = k.float().clone().requires_grad_()
+    vr = v.float().clone().requires_grad_()
+    kh = kr.view(B, S, nh, d).transpose(1, 2)
+    vh = vr.view(B, S, nh, d).transpose(1, 2)
+    refs = []
+    for qi in range(2):
+        qh = qr[qi * B:(qi + 1) * B].view(B, 1, nh, d).transpose(1, 2)
+        a = (qh @ kh.transpose(-2, -1)) * d ** -0.5
+        a = a.masked_fill(mask.view(B, 1, 1, S) == 0, -1e9).softmax(-1)
+        if drop_p > 0:
+            idx = np.arange(B * nh * S).astype(np.uint64)
+            a = a * torch.from_numpy(drop_scale(seeds[qi], idx, drop_p)).to(DEV).view(B, nh, 1, S)
+        refs.append((a @ vh).transpose(1, 2).reshape(B, P))
+    ref = torch.cat(refs)
+    assert rel_err(out, ref) < 1e-5
+    do = torch.randn(2 * B, P, device=DEV)
+    ref.backward(do)
+    dq = torch.empty(2 * B, P, device=DEV)
+    dkv = torch.zeros(B * S, 2 * P, device=DEV)
+    ops.xattn_bwd(q, k, v, probs, do, B, S, nh, dq, dkv[:, :P], dkv[:, P:], seeds, drop_p=drop_p)
+    assert rel_err(dq, qr.grad) < 1e-5
+    assert rel_err(dkv[:, :P], kr.grad) < 1e-5
+    assert rel_err(dkv[:, P:], vr.grad) < 1e-5
+
+
 @pytest.mark.parametrize("B,L,T,P,drop_p", [(2, 12, 49, 128, 0.0), (3, 64, 499, 768, 0.0), (2, 20, 130, 256, 0.1)])
 def test_align_attn(ops, B, L, T, P, drop_p):
     """WordLevelAlignmentModule's nn.MultiheadAttention core (4 heads, key padding mask,
