@@ -20,6 +20,7 @@
 // "swapped" products (Sᵀ = K·Qᵀ) keep the softmax row on the lane, and accumulator
 // tiles feed the next MFMA directly as B operands (no LDS round trip for P or dS).
 #include <cstdlib>
+#include <type_traits>
 #include "common.h"
 #include "../../include/ste.h"
 
@@ -932,32 +933,71 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
   }
 }
 
-// ============================================== relative-key forward, v3 (audio self-attention)
-// Same block shape, K/V ring and hi/lo P split as v2, with the per-score vector work cut down
-// (rel2 measured ~17 VALU instructions per score, more than its MFMA time):
-//  * the relative term comes from a per-query-row BIAS TABLE built once per block: row q holds
-//    c2·Q_q·E[clamp(k - q) + left] for the 88 keys k in [ks - 4, ks + 84), ks = floor4(q - left),
-//    already clamped and scaled, so a lane's 4 consecutive keys read one aligned float4 (offset
-//    clamped into the table: keys before it are bin 0, keys after it the last bin).  Row stride
-//    92 floats keeps the 16 rows of a read on distinct banks;
-//  * every score is then one FMA (s·c2 + bias) before the max; out-of-band tiles use the row's
-//    constant edge bias; key masks / keys past T are applied only on tiles that have such keys;
-//  * the running max is rescaled lazily (only when some row of the group grew) and row sums stay
-//    per lane until the end.
-namespace rel3 {
+// ============================================== relative-key forward, v4 (audio self-attention)
+// rel2's block shape (4 waves x 32 queries, two 16-row groups sharing every K/V fragment, 64-key
+// tiles in a 2-deep global_load_lds ring) with the per-score vector work cut down — rel2 spent
+// ~16 VALU instructions per score against 1.5 MFMA per 32 scores:
+//  * row max / row sum across the 4 lane groups of a query by v_permlane16/32_swap (rel2:
+//    ds_bpermute + index arithmetic + an lgkmcnt(0) drain per step);
+//  * the running max is raised only when some row of the group grew by more than 2^8 (deferred
+//    rescale): O and l are rescaled on those tiles only, probabilities stay <= 256;
+//  * per-tile key-validity words (in range and unmasked) are ballots made once per block, so a
+//    fully valid tile costs one LDS read and no mask work;
+//  * the relative term reads a padded Q·Eᵀ row: entry e holds the (scaled) bin clamp(e-3), so the
+//    4 consecutive keys of a lane need one clamped base (v_med3) and two ds_read2_b32, never a
+//    per-score clamp or address;
+//  * transposed V reads carry their tile offsets as instruction immediates.
+namespace rel4 {
 constexpr int WQ = 32, BQ = 128;
-constexpr int TW = 92;                     // bias-table row stride (floats); 92 mod 64 = 28
-constexpr int TKEYS = 88;                  // keys per row: [ks - 4, ks + 84)
+constexpr int QS = 82;                     // padded Q·Eᵀ row stride (floats), entry e <-> bin e - PADL
+constexpr int PADL = 3;
+constexpr int MAXT = 64;                   // key tiles of 64 (T <= 4096)
 constexpr int KV = 2 * TILE;
-constexpr int MASK_OFF = 2 * KV;
-constexpr int TAB_OFF = MASK_OFF + 512;
-constexpr int FWD_LDS = TAB_OFF + 4 * WQ * TW * 4;   // 80,384 B: two blocks per CU
+constexpr int OKW_OFF = 2 * KV;            // MAXT 64-bit validity words
+constexpr int QE_OFF = OKW_OFF + MAXT * 8;
+constexpr int FWD_LDS = QE_OFF + 4 * WQ * QS * 4;   // 74,752 B: two blocks per CU
+constexpr float THRESH = 8.f;              // deferred rescale: p <= 2^THRESH
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
-}  // namespace rel3
+constexpr int max_nrel() { return QS - 2 * PADL - 1; }   // entries up to bin nrel + 3
+}  // namespace rel4
 
-__global__ __launch_bounds__(NT, 2) void attn_fwd_rel3_kernel(ste_attn_args a) {
-  using namespace rel3;
+// v_max3_f32 without the canonicalising v_max hipcc puts in front of fmaxf on MFMA results
+STE_DEV float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// max / sum over the 4 lanes {l, l^16, l^32, l^48} (one query row of the swapped layout)
+STE_DEV float rowmax4(float x) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  const float y = max3f(__builtin_bit_cast(float, (uint32_t)p[0]), __builtin_bit_cast(float, (uint32_t)p[1]),
+                        __builtin_bit_cast(float, (uint32_t)p[1]));
+  const uint32_t v = __builtin_bit_cast(uint32_t, y);
+  auto q = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return max3f(__builtin_bit_cast(float, (uint32_t)q[0]), __builtin_bit_cast(float, (uint32_t)q[1]),
+               __builtin_bit_cast(float, (uint32_t)q[1]));
+}
+STE_DEV float rowsum4(float x) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  float y = __builtin_bit_cast(float, (uint32_t)p[0]) + __builtin_bit_cast(float, (uint32_t)p[1]);
+  const uint32_t v = __builtin_bit_cast(uint32_t, y);
+  auto q = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return __builtin_bit_cast(float, (uint32_t)q[0]) + __builtin_bit_cast(float, (uint32_t)q[1]);
+}
+// ds_read_b64_tr_b16 with an immediate byte offset (asm: see ds_read_tr16_asm)
+template <int OFF>
+STE_DEV s16x4 ds_read_tr16_off(uint32_t addr) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF) : "memory");
+  return r;
+}
+
+template <bool SPLIT>
+__global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
+  using namespace rel4;
   extern __shared__ __attribute__((aligned(16))) char sm[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -971,58 +1011,9 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel3_kernel(ste_attn_args a) {
   const bf16* Vb = (const bf16*)a.v + h * HD;
   const int qw = tile * BQ + w * WQ;
   const float c2 = a.scale * LOG2E;
-
-  bf16x8 qf[2][2];
-#pragma unroll
-  for (int gq = 0; gq < 2; ++gq)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int q = qw + 16 * gq + li;
-      qf[gq][s] = q < T ? *reinterpret_cast<const bf16x8*>(Qb + (int64_t)(bT + q) * a.ldq + 32 * s + 8 * g) : bf16x8{};
-    }
-  // ---- bias table: E staged over the ring (free until tile 0), Q·Eᵀ on the MFMA, scattered
-  // into each row's clamped key window
-  float* tab = reinterpret_cast<float*>(sm + TAB_OFF) + w * WQ * TW;
-  stage_E(sm, (const bf16*)a.rel_E, nrel, NREL, tid);
-  __syncthreads();
-#pragma unroll
-  for (int gq = 0; gq < 2; ++gq) {
-    const int q = qw + 16 * gq + li;
-    const int ks = (q - left) - ((q - left) & 3);
-    float* row = tab + (16 * gq + li) * TW;
-#pragma unroll
-    for (int jt = 0; jt < NREL / 16; ++jt) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sm, jt * 16, s, lane), qf[gq][s], acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = jt * 16 + 4 * g + r;
-        const float v = acc[r] * c2;
-        if (j == 0) {                              // keys <= q - left: idx 0 .. q - left - ks + 4
-          for (int i = 0; i <= q - left - ks + 4; ++i) row[i] = v;
-        } else if (j == nrel - 1) {                // keys >= q + right
-          for (int i = q + right - ks + 4; i < TKEYS; ++i) row[i] = v;
-        } else if (j < nrel - 1) {
-          row[j - left + q - ks + 4] = v;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  float blo[2], bhi[2];
-  int ksr[2];
-#pragma unroll
-  for (int gq = 0; gq < 2; ++gq) {
-    const int q = qw + 16 * gq + li;
-    ksr[gq] = (q - left) - ((q - left) & 3);
-    blo[gq] = tab[(16 * gq + li) * TW];
-    bhi[gq] = tab[(16 * gq + li) * TW + TKEYS - 1];
-  }
-
-  char* sMask = sm + MASK_OFF;
   const int nkt = (T + TK - 1) / TK;
-  const bool has_mask = a.key_mask != nullptr;
+
+  // wave w stages K pieces 2w,2w+1 and V pieces 2w,2w+1 of each tile
   auto issue = [&](int kt) {
     char* buf = sm + (kt & 1) * KV;
     const int kb = kt * TK;
@@ -1030,29 +1021,105 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel3_kernel(ste_attn_args a) {
     glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w + 1, lane);
     glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w, lane);
     glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w + 1, lane);
-    if (w == 0 && has_mask) glds_mask(a.key_mask, bT, kb, T, sMask + (kt & 1) * 256, lane);
   };
+  // prologue: every global read is issued up front and waited once (the first two K/V tiles by
+  // DMA, Q and E fragments and the key-mask flags into registers)
   issue(0);
   if (nkt > 1) issue(1);
-  if (nkt > 1) {
-    if (w == 0 && has_mask) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bf16x8 qf[2][2], ef[NREL / 16][2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int q = qw + 16 * gq + li;
+      qf[gq][s] = q < T ? *reinterpret_cast<const bf16x8*>(Qb + (int64_t)(bT + q) * a.ldq + 32 * s + 8 * g) : bf16x8{};
+    }
+#pragma unroll
+  for (int jt = 0; jt < NREL / 16; ++jt)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {   // E row jt*16 + li as the A operand (rows >= nrel: zero)
+      const int j = jt * 16 + li;
+      ef[jt][s] = j < nrel ? *reinterpret_cast<const bf16x8*>((const bf16*)a.rel_E + j * HD + 32 * s + 8 * g)
+                           : bf16x8{};
+    }
+  // key-validity words: bit j of word kt = key 64kt+j is < T and unmasked
+  uint64_t* okw = reinterpret_cast<uint64_t*>(sm + OKW_OFF);
+  for (int kt = w; kt < nkt; kt += 4) {
+    const int key = kt * TK + lane;
+    const bool ok = key < T && (a.key_mask == nullptr || a.key_mask[bT + key] != 0);
+    const uint64_t word = __ballot(ok);
+    if (lane == 0) okw[kt] = word;
   }
-  __builtin_amdgcn_s_barrier();
+  // padded, pre-scaled Q·Eᵀ rows of the wave's 32 queries: entry PADL + j = bin j,
+  // entries 0..PADL-1 replicate bin 0 and PADL+nrel.. replicate bin nrel-1
+  float* qe = reinterpret_cast<float*>(sm + QE_OFF) + w * WQ * QS;
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int jt = 0; jt < NREL / 16; ++jt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) acc = mfma16(ef[jt][s], qf[gq][s], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = jt * 16 + 4 * g + r;
+        if (j < nrel) qe[(16 * gq + li) * QS + PADL + j] = acc[r] * c2;
+      }
+    }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (lane < WQ) {   // one row per lane
+    float* row = qe + lane * QS;
+    const float e0 = row[PADL], e1 = row[PADL + nrel - 1];
+#pragma unroll
+    for (int e = 0; e < PADL; ++e) row[e] = e0;
+    for (int e = PADL + nrel; e < QS; ++e) row[e] = e1;
+  }
+  float blo[2], bhi[2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    blo[gq] = qe[(16 * gq + li) * QS + PADL];
+    bhi[gq] = qe[(16 * gq + li) * QS + PADL + nrel - 1];
+  }
+  if (nkt > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // tile 0 landed (this wave's pieces)
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();   // every wave's tile-0 pieces, validity words and table rows
 
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-  f32x4 o[2][4];
+  // lane constants of the transposed V reads: frag_tr's rows 32u+4g+q (+16), column quad 4dt+p
+  const int tq = li >> 2, tp = li & 3, r0 = 4 * g + tq;
+  uint32_t voff[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) voff[dt] = (uint32_t)tr_off(r0, 4 * dt + tp);
+  typedef __attribute__((address_space(3))) const char lds_cchar;
+  const uint32_t sm_base = (uint32_t)(uintptr_t)(lds_cchar*)sm;
+
+  // the table's LDS offset as an opaque value: hipcc would fold the constant into each read's
+  // immediate, where it does not fit ds_read2_b32's 8-bit offsets (an extra add per read)
+  int qe_off = QE_OFF;
+  asm volatile("" : "+s"(qe_off));
+  auto okw_of = [&](int kt) -> uint64_t {   // wave-uniform: into scalar registers
+    const uint64_t v = okw[kt];
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
+  };
+  float m[2] = {-INFINITY, -INFINITY};
+  f32x4 o[2][4], lsum[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq)
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int kt = 0; kt < nkt; ++kt) {
-    const char* tK = sm + (kt & 1) * KV;
-    const char* tV = tK + TILE;
-    const int* mk = reinterpret_cast<const int*>(sMask + (kt & 1) * 256);
+  // one key tile; MASKED: the tile has keys past T or masked keys (separate straight-line code,
+  // so the common fully valid tile carries no select work and no branch-merge copies)
+  auto tile_step = [&](const int kt, auto masked_c) {
+    constexpr bool MASKED = decltype(masked_c)::value;
+    const int slot = kt & 1;
+    const char* tK = sm + slot * KV;
+    const uint32_t vbase = sm_base + slot * KV + TILE;
     const int kb = kt * TK;
     bf16x8 kf[4][2];
 #pragma unroll
@@ -1063,23 +1130,18 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel3_kernel(ste_attn_args a) {
 #pragma unroll
     for (int gq = 0; gq < 2; ++gq)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        s[gq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) s[gq][t] = mfma16(kf[t][ss], qf[gq][ss], s[gq][t]);
-      }
+      for (int t = 0; t < 4; ++t)
+        s[gq][t] = mfma16(kf[t][1], qf[gq][1], mfma16(kf[t][0], qf[gq][0], f32x4{0.f, 0.f, 0.f, 0.f}));
     bf16x8 vf[4][2];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) vf[dt][u] = frag_tr_asm(tV, dt * 16, u, lane);
-    // keys past T or masked: this lane's 4 keys per t as additive fills (wave-uniform test)
-    const bool tail = kb + TK > T;
-    const bool masked_tile = has_mask && __ballot(mk[lane] == 0) != 0;
-    const bool fix = tail || masked_tile;
+    for (int dt = 0; dt < 4; ++dt) {
+      const uint32_t va = vbase + voff[dt];
+      vf[dt][0] = join_tr(ds_read_tr16_off<0>(va), ds_read_tr16_off<16 * 128>(va));
+      vf[dt][1] = join_tr(ds_read_tr16_off<32 * 128>(va), ds_read_tr16_off<48 * 128>(va));
+    }
 #pragma unroll
     for (int gq = 0; gq < 2; ++gq) {
-      const int q0g = qw + 16 * gq;
+      const int q0g = qw + 16 * gq, myq = q0g + li;
       const bool all_lo = (kb + TK - 1) - q0g <= -left;
       const bool all_hi = kb - (q0g + 15) >= right;
       if (all_lo || all_hi) {
@@ -1087,84 +1149,87 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel3_kernel(ste_attn_args a) {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s[gq][t][r] = fmaf(s[gq][t][r], c2, bc);
+          for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_fmaf(s[gq][t][r], c2, bc);
       } else {
-        const float* row = tab + (16 * gq + li) * TW;
+        const float* qrow = reinterpret_cast<const float*>(sm + qe_off) + (w * WQ + 16 * gq + li) * QS + PADL;
+        const int d0 = kb + 4 * g - myq + left;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const int off = min(max(kb + 16 * t + 4 * g - ksr[gq] + 4, 0), TKEYS - 4);
-          const f32x4 bt = *reinterpret_cast<const f32x4*>(row + off);
+          const float* qp = qrow + med3i(d0 + 16 * t, -PADL, nrel);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s[gq][t][r] = fmaf(s[gq][t][r], c2, bt[r]);
+          for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_fmaf(s[gq][t][r], c2, qp[r]);
         }
       }
-      if (fix) {
+      if constexpr (MASKED) {   // key kb+16t+4g+r: past T -> -inf, masked -> finfo.min (as rel2)
+        const uint64_t okb = okw_of(kt);
+        const uint32_t wlo = (uint32_t)(okb >> (4 * g)), whi = (uint32_t)(okb >> (32 + 4 * g));
+        const int lim = T - kb - 4 * g;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int k0 = 16 * t + 4 * g;
-          int4 mw = has_mask ? *reinterpret_cast<const int4*>(mk + k0) : int4{1, 1, 1, 1};
-          const int mv[4] = {mw.x, mw.y, mw.z, mw.w};
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float fill = (kb + k0 + r < T) ? NEG_MASK : -INFINITY;
-            s[gq][t][r] = (kb + k0 + r < T && mv[r] != 0) ? s[gq][t][r] : fill;
+            const uint32_t wd = t < 2 ? wlo : whi;
+            const bool ok = (wd >> (16 * (t & 1) + r)) & 1u;
+            const float fill = 16 * t + r < lim ? NEG_MASK : -INFINITY;
+            s[gq][t][r] = ok ? s[gq][t][r] : fill;
           }
-        }
       }
-      float tmax = fmaxf(fmaxf(fmaxf(s[gq][0][0], s[gq][0][1]), fmaxf(s[gq][0][2], s[gq][0][3])),
-                         fmaxf(fmaxf(s[gq][1][0], s[gq][1][1]), fmaxf(s[gq][1][2], s[gq][1][3])));
-      tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(s[gq][2][0], s[gq][2][1]), fmaxf(s[gq][2][2], s[gq][2][3])),
-                               fmaxf(fmaxf(s[gq][3][0], s[gq][3][1]), fmaxf(s[gq][3][2], s[gq][3][3]))));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      if (__ballot(tmax > m[gq]) != 0) {   // some row's max grew: rescale (alpha = 1 elsewhere)
+      float tmax = max3f(s[gq][0][0], s[gq][0][1], s[gq][0][2]);
+      tmax = max3f(tmax, s[gq][0][3], s[gq][1][0]);
+      tmax = max3f(tmax, s[gq][1][1], s[gq][1][2]);
+      tmax = max3f(tmax, s[gq][1][3], s[gq][2][0]);
+      tmax = max3f(tmax, s[gq][2][1], s[gq][2][2]);
+      tmax = max3f(tmax, s[gq][2][3], s[gq][3][0]);
+      tmax = max3f(tmax, s[gq][3][1], s[gq][3][2]);
+      tmax = rowmax4(max3f(tmax, s[gq][3][3], tmax));
+      // deferred rescale: raise the running max only when a row grew past m + THRESH
+      if (__builtin_amdgcn_ballot_w64(tmax > m[gq] + THRESH) != 0ull) {
         const float mnew = fmaxf(m[gq], tmax);
         const float alpha = __builtin_amdgcn_exp2f(m[gq] - mnew);
-        l[gq] *= alpha;
+        lsum[gq] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
         m[gq] = mnew;
       }
-      float psum = 0.f;
+      const float mg = m[gq];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(s[gq][t][r] - m[gq]);
-          psum += pv;
-          s[gq][t][r] = pv;
-        }
-      l[gq] += psum;   // per-lane partial: reduced across the row's 4 lanes at the end
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int gq = 0; gq < 2; ++gq)
+        for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_amdgcn_exp2f(s[gq][t][r] - mg);
+      if (gq == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const bf16x8 pb = pack_acc(s[gq][2 * u], s[gq][2 * u + 1]);
-        const bf16x8 pl = pack_acc_lo(s[gq][2 * u], s[gq][2 * u + 1], pb);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pb, o[gq][dt]);
+        lsum[gq] = mfma16(ones, pb, lsum[gq]);   // row sum of the same (rounded) P, on the MFMA
+        if (SPLIT) {
+          const bf16x8 pl = pack_acc_lo(s[gq][2 * u], s[gq][2 * u + 1], pb);
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pl, o[gq][dt]);
+          for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pl, o[gq][dt]);
+          lsum[gq] = mfma16(ones, pl, lsum[gq]);
+        }
       }
+    }
     if (kt + 1 < nkt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (this wave's pieces)
       __builtin_amdgcn_s_barrier();                     // ... every wave's, and tile kt fully read
       if (kt + 2 < nkt) issue(kt + 2);
     }
+  };
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (okw_of(kt) == ~0ull) tile_step(kt, std::false_type{});
+    else tile_step(kt, std::true_type{});
   }
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq) {
-    float lt = l[gq];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    const float lt = lsum[gq][0];   // every accumulator row holds the full row sum
     const int myq = qw + 16 * gq + li;
     if (myq < T) {
       const float inv_l = 1.0f / lt;
       bf16* O = (bf16*)a.o + (int64_t)(bT + myq) * a.ldo + h * HD;
-      if (a.o_lo) {
+      if (SPLIT && a.o_lo) {
         bf16* Ol = (bf16*)a.o_lo + (int64_t)(bT + myq) * a.ldolo + h * HD;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
@@ -1173,12 +1238,12 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel3_kernel(ste_attn_args a) {
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) store_bf16x4(O + 16 * dt + 4 * g, o[gq][dt] * inv_l);
       }
+      // natural-log LSE; a row whose every key is masked is stored as -inf (see rel2)
       if (g == 0)
         a.lse[(int64_t)(b * H + h) * T + myq] = m[gq] == NEG_MASK ? -INFINITY : (m[gq] + log2f(lt)) * LN2;
     }
   }
 }
-
 // ====================================== relative-key backward, v2: dQ (+ delta, + bins G)
 // 4 waves x 16 queries, K/V ring as in the forward.  delta = rowsum(dO*O) is computed here
 // from the wave's own dO/O fragments (no separate pass) and written for the dK/dV kernel.
@@ -2187,13 +2252,12 @@ bool rel_v2() {
   return v == 1;
 }
 
-// STE_ATTN_FWD=3: the v3 relative-key forward (bias table; measured 5 % slower than v2 at c2,
-// kept for A/B work)
-bool rel_fwd_v3() {
+// STE_ATTN_FWD=2: the v2 relative-key forward instead of v4 (A/B comparisons in one process)
+bool rel_fwd_v4() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("STE_ATTN_FWD");
-    v = (e && e[0] == '3') ? 1 : 0;
+    const char* e = getenv("STE_ATTN_FWD");   // "2": the rel2 forward
+    v = (e && e[0] == '2') ? 0 : 1;
   }
   return v == 1;
 }
@@ -2239,9 +2303,10 @@ extern "C" int ste_attention_fwd(const ste_attn_args* a, void* stream) {
     dim3 g2((unsigned)(((a->T + rel2::BQ - 1) / rel2::BQ) * a->H * a->B));
     // the hi/lo split of P only when a backward follows (o_lo given); a forward-only call (no_grad
     // evaluation) saves the second PV product
-    if (rel_fwd_v3() && a->rel_left + a->rel_right + 4 <= rel3::TKEYS - 4)
-      hipLaunchKernelGGL(attn_fwd_rel3_kernel, g2, dim3(NT), rel3::FWD_LDS, s, *a);
-    else if (a->o_lo)
+    if (rel_fwd_v4() && a->rel_left + a->rel_right + 1 <= rel4::max_nrel() && a->T <= rel4::MAXT * TK) {
+      if (a->o_lo) hipLaunchKernelGGL(attn_fwd_rel4_kernel<true>, g2, dim3(NT), rel4::FWD_LDS, s, *a);
+      else hipLaunchKernelGGL(attn_fwd_rel4_kernel<false>, g2, dim3(NT), rel4::FWD_LDS, s, *a);
+    } else if (a->o_lo)
       hipLaunchKernelGGL(attn_fwd_rel2_kernel<true>, g2, dim3(NT), rel2::FWD_LDS, s, *a);
     else
       hipLaunchKernelGGL(attn_fwd_rel2_kernel<false>, g2, dim3(NT), rel2::FWD_LDS, s, *a);
