@@ -296,16 +296,23 @@ def main(argv=None):
                 step(*d)
             assert step._micro == 0, "an optimizer step per timed step"
 
-    for _ in range(args.warmup):
-        run()
+    # the step's own stream at the highest priority: the text encoder's side stream (normal
+    # priority) then fills CUs the audio chain leaves idle instead of competing for them
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    ops.GEMM_TRACE, ops.HBM_TRACE = [], []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize()
+    prio = os.environ.get("STE_MAIN_PRIORITY", "1") != "0"
+    main_stream = torch.cuda.Stream(priority=torch.cuda.Stream.priority_range()[1]) if prio else \
+        torch.cuda.current_stream()
+    with torch.cuda.stream(main_stream):
+        for _ in range(args.warmup):
+            run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ops.GEMM_TRACE, ops.HBM_TRACE = [], []
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run()
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0

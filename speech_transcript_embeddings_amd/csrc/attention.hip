@@ -1511,8 +1511,38 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
   const int qw = tile * DQ3_Q + w * DQ3_WQ;
   const float c2 = a.scale * LOG2E;
 
-  bf16x8 qf[2][2], df[2][2];
+  char* sMask = sm + MASK_OFF;
+  const int nkt = (T + TK - 1) / TK;
+  const bool has_mask = a.key_mask != nullptr;
+  auto issue = [&](int kt) {
+    char* buf = sm + (kt & 1) * KV;
+    const int kb = kt * TK;
+    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w, lane);
+    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w + 1, lane);
+    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w, lane);
+    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w + 1, lane);
+    if (w == 0 && has_mask) glds_mask(a.key_mask, bT, kb, T, sMask + (kt & 1) * 256, lane);
+  };
+  // E rows (80, clamped to nrel-1: finite, and the G entries they meet are zero) into a free ring
+  // slot for the closing dQ += G·E product: wave w stages pieces w, w+4, w+8
+  auto issue_E = [&](char* slot) {
+    for (int pc = w; pc < NREL / 8; pc += 4)
+      glds_tile_piece((const bf16*)a.rel_E, HD, 0, 0, nrel, slot, pc, lane);
+  };
+  // prologue: the first K/V tiles by DMA, then every register operand, waited once
+  issue(0);
+  if (nkt > 1) issue(1);
+  else issue_E(sm + KV);
+  bf16x8 qf[2][2], df[2][2], ef[NREL / 16][2];
   float dl[2], nl2[2], pm[2];
+#pragma unroll
+  for (int jt = 0; jt < NREL / 16; ++jt)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {   // E row jt*16 + li as the A operand of Q·Eᵀ (rows >= nrel: zero)
+      const int j = jt * 16 + li;
+      ef[jt][s] = j < nrel ? *reinterpret_cast<const bf16x8*>((const bf16*)a.rel_E + j * HD + 32 * s + 8 * g)
+                           : bf16x8{};
+    }
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq) {
     const int myq = qw + 16 * gq + li;
@@ -1529,8 +1559,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
 #pragma unroll
       for (int e = 0; e < 8; ++e) dpart += (float)df[gq][s][e] * ((float)of[e] + (float)ol[e]);
     }
-    dpart += __shfl_xor(dpart, 16, 64);
-    dpart += __shfl_xor(dpart, 32, 64);
+    dpart = rowsum4(dpart);
     dl[gq] = dpart;
     const int64_t rowid = (int64_t)(b * H + h) * T + myq;
     if (qv && g == 0) a.delta[rowid] = dpart;
@@ -1539,47 +1568,33 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
     pm[gq] = lse == -INFINITY ? 1.0f / T : 0.f;
   }
 
+  // raw Q·Eᵀ rows of the wave's 32 queries (wave-private)
   float* tb = reinterpret_cast<float*>(sm + DQ3_T_OFF) + w * DQ3_WQ * GT3;
-  stage_E(sm, (const bf16*)a.rel_E, nrel, NREL, tid);
-  __syncthreads();
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq)
 #pragma unroll
     for (int jt = 0; jt < NREL / 16; ++jt) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sm, jt * 16, s, lane), qf[gq][s], acc);
+      for (int s = 0; s < 2; ++s) acc = mfma16(ef[jt][s], qf[gq][s], acc);
       *reinterpret_cast<f32x4*>(tb + (16 * gq + li) * GT3 + jt * 16 + 4 * g) = acc;
     }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   float blo[2], bhi[2];
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq) {
     blo[gq] = tb[(16 * gq + li) * GT3] * c2 + nl2[gq];
     bhi[gq] = tb[(16 * gq + li) * GT3 + nrel - 1] * c2 + nl2[gq];
   }
-
-  char* sMask = sm + MASK_OFF;
-  const int nkt = (T + TK - 1) / TK;
-  const bool has_mask = a.key_mask != nullptr;
-  auto issue = [&](int kt) {
-    char* buf = sm + (kt & 1) * KV;
-    const int kb = kt * TK;
-    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w, lane);
-    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w + 1, lane);
-    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w, lane);
-    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w + 1, lane);
-    if (w == 0 && has_mask) glds_mask(a.key_mask, bT, kb, T, sMask + (kt & 1) * 256, lane);
-  };
-  issue(0);
-  if (nkt > 1) issue(1);
   if (nkt > 1) {
     if (w == 0 && has_mask) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  __builtin_amdgcn_s_barrier();
+  __syncthreads();   // every wave's tile-0 pieces
 
   f32x4 dq[2][4];
 #pragma unroll
@@ -1702,15 +1717,15 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
       if (kt + 2 < nkt) issue(kt + 2);
     }
   }
+  // tile nkt-2's slot has been free since the last in-loop barrier: E for the closing product
+  if (nkt > 1) issue_E(sm + (nkt & 1) * KV);
   // finish the G rows: register sums of the clamped bins, zeros for interior bins whose key
   // lies outside [0, nkt·64) (never visited, still holding Q·E)
   const int kend = nkt * TK;
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq) {
-    glo[gq] += __shfl_xor(glo[gq], 16, 64);
-    glo[gq] += __shfl_xor(glo[gq], 32, 64);
-    ghi[gq] += __shfl_xor(ghi[gq], 16, 64);
-    ghi[gq] += __shfl_xor(ghi[gq], 32, 64);
+    glo[gq] = rowsum4(glo[gq]);
+    ghi[gq] = rowsum4(ghi[gq]);
     const int myq = qw + 16 * gq + li;
     float* row = tb + (16 * gq + li) * GT3;
     for (int j = 1 + g; j < nrel - 1; j += 4) {
@@ -1723,9 +1738,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
       row[nrel - 1] = ghi[gq];
     }
   }
-  __syncthreads();                       // ring free: restage E (80 rows) for dQ += G·E
-  stage_E(sm, (const bf16*)a.rel_E, nrel, NREL, tid);
-  __syncthreads();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's E pieces
+  __syncthreads();                                    // every wave's (and the G rows)
+  const char* sE = sm + (nkt & 1) * KV;               // the slot issue_E filled
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq) {
     const float* row = tb + (16 * gq + li) * GT3;
@@ -1735,7 +1750,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
       const f32x4 g1 = *reinterpret_cast<const f32x4*>(row + 32 * u + 16 + 4 * g);
       const bf16x8 pb = pack_acc(g0, g1);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) dq[gq][dt] = mfma16(frag_tr(sm, dt * 16, u, lane), pb, dq[gq][dt]);
+      for (int dt = 0; dt < 4; ++dt) dq[gq][dt] = mfma16(frag_tr(sE, dt * 16, u, lane), pb, dq[gq][dt]);
     }
     // bins 64..79: one 16x16x16 product (A: E rows 64+4g.., B: this row's G values)
     const f32x4 gt4 = *reinterpret_cast<const f32x4*>(row + 64 + 4 * g);
@@ -1744,7 +1759,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
     const int q = li >> 2, pq = li & 3;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      const s16x4 ea = ds_read_tr16(sm + tr_off(64 + 4 * g + q, dt * 4 + pq));
+      const s16x4 ea = ds_read_tr16(sE + tr_off(64 + 4 * g + q, dt * 4 + pq));
       dq[gq][dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ea, __builtin_bit_cast(s16x4, gb), dq[gq][dt], 0, 0, 0);
     }
   }
