@@ -200,8 +200,9 @@ __global__ __launch_bounds__(128) void fbank_stats_kernel(const int32_t* __restr
   const int len = lengths[b];
   const int F = len >= FRAME ? 1 + (len - FRAME) / HOP : 0;
   const float* x = work + (int64_t)b * Fmax * NMEL + m;
-  // the sums must run frame by frame in order (numpy's rounding); loads go 16 frames ahead
-  constexpr int U = 16;
+  // the sums must run frame by frame in order (numpy's rounding); loads go 48 frames ahead
+  // (the chain is load-latency bound; vmcnt holds at most 63 loads in flight)
+  constexpr int U = 48;
   float s = 0.f;
   for (int f0 = 0; f0 < F; f0 += U) {
     float v[U];
@@ -262,6 +263,25 @@ __global__ __launch_bounds__(256) void fbank_norm_kernel(const int32_t* __restri
   }
 }
 
+// The constant tables (twiddles, window, mel filters) depend on nothing but the extractor's
+// parameters: built once per device into module memory by a single-block launch, then shared by
+// every call (the build runs serial fp64 loops: ~40 us that used to be paid per batch).
+__device__ float g_fbank_tab[TABLE_FLOATS];
+
+const float* fbank_tables(hipStream_t s) {
+  static const float* tab[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!tab[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_fbank_tab)) != hipSuccess) return nullptr;
+    hipLaunchKernelGGL(fbank_tables_kernel, dim3(1), dim3(256), 0, s, (float*)p);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return nullptr;
+    tab[dev] = (const float*)p;
+  }
+  return tab[dev];
+}
+
 }  // namespace
 
 extern "C" int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* lengths, int B, int Tmax, float pad_value,
@@ -269,10 +289,9 @@ extern "C" int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* length
   if (B <= 0 || Tmax <= 0 || !wav || !lengths || !feats || !mask || !work) return STE_ERR_ARG;
   const int Fmax = 2 * Tmax;
   hipStream_t s = (hipStream_t)stream;
-  float* tab = work;
+  const float* tab = fbank_tables(s);
+  if (!tab) return STE_ERR_ARG;
   float* logmel = work + TABLE_FLOATS;
-  hipLaunchKernelGGL(fbank_tables_kernel, dim3(1), dim3(256), 0, s, tab);
-  STE_CHECK_LAUNCH();
   const int fpb = 4 * FRAMES_PER_WAVE;
   hipLaunchKernelGGL(fbank_logmel_kernel, dim3((Fmax + fpb - 1) / fpb, B), dim3(256), 0, s, wav, ld_wav, lengths,
                      Fmax, tab, logmel);
