@@ -99,9 +99,19 @@ __global__ __launch_bounds__(NT) void glu_dwconv_bwd_kernel(const bf16* __restri
   __shared__ float sw[CC * K];
   float (*sd)[CC] = reinterpret_cast<float (*)[CC]>(lds);              // dout rows t0 .. t0+TT+K-2
   float (*sg)[CC] = reinterpret_cast<float (*)[CC]>(lds + ROWS * CC);  // g rows t0-(K-1) .. t0+TT-1 (DW only)
-  const int b = blockIdx.z, t0 = blockIdx.x * TT, c0 = blockIdx.y * CC;
+  const int b = blockIdx.z, c0 = blockIdx.y * CC;
   const int tid = threadIdx.x;
+  const int c = tid & (CC - 1), rg = tid >> 6;
   for (int i = tid; i < CC * K; i += NT) sw[i] = w[c0 * K + i];
+  float dwp[DW ? K : 1];
+#pragma unroll
+  for (int k = 0; k < (DW ? K : 1); ++k) dwp[k] = 0.f;
+  // DW: a block walks several 64-row tiles (grid.x < tiles) and keeps its dW partials in
+  // registers across them, so each (channel, tap) address takes one atomic per block, not per tile
+  const int ntile = (T + TT - 1) / TT;
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+  const int t0 = tile * TT;
+  __syncthreads();   // sw staged / the previous tile's LDS reads done
   for (int i = tid; i < ROWS * (CC / 8); i += NT) {  // 16-B loads of 8 channels
     const int r = i / (CC / 8), c8 = (i % (CC / 8)) * 8;
     const int td = t0 + r;
@@ -122,13 +132,9 @@ __global__ __launch_bounds__(NT) void glu_dwconv_bwd_kernel(const bf16* __restri
     }
   }
   __syncthreads();
-  const int c = tid & (CC - 1), rg = tid >> 6;
   float wk[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) wk[k] = sw[c * K + k];
-  float dwp[DW ? K : 1];
-#pragma unroll
-  for (int k = 0; k < (DW ? K : 1); ++k) dwp[k] = 0.f;
   const int rbeg = rg * RPT;
   // register windows of the thread's RPT + K - 1 staged rows (one LDS read per row)
   float dwin[RPT + K - 1], gwin[DW ? RPT + K - 1 : 1];
@@ -174,6 +180,7 @@ __global__ __launch_bounds__(NT) void glu_dwconv_bwd_kernel(const bf16* __restri
     *reinterpret_cast<bf16x8*>(dpre + row * 2 * C + c0 + c8) = da;
     *reinterpret_cast<bf16x8*>(dpre + row * 2 * C + C + c0 + c8) = dgate;
   }
+  }  // row tiles
   if (!DW) return;
   // reduce the 4 row groups' partials through the (now free) staging LDS: [rg][c][K+1]
   __syncthreads();
@@ -206,9 +213,14 @@ extern "C" int ste_glu_dwconv_bwd(const void* pre, const float* w, const void* d
                                   int T, int C, int K, void* stream) {
   if (B <= 0 || T <= 0 || C <= 0 || (C % CC) != 0 || K != KMAX) return STE_ERR_SHAPE;
   dim3 grid((T + TT - 1) / TT, C / CC, B);
-  if (dw)
+  if (dw) {
+    // ~8 row tiles per block: 8x fewer same-address atomics on dW (their contention, not the
+    // arithmetic, was most of this variant's time), still >= 2 blocks per CU at B = 64
+    const unsigned per = 8;   // measured 1/2/4/8/24 tiles: 237/200/196/186/188 us at T = 499
+    grid.x = (grid.x + per - 1) / per;
     hipLaunchKernelGGL((glu_dwconv_bwd_kernel<KMAX, true>), grid, dim3(NT), 0, (hipStream_t)stream, (const bf16*)pre,
                        w, (const bf16*)dout, (bf16*)dpre, dw, T, C);
+  }
   else
     hipLaunchKernelGGL((glu_dwconv_bwd_kernel<KMAX, false>), grid, dim3(NT), 0, (hipStream_t)stream, (const bf16*)pre,
                        w, (const bf16*)dout, (bf16*)dpre, dw, T, C);

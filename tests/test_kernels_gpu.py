@@ -351,7 +351,7 @@ def test_attention_text(ops, drop_p):
 
 
 # ---------------------------------------------------------------- conv
-@pytest.mark.parametrize("T,Cc", [(37, 128), (150, 128), (37, 256), (499, 512), (300, 1024)])
+@pytest.mark.parametrize("T,Cc", [(37, 128), (150, 128), (37, 256), (499, 512), (300, 1024), (1499, 128)])
 def test_glu_dwconv(ops, T, Cc):
     torch.manual_seed(T)
     B = 2
