@@ -56,7 +56,7 @@ def main():
         return e0.elapsed_time(e1) * 1e3 / a.iters
 
     for name, (K, N, epi) in cases.items():
-        if a.only and a.only != name:
+        if a.only and not name.startswith(a.only):
             continue
         A = x if K == D else (h if K == F else rnd(M, K))
         W = rnd(N, K, sc=0.02)
@@ -88,7 +88,7 @@ def main():
         print(json.dumps({name: out[name]}), flush=True)
     # weight gradients: dW[N,K] = dYᵀ·X over M rows (k-major operands, split-K slabs)
     for name, (N, K) in {"dw_ffn_in": (F, D), "dw_ffn_out": (D, F), "dw_qkv": (3 * D, D), "dw_o": (D, D)}.items():
-        if a.only and a.only != name:
+        if a.only and not name.startswith(a.only):
             continue
         dy = rnd(M, N)
         X = x if K == D else h

@@ -978,6 +978,25 @@ STE_DEV void vm_wait8(int extra) {
   else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
 }
 
+// Operands of batch entry `batch` and its K-tile count.  Split-K slab launches (ste_gemm's
+// weight-gradient plan: A_KC = B_KC = false, batch = slab) mark themselves with ws_bytes =
+// -(rem + 1), a field the kernel never reads otherwise: the K/64 - S·Kc K-tiles that do not
+// divide over the S slabs go one each to slabs 0..rem-1 (slab s starts at K-tile
+// s·Kc + min(s, rem)), so no remainder launch is needed.
+STE_DEV void operand_bases(const ste_gemm_args& p, int batch, const bf16*& A, const bf16*& B, int& nk) {
+  if (p.ws_bytes < 0) {
+    const int kc = p.K / 64, rem = (int)(-p.ws_bytes - 1);
+    const int64_t k0 = ((int64_t)batch * kc + (batch < rem ? batch : rem)) * 64;
+    A = (const bf16*)p.A + k0 * p.lda;
+    B = (const bf16*)p.B + k0 * p.ldb;
+    nk = kc + (batch < rem ? 1 : 0);
+    return;
+  }
+  A = (const bf16*)p.A + (int64_t)batch * p.strideA;
+  B = (const bf16*)p.B + (int64_t)batch * p.strideB;
+  nk = p.K / 64;
+}
+
 template <bool A_KC, bool B_KC, int EF, int ACT>
 __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
   using namespace ph8;
@@ -990,14 +1009,15 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
   const int wm = wave >> 2, wn = wave & 3;
   const int num_m = (p.M + 255) / 256, num_n = (p.N + 255) / 256;
   const int total = num_m * num_n * p.batch;
-  const int nk = p.K / 64;
+  int nk = p.K / 64;
   int vb = blockIdx.x;
   if (vb >= total) return;
   int batch, tm, tn;
   map_tile_bid(xcd_remap(vb, total), num_m, num_n, batch, tm, tn);
   int m0 = tm * 256, n0 = tn * 256;
-  const bf16* A = (const bf16*)p.A + (int64_t)batch * p.strideA;
-  const bf16* B = (const bf16*)p.B + (int64_t)batch * p.strideB;
+  const bf16* A;
+  const bf16* B;
+  operand_bases(p, batch, A, B, nk);
 #define STAGE_A(t, h) stage_half<A_KC, 64>(A, p.lda, m0, p.M, (t) * 64, h, smem + ((t) & 1) * BUF + (h) * HALF, wave, lane)
 #define STAGE_B(t, h) \
   stage_half<B_KC, 128>(B, p.ldb, n0, p.N, (t) * 64, h, smem + ((t) & 1) * BUF + (2 + (h)) * HALF, wave, lane)
@@ -1133,8 +1153,7 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
         map_tile_bid(xcd_remap(vb_next, total), num_m, num_n, batch, tm, tn);
         m0 = tm * 256;
         n0 = tn * 256;
-        A = (const bf16*)p.A + (int64_t)batch * p.strideA;
-        B = (const bf16*)p.B + (int64_t)batch * p.strideB;
+        operand_bases(p, batch, A, B, nk);
         STAGE_PROLOGUE();
       }
     };
@@ -1230,17 +1249,28 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ 
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int m = (int)(i / n4), c = (int)(i - (int64_t)m * n4) * 4;
     const float* w = ws + (int64_t)m * N + c;
-    f32x4 acc = *reinterpret_cast<const f32x4*>(w);
-    for (int k = 1; k < S; ++k) acc += *reinterpret_cast<const f32x4*>(w + k * slab);
     float* cp = C + (int64_t)m * ldc + c;
-    f32x4 v = acc * alpha;
-    if (beta != 0.f) v += *reinterpret_cast<const f32x4*>(cp) * beta;
-    *reinterpret_cast<f32x4*>(cp) = v;
+    const f32x4 cv = beta != 0.f ? *reinterpret_cast<const f32x4*>(cp) : f32x4{0.f, 0.f, 0.f, 0.f};
+    // up to 8 slab loads in flight, summed in slab order (run-to-run identical)
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < S; k0 += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        v[k] = k0 + k < S ? *reinterpret_cast<const f32x4*>(w + (k0 + k) * slab) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k0 + k < S) acc = k0 + k == 0 ? v[k] : acc + v[k];
+    }
+    f32x4 out = acc * alpha;
+    if (beta != 0.f) out += cv * beta;
+    *reinterpret_cast<f32x4*>(cp) = out;
   }
 }
 
-// Weight-gradient plan: S K-slabs of Kc 64-deep tiles each on the 8-phase kernel with both
-// operands k-major; the K remainder (< S tiles + a ragged tail) goes to the small kernel.
+// Weight-gradient plan: S K-slabs of Kc (or Kc + 1: the K/64 - S·Kc leftover tiles, one each
+// to the first slabs) 64-deep tiles on the 8-phase kernel with both operands k-major; only a
+// ragged K % 64 tail goes to the small kernel.
 struct SplitPlan {
   int S, Kc;  // S == 0: not applicable
 };
@@ -1364,10 +1394,14 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
     if (pl.S > 0) {
       ste_gemm_args g = a;
       const int64_t kc = (int64_t)pl.Kc * 64;
+      const int nk_all = a.K / 64;
+      const int rem = nk_all - pl.S * pl.Kc;   // whole K-tiles past S·Kc: one each to slabs 0..rem-1
       g.K = (int)kc;
       g.batch = pl.S;
       g.strideA = kc * a.lda;
       g.strideB = kc * a.ldb;
+      g.ws = nullptr;
+      g.ws_bytes = -(int64_t)(rem + 1);
       g.C = a.ws; g.ldc = a.N; g.strideC = (int64_t)a.M * a.N; g.c_bf16 = 0;
       g.alpha = 1.f; g.beta = 0.f;
       if (int e = launch_8ph<false, false>(g, s)) return e;
@@ -1376,8 +1410,8 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, (float*)a.C, a.ldc, a.ws, a.M, a.N,
                          pl.S, a.alpha, a.beta);
       STE_CHECK_LAUNCH();
-      const int64_t kdone = kc * pl.S;
-      if (kdone < a.K) {  // remainder rows: accumulate on the small kernel
+      const int64_t kdone = (int64_t)nk_all * 64;
+      if (kdone < a.K) {  // the ragged K % 64 tail: accumulate on the small kernel
         ste_gemm_args r = a;
         r.K = (int)(a.K - kdone);
         r.A = (const bf16*)a.A + kdone * a.lda;

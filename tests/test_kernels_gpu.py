@@ -83,7 +83,8 @@ def test_dx_through_cached_transpose():
     assert torch.equal(st.wt(frozen), st.w(frozen).t())
 
 
-@pytest.mark.parametrize("M,N,K,ws_mb", [(4096, 1024, 31936, 80),   # c2 FFN intermediate dW: S=4, K tail 3 tiles
+@pytest.mark.parametrize("M,N,K,ws_mb", [(4096, 1024, 31936, 80),   # c2 FFN intermediate dW: S=4, 3 leftover K-tiles on slabs 0-2
+                                         (1024, 1024, 31936, 80),   # c2 O-proj dW: S=16, Kc=31, 3 leftover K-tiles
                                          (1024, 1024, 15968, 80),   # c3 (b=32) O-proj dW: S=16, ragged 32-row tail
                                          (3072, 768, 8192, 80),     # text QKV dW over 2bL rows
                                          (1032, 520, 4160, 8),      # ragged M/N tiles; workspace caps S at 3
