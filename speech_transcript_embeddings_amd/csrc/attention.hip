@@ -1483,11 +1483,11 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel2_kernel(ste_attn_args a
 // key's dS is written to the same slot; the clamped bins 0 and nrel-1 stay intact for the other
 // keys and their G sums live in registers.  Interior bins whose key was never visited (k < 0 or
 // past the last tile) are zeroed after the loop.  With the 80-float rows (bins 64..79 by one
-// 16x16x16 MFMA) the block needs 74 KB of LDS: two blocks per CU.
+// 16x16x16 MFMA; rows padded to 84 floats) the block needs 76 KB of LDS: two blocks per CU.
 namespace rel2 {
 constexpr int DQ3_WQ = 32;
 constexpr int DQ3_Q = 4 * DQ3_WQ;
-constexpr int GT3 = NREL;                                  // 80-float Q·Eᵀ / G rows
+constexpr int GT3 = NREL + 4;   // 84-float Q·Eᵀ / G rows (bins 0..79; stride 84: <= 2-way LDS bank conflicts)
 constexpr int DQ3_T_OFF = MASK_OFF + 512;
 constexpr int DQ3_LDS = DQ3_T_OFF + 4 * DQ3_WQ * GT3 * 4;
 }  // namespace rel2
@@ -1796,7 +1796,8 @@ constexpr int KV_E_OFF = 2 * QD;
 constexpr int KV_QE_OFF = KV_E_OFF + NREL * 128;
 constexpr int KV_EDGE_OFF = KV_QE_OFF + 64 * QEW * 4;   // elo[64], ehi[64]
 constexpr int DKV_LDS = KV_EDGE_OFF + 512;
-constexpr int KV_EDGE3_OFF = KV_QE_OFF + 64 * NREL * 4;   // v3: Q·Eᵀ rows of NREL floats
+constexpr int QE3 = NREL + 4;                               // v3: Q·Eᵀ rows padded to 84 floats
+constexpr int KV_EDGE3_OFF = KV_QE_OFF + 64 * QE3 * 4;     // (the band reads: <= 2-way bank conflicts)
 constexpr int DKV3_LDS = KV_EDGE3_OFF + 512;
 }  // namespace rel2
 
@@ -2086,9 +2087,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
       bf16x8 qfr[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) qfr[s] = frag_kc(tQ, 16 * w, s, lane);
-      // rows of NREL floats, one 16-B store per lane and bin tile (no per-element predicates);
+      // rows of QE3 floats, one 16-B store per lane and bin tile (no per-element predicates);
       // the edge bins are copied to elo/ehi by the row's g == 0 lane after its own stores
-      float* qrow = qet3 + (16 * w + li) * NREL;
+      float* qrow = qet3 + (16 * w + li) * QE3;
 #pragma unroll
       for (int jt = 0; jt < NREL / 16; ++jt) {
         if (!blk_band && jt != 0 && jt != (nrel - 1) / 16) continue;
@@ -2152,7 +2153,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
               const int ql = 16 * n + 4 * g + r;
               int d = mykey - (qb + ql);
               d = med3i(d, -left, right);
-              sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r] + qet3[ql * NREL + d + left], c2, nl2[n][r]));
+              sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r] + qet3[ql * QE3 + d + left], c2, nl2[n][r]));
             }
           }
           if (any_masked && kmask[gk]) {
@@ -2250,6 +2251,114 @@ __global__ __launch_bounds__(256) void attn_rel_dE2_kernel(ste_attn_args a) {
   }
 }
 
+// ======================= dE on the MFMA: dE[j][d] += scale · Σ_(b,h,t) G[(b,h,t)][j] · Q[b*T+t][h*64+d]
+// One block per (batch, head), 4 waves.  64-row chunks of G (fp32, split into bf16 hi + lo so
+// the product keeps ~16 mantissa bits of G; Q is bf16 already) and of Q are staged into [64][64]
+// transposed-read images (tr_off layout; bins 64..79 in a second image); wave w accumulates the
+// 80 x 16 block d = 16w..16w+15 of the (b,h) partial with 16x16x32 MFMAs (A: G read transposed,
+// lane -> bin; B: Q read transposed, lane -> d).  The next chunk's global loads are in flight
+// during the MFMAs.  The 80 x 64 partial is written over the (b,h)'s own first 5,120 G floats
+// (consumed by then; T >= 64), and attn_rel_dE3_sum adds the B·H partials in a fixed order, so
+// dE is run-to-run identical (the VALU kernel above summed per-block partials with atomics).
+namespace rel_de {
+constexpr int IMG = TILE;          // [64 rows][64 bf16], tr_off layout
+constexpr int LDS = 5 * IMG;       // G hi (bins 0..63, 64..79), G lo (same), Q
+constexpr int MIN_T = 64;          // the partial needs 80 x 64 floats of the (b,h)'s G rows
+}  // namespace rel_de
+
+__global__ __launch_bounds__(256) void attn_rel_dE3_kernel(ste_attn_args a) {
+  using namespace rel_de;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bh = blockIdx.x, h = bh % a.H, b = bh / a.H, T = a.T;
+  float* G = a.gwork + (int64_t)bh * T * NREL;
+  const bf16* Q = (const bf16*)a.q + (int64_t)b * T * a.ldq + h * HD;
+  char* const qi = sm + 4 * IMG;   // G hi images at sm + {0, 1}·IMG, G lo at sm + {2, 3}·IMG
+  f32x4 acc[5];
+#pragma unroll
+  for (int jt = 0; jt < 5; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // per chunk and thread: 5 f32x4 of G (64 rows x 20 quads) and 2 bf16x8 of Q (64 rows x 8)
+  f32x4 gv[5];
+  bf16x8 qv[2];
+  auto load = [&](int t0) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int i = tid + 256 * k, r = i / 20, c = (i % 20) * 4;
+      gv[k] = t0 + r < T ? *reinterpret_cast<const f32x4*>(G + (int64_t)(t0 + r) * NREL + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + 256 * k, r = i >> 3, c = (i & 7) * 8;
+      qv[k] = t0 + r < T ? *reinterpret_cast<const bf16x8*>(Q + (int64_t)(t0 + r) * a.ldq + c) : bf16x8{};
+    }
+  };
+  const int nch = (T + 63) / 64;
+  load(0);
+  for (int ch = 0; ch < nch; ++ch) {
+    __syncthreads();   // the previous chunk's fragment reads are done
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int i = tid + 256 * k, r = i / 20, c = (i % 20) * 4;
+      bf16x4 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hi[e] = (bf16)gv[k][e];
+        lo[e] = (bf16)(gv[k][e] - (float)hi[e]);
+      }
+      const int off = tr_off(r, (c & 63) >> 2);
+      *reinterpret_cast<bf16x4*>(sm + (c >> 6) * IMG + off) = hi;
+      *reinterpret_cast<bf16x4*>(sm + (2 + (c >> 6)) * IMG + off) = lo;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + 256 * k, r = i >> 3, c = (i & 7) * 8;
+      *reinterpret_cast<bf16x8*>(qi + tr_off(r, c >> 2)) = qv[k];
+    }
+    if (ch + 1 < nch) load((ch + 1) * 64);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16x8 qb = frag_tr(qi, 16 * w, u, lane);
+#pragma unroll
+      for (int jt = 0; jt < 5; ++jt) {
+        acc[jt] = mfma16(frag_tr(sm + (jt >> 2) * IMG, (jt & 3) * 16, u, lane), qb, acc[jt]);
+        acc[jt] = mfma16(frag_tr(sm + (2 + (jt >> 2)) * IMG, (jt & 3) * 16, u, lane), qb, acc[jt]);
+      }
+    }
+  }
+  __syncthreads();   // every wave's G loads were consumed before the last barrier; the rows are free
+#pragma unroll
+  for (int jt = 0; jt < 5; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) G[(16 * jt + 4 * g + r) * HD + 16 * w + li] = acc[jt][r];
+}
+
+// dE[j][·] += scale · Σ_p partial_p[j][·] over the B·H partials, p in a fixed order: block = bin,
+// 16 lanes groups each sum every 16th partial, then one ordered sum of the 16.
+__global__ __launch_bounds__(1024) void attn_rel_dE3_sum_kernel(ste_attn_args a) {
+  __shared__ float red[16][HD];
+  const int j = blockIdx.x, d = threadIdx.x & 63, sub = threadIdx.x >> 6;
+  const int nbh = a.B * a.H;
+  const int64_t stride = (int64_t)a.T * NREL;
+  const float* P = a.gwork + j * HD + d;
+  float s = 0.f;
+  int p = sub;
+  for (; p + 48 < nbh; p += 64) {
+    const float v0 = P[p * stride], v1 = P[(p + 16) * stride], v2 = P[(p + 32) * stride], v3 = P[(p + 48) * stride];
+    s += v0; s += v1; s += v2; s += v3;
+  }
+  for (; p < nbh; p += 16) s += P[p * stride];
+  red[sub][d] = s;
+  __syncthreads();
+  if (sub == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][d];
+    a.dE[j * HD + d] += t * a.scale;
+  }
+}
+
 constexpr int FWD_LDS = 4 * TILE + NREL * 128 + 4 * 16 * NREL * 4 + 2 * 64 * 4;
 constexpr int DQ_LDS = 2 * TILE + 96 * 128 + 4 * 16 * NREL * 4 + 4 * 16 * 96 * 4 + 64 * 4;
 constexpr int DKV_LDS = 4 * TILE + NREL * 128 + 64 * NREL * 4 + 2 * 128 * 4;
@@ -2257,6 +2366,15 @@ constexpr int DKV_LDS = 4 * TILE + NREL * 128 + 64 * NREL * 4 + 2 * 128 * 4;
 template <template <bool, bool> class K>
 struct Dispatch;
 
+// STE_ATTN_DE=2: the VALU dE kernel (atomics) instead of the MFMA one (A/B runs)
+bool rel_de3() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("STE_ATTN_DE");
+    v = (e && e[0] == '2') ? 0 : 1;
+  }
+  return v == 1;
+}
 // STE_ATTN_V1=1: the original relative-key kernels (A/B comparisons in one process)
 bool rel_v2() {
   static int v = -1;
@@ -2357,7 +2475,14 @@ extern "C" int ste_attention_bwd(const ste_attn_args* a, void* stream) {
     else hipLaunchKernelGGL(attn_bwd_dkv_rel2_kernel, gk, dim3(NT), rel2::DKV_LDS, s, *a);
     STE_CHECK_LAUNCH();
     if (a->dE) {
-      hipLaunchKernelGGL(attn_rel_dE2_kernel, dim3((unsigned)(a->B * a->H)), dim3(256), 0, s, *a);
+      if (a->T >= rel_de::MIN_T && rel_de3()) {
+        hipLaunchKernelGGL(attn_rel_dE3_kernel, dim3((unsigned)(a->B * a->H)), dim3(256), rel_de::LDS, s, *a);
+        STE_CHECK_LAUNCH();
+        hipLaunchKernelGGL(attn_rel_dE3_sum_kernel, dim3((unsigned)(a->rel_left + a->rel_right + 1)), dim3(1024), 0, s,
+                           *a);
+      } else {
+        hipLaunchKernelGGL(attn_rel_dE2_kernel, dim3((unsigned)(a->B * a->H)), dim3(256), 0, s, *a);
+      }
       STE_CHECK_LAUNCH();
     }
     return 0;

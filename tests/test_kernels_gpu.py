@@ -311,9 +311,35 @@ def _attn_case(ops, B, T, H, rel, masked, drop_p, seed=7, qk_scale=0.7, v_common
     return errs
 
 
-@pytest.mark.parametrize("T", [99, 150, 499])
+@pytest.mark.parametrize("T", [40, 99, 150, 499])   # T < 64: the atomic dE kernel; else the MFMA one
 def test_attention_relkey(ops, T):
     _attn_case(ops, B=2, T=T, H=2, rel=True, masked=True, drop_p=0.0)
+
+
+def test_attention_relkey_dE_deterministic(ops):
+    """The MFMA dE kernel writes one partial per (batch, head) and sums them in a fixed order:
+    two identical backward calls give bit-identical dE (16 partials here, > one 16-way lane group)."""
+    B, T, H, D = 4, 130, 4, 64
+    W = H * D
+    torch.manual_seed(7)
+    qkv = (torch.randn(B * T, 3 * W, device=DEV) * 0.5).bfloat16()
+    q, k, v = qkv[:, :W], qkv[:, W:2 * W], qkv[:, 2 * W:]
+    E = (torch.randn(73, D, device=DEV) * 0.5).bfloat16()
+    o = torch.empty(B * T, W, device=DEV, dtype=torch.bfloat16)
+    olo = torch.empty_like(o)
+    lse = torch.empty(B * H * T, device=DEV)
+    ops.attention_fwd(q, k, v, B=B, T=T, H=H, o=o, lse=lse, rel_E=E, o_lo=olo)
+    do = torch.randn(B * T, W, device=DEV).bfloat16()
+    outs = []
+    for _ in range(2):
+        dqkv = torch.zeros(B * T, 3 * W, device=DEV, dtype=torch.bfloat16)
+        dE = torch.zeros(73, D, device=DEV)
+        ops.attention_bwd(q, k, v, o, lse, do, dqkv[:, :W], dqkv[:, W:2 * W], dqkv[:, 2 * W:], B=B, T=T, H=H,
+                          delta=torch.empty(B * H * T, device=DEV), rel_E=E, dE=dE,
+                          gwork=torch.empty(B * H * T * 80, device=DEV), o_lo=olo)
+        outs.append(dE)
+    assert torch.equal(outs[0], outs[1])
+    assert outs[0].abs().sum() > 0
 
 
 def test_attention_relkey_fully_masked_row(ops):
