@@ -29,8 +29,22 @@ STE_DEV void load_row(const void* base, bool is_bf16, int64_t ld, int row, int c
 
 // One row of the forward: v holds the row's input values on entry and its output values
 // (after row scale, activation, dropout) on exit; every requested output is written.
+// gamma / beta of the lane's columns, loaded once per wave (not per row)
 template <int MAXC>
-STE_DEV void ln_fwd_row(const ste_ln_fwd_args& a, int row, int lane, float (&v)[MAXC * 4]) {
+struct LnParams {
+  f32x4 g[MAXC], b[MAXC];
+  STE_DEV void load(const float* gamma, const float* beta, int cols, int lane) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int col = (lane + c * 64) * 4;
+      g[c] = col < cols ? *reinterpret_cast<const f32x4*>(gamma + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+      b[c] = (beta && col < cols) ? *reinterpret_cast<const f32x4*>(beta + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+};
+
+template <int MAXC>
+STE_DEV void ln_fwd_row(const ste_ln_fwd_args& a, const LnParams<MAXC>& pr, int row, int lane, float (&v)[MAXC * 4]) {
   const float inv_n = 1.0f / (float)a.cols;
   const uint32_t thresh = (uint32_t)(a.drop_p * 4294967296.0);
   const float inv_keep = a.drop_p > 0.f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
@@ -54,8 +68,7 @@ STE_DEV void ln_fwd_row(const ste_ln_fwd_args& a, int row, int lane, float (&v)[
   for (int c = 0; c < MAXC; ++c) {
     int col = (lane + c * 64) * 4;
     if (col >= a.cols) continue;
-    f32x4 g = *reinterpret_cast<const f32x4*>(a.gamma + col);
-    f32x4 b = *reinterpret_cast<const f32x4*>(a.beta + col);
+    const f32x4 g = pr.g[c], b = pr.b[c];
     f32x4 y;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -90,10 +103,12 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(ste_ln_fwd_args a) {
   const int lane = threadIdx.x & 63;
   const int wave = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * (NT / 64);
+  LnParams<MAXC> pa;
+  pa.load(a.gamma, a.beta, a.cols, lane);
   for (int row = wave; row < a.rows; row += nwaves) {
     float v[MAXC * 4];
     load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, v);
-    ln_fwd_row<MAXC>(a, row, lane, v);
+    ln_fwd_row<MAXC>(a, pa, row, lane, v);
   }
 }
 
@@ -105,11 +120,14 @@ __global__ __launch_bounds__(NT) void ln_fwd_pair_kernel(ste_ln_fwd_args a, ste_
   const int lane = threadIdx.x & 63;
   const int wave = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * (NT / 64);
+  LnParams<MAXC> pa, pb;
+  pa.load(a.gamma, a.beta, a.cols, lane);
+  pb.load(b.gamma, b.beta, b.cols, lane);
   for (int row = wave; row < a.rows; row += nwaves) {
     float v[MAXC * 4];
     load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, v);
-    ln_fwd_row<MAXC>(a, row, lane, v);
-    ln_fwd_row<MAXC>(b, row, lane, v);
+    ln_fwd_row<MAXC>(a, pa, row, lane, v);
+    ln_fwd_row<MAXC>(b, pb, row, lane, v);
   }
 }
 
@@ -125,9 +143,12 @@ struct LnAcc {
 
 // One row of the backward: x holds the input row, g the incoming gradient; on exit g holds
 // this LN's input gradient (dx, dres included); requested outputs are written.
-template <int MAXC>
+// PRE: gamma (beta) and the residual row come preloaded in pr / dr (the single kernel: one memory
+// round trip per row); otherwise they are read where used (the pair kernel, whose register count
+// the preloads would raise from 4 to 3 waves per SIMD: measured 11-35 % slower).
+template <int MAXC, bool PRE>
 STE_DEV void ln_bwd_row(const ste_ln_bwd_args& a, int row, int lane, float (&x)[MAXC * 4], float (&g)[MAXC * 4],
-                        LnAcc<MAXC>& acc) {
+                        const float* dr, const LnParams<MAXC>* pr, LnAcc<MAXC>& acc) {
   const float inv_n = 1.0f / (float)a.cols;
   const uint32_t thresh = (uint32_t)(a.drop_p * 4294967296.0);
   const float inv_keep = a.drop_p > 0.f ? 1.0f / (1.0f - a.drop_p) : 1.0f;
@@ -140,9 +161,14 @@ STE_DEV void ln_bwd_row(const ste_ln_bwd_args& a, int row, int lane, float (&x)[
   for (int c = 0; c < MAXC; ++c) {
     int col = (lane + c * 64) * 4;
     if (col >= a.cols) continue;
-    f32x4 gm = *reinterpret_cast<const f32x4*>(a.gamma + col);
-    f32x4 bt = {0.f, 0.f, 0.f, 0.f};
-    if (a.act == STE_ACT_SWISH) bt = *reinterpret_cast<const f32x4*>(a.beta + col);
+    f32x4 gm, bt = {0.f, 0.f, 0.f, 0.f};    // bt used only under swish
+    if constexpr (PRE) {
+      gm = pr->g[c];
+      bt = pr->b[c];
+    } else {
+      gm = *reinterpret_cast<const f32x4*>(a.gamma + col);
+      if (a.act == STE_ACT_SWISH) bt = *reinterpret_cast<const f32x4*>(a.beta + col);
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int i = c * 4 + e;
@@ -173,7 +199,14 @@ STE_DEV void ln_bwd_row(const ste_ln_bwd_args& a, int row, int lane, float (&x)[
       const int i = c * 4 + e;
       d[e] = rstd * (g[i] - s1 - x[i] * s2);
     }
-    if (a.dres) d += *reinterpret_cast<const f32x4*>(a.dres + (int64_t)row * a.lddres + col);
+    if (a.dres) {
+      if (PRE) {   // loaded with the row's other operands (one memory round trip per row)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[e] += dr[c * 4 + e];
+      } else {
+        d += *reinterpret_cast<const f32x4*>(a.dres + (int64_t)row * a.lddres + col);
+      }
+    }
     if (a.dx) *reinterpret_cast<f32x4*>(a.dx + (int64_t)row * a.lddx + col) = d;
     if (a.dxb || a.dsum) {
       f32x4 o = d * (a.out_scale * ors);
@@ -223,11 +256,14 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
   const int nwaves = gridDim.x * (NT / 64);
   LnAcc<MAXC> acc;
   acc.zero();
+  LnParams<MAXC> pa;
+  pa.load(a.gamma, a.act == STE_ACT_SWISH ? a.beta : nullptr, a.cols, lane);
   for (int row = wave; row < a.rows; row += nwaves) {
-    float x[MAXC * 4], g[MAXC * 4];
+    float x[MAXC * 4], g[MAXC * 4], dr[MAXC * 4];
     load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, x);
     load_row<MAXC>(a.dy, a.dy_bf16, a.lddy, row, a.cols, lane, g);
-    ln_bwd_row<MAXC>(a, row, lane, x, g, acc);
+    if (a.dres) load_row<MAXC>(a.dres, false, a.lddres, row, a.cols, lane, dr);
+    ln_bwd_row<MAXC, true>(a, row, lane, x, g, dr, &pa, acc);
   }
   if constexpr (REDUCE) ln_flush<MAXC>(a, acc, red, lane, wid);
 }
@@ -248,9 +284,9 @@ __global__ __launch_bounds__(NT) void ln_bwd_pair_kernel(ste_ln_bwd_args a, ste_
     float x[MAXC * 4], g[MAXC * 4];
     load_row<MAXC>(b.x, b.x_bf16, b.ldx, row, b.cols, lane, x);
     load_row<MAXC>(b.dy, b.dy_bf16, b.lddy, row, b.cols, lane, g);
-    ln_bwd_row<MAXC>(b, row, lane, x, g, acc_b);
+    ln_bwd_row<MAXC, false>(b, row, lane, x, g, nullptr, nullptr, acc_b);
     load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, x);
-    ln_bwd_row<MAXC>(a, row, lane, x, g, acc_a);
+    ln_bwd_row<MAXC, false>(a, row, lane, x, g, nullptr, nullptr, acc_a);
   }
   if constexpr (REDUCE) {
     ln_flush<MAXC>(b, acc_b, red, lane, wid);
