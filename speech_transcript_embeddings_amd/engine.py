@@ -418,10 +418,15 @@ class Engine:
             if sv is not None:
                 dx, pending = self._conformer_bwd(i, sv, dx, b, T, maskf, mask32, pending)
                 ctx["a_layers"][i] = None
-            if layers_done is not None and i == lo:
-                if pending is not None:   # the lowest trainable layer's FFN1-LN gradients must be final
+            if i == lo:
+                # the lowest trainable layer's FFN1-LN gradients must be final before its sync;
+                # flushed on every micro-batch (not only the one that syncs), so a micro-batch's
+                # gradients never depend on its place in the accumulation window (the single and
+                # pair LN kernels agree only to fp32 rounding)
+                if pending is not None:
                     dx, pending = self._flush_ln(pending), None
-                layers_done()
+                if layers_done is not None:
+                    layers_done()
         if pending is not None:
             dx = self._flush_ln(pending)
         s = self.s
