@@ -3,7 +3,10 @@ launches, two streams), (b) its enqueue-only host time, (c) one captured hipGrap
 replayed.  The replay repeats the captured step's per-step scalars (dropout seed, lr factor, Adam
 step), which is fine for timing and nothing else.
 
-    python profiles/graph_probe.py [--batch 64] [--steps 10]
+    python profiles/graph_probe.py [--batch 64] [--steps 10] [--seconds 10]
+
+A tiny batch (--batch 2 --seconds 1) makes the GPU work small, so the eager step time there is
+the host's cost of issuing one step (≈ the same ~2,000 launches).
 """
 import argparse
 import json
@@ -20,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--seconds", type=float, default=10.0)
     a = ap.parse_args()
     from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
     from speech_transcript_embeddings_amd.train import TrainStep, synthetic_batch
@@ -27,7 +31,7 @@ def main():
                                    spec_augment=False)
     model.audio_cfg.layerdrop = 0.0
     step = TrainStep(model, warmup=100, total_steps=100000)
-    d = synthetic_batch(a.batch, 160000, 64, device="cuda", seed=0)
+    d = synthetic_batch(a.batch, int(a.seconds * 16000), 64, device="cuda", seed=0)
     out = {}
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
