@@ -53,8 +53,8 @@ GFLOP_FWD_PER_PAIR = 641.8                 # SURVEY §8(d) forward only: 615.1 a
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)     # >= 20 timed steps after >= 5 warm-ups
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--global-batch", type=int, default=None,
                     help="global batch per optimizer step (default: 64 at N=1 = c2, 256 at N>1 = c3)")
     ap.add_argument("--micro-batch", type=int, default=64, help="largest per-GPU micro-batch")
@@ -261,9 +261,17 @@ def main(argv=None):
         if world > 1:
             dist.destroy_process_group()
         return
+    # STE_BENCH_BACKEND=gloo with STE_BENCH_SHARE_GPU=1: rehearsal of the multi-rank flow with every
+    # rank on GPU 0 (a one-GPU box); the measured runs use RCCL ("nccl"), one GPU per rank
+    if os.environ.get("STE_BENCH_SHARE_GPU") == "1":
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("STE_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from speech_transcript_embeddings_amd import ops
     from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
     from speech_transcript_embeddings_amd.train import TrainStep, synthetic_batch
