@@ -146,7 +146,7 @@ struct LnAcc {
 // PRE: gamma (beta) and the residual row come preloaded in pr / dr (the single kernel: one memory
 // round trip per row); otherwise they are read where used (the pair kernel, whose register count
 // the preloads would raise from 4 to 3 waves per SIMD: measured 11-35 % slower).
-template <int MAXC, bool PRE>
+template <int MAXC, bool PRE, bool DRPRE = PRE>
 STE_DEV void ln_bwd_row(const ste_ln_bwd_args& a, int row, int lane, float (&x)[MAXC * 4], float (&g)[MAXC * 4],
                         const float* dr, const LnParams<MAXC>* pr, LnAcc<MAXC>& acc) {
   const float inv_n = 1.0f / (float)a.cols;
@@ -200,7 +200,7 @@ STE_DEV void ln_bwd_row(const ste_ln_bwd_args& a, int row, int lane, float (&x)[
       d[e] = rstd * (g[i] - s1 - x[i] * s2);
     }
     if (a.dres) {
-      if (PRE) {   // loaded with the row's other operands (one memory round trip per row)
+      if (DRPRE) {   // loaded with the row's other operands (one memory round trip per row)
 #pragma unroll
         for (int e = 0; e < 4; ++e) d[e] += dr[c * 4 + e];
       } else {
@@ -272,7 +272,10 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
 // produces d(LN_a output) in registers, which is LN_a's incoming gradient.  b.dx may be NULL
 // (the intermediate gradient never touches HBM).
 template <int MAXC, bool REDUCE>
-__global__ __launch_bounds__(NT) void ln_bwd_pair_kernel(ste_ln_bwd_args a, ste_ln_bwd_args b) {
+// without column sums: b's residual row is issued with its x and dy and the kernel is held to
+// 128 VGPRs (4 waves per SIMD; 143 -> 135 us at c2 rows); with them (trainable layers, 2 calls
+// per step) the register count would spill, so the residual is read where used
+__global__ __launch_bounds__(NT, REDUCE ? 1 : 4) void ln_bwd_pair_kernel(ste_ln_bwd_args a, ste_ln_bwd_args b) {
   __shared__ float red[REDUCE ? NT / 64 : 1][REDUCE ? MAXC * 4 * 64 : 1];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wave = blockIdx.x * (NT / 64) + wid;
@@ -281,10 +284,11 @@ __global__ __launch_bounds__(NT) void ln_bwd_pair_kernel(ste_ln_bwd_args a, ste_
   acc_a.zero();
   acc_b.zero();
   for (int row = wave; row < a.rows; row += nwaves) {
-    float x[MAXC * 4], g[MAXC * 4];
+    float x[MAXC * 4], g[MAXC * 4], dr[MAXC * 4];
     load_row<MAXC>(b.x, b.x_bf16, b.ldx, row, b.cols, lane, x);
     load_row<MAXC>(b.dy, b.dy_bf16, b.lddy, row, b.cols, lane, g);
-    ln_bwd_row<MAXC, false>(b, row, lane, x, g, nullptr, nullptr, acc_b);
+    if (!REDUCE && b.dres) load_row<MAXC>(b.dres, false, b.lddres, row, b.cols, lane, dr);
+    ln_bwd_row<MAXC, false, !REDUCE>(b, row, lane, x, g, dr, nullptr, acc_b);
     load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, x);
     ln_bwd_row<MAXC, false>(a, row, lane, x, g, nullptr, nullptr, acc_a);
   }
