@@ -342,8 +342,13 @@ def main(argv=None):
         elapsed = float(t.item())
 
     # dominant-kernel roofline from per-launch HIP event timings of the timed steps
+    # launches on the step's own stream only: a side-stream launch (the text encoder) overlaps the
+    # main stream, so its event interval includes time spent waiting for CUs
+    own = main_stream.cuda_stream
     agg = {}
-    for name, flops, e0, e1, _shape in trace:
+    for name, flops, e0, e1, _shape, sid in trace:
+        if sid != own:
+            continue
         a = agg.setdefault(name, [0, 0.0, 0.0])
         a[0] += 1
         a[1] += flops
@@ -353,7 +358,9 @@ def main(argv=None):
     achieved = fl / tm / 1e12
     gemm_time = sum(a[2] for a in agg.values()) / args.trace_steps
     hagg = {}
-    for name, nb, e0, e1 in htrace:
+    for name, nb, e0, e1, sid in htrace:
+        if sid != own:
+            continue
         a = hagg.setdefault(name, [0, 0.0, 0.0])
         a[0] += 1
         a[1] += nb
@@ -406,7 +413,7 @@ def main(argv=None):
                      "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
                      "avg_launch_us": round(tm / n_l * 1e6, 2), "algorithmic_gflop_per_launch": round(fl / n_l / 1e9, 3),
                      "gemm_ms_per_step_all_variants": round(gemm_time * 1e3, 2),
-                     "timing": f"HIP events per launch on the launch stream, {args.trace_steps} traced steps after the timed ones"},
+                     "timing": f"HIP events per launch on the launch stream, {args.trace_steps} traced steps after the timed ones; main-stream launches only"},
         "hbm_kernels": hbm,
         "loss": round(loss, 5),
     }

@@ -98,7 +98,8 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
         ev0.record()
         launch()
         ev1.record()
-        GEMM_TRACE.append((name or gemm_kernel_name(args), 2.0 * M * N * K * batch, ev0, ev1, (M, N, K, batch)))
+        GEMM_TRACE.append((name or gemm_kernel_name(args), 2.0 * M * N * K * batch, ev0, ev1, (M, N, K, batch),
+                           torch.cuda.current_stream().cuda_stream))
     else:
         launch()
     return q8 if out is False else out
@@ -119,7 +120,7 @@ def _traced(name, nbytes, launch):
     ev0.record()
     launch()
     ev1.record()
-    HBM_TRACE.append((name, float(nbytes), ev0, ev1))
+    HBM_TRACE.append((name, float(nbytes), ev0, ev1, torch.cuda.current_stream().cuda_stream))
 
 
 def _nb(t):
