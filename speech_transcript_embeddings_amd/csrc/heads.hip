@@ -44,45 +44,82 @@ STE_DEV float dot_bf16_f32(const bf16* a, const float* b, int n, int lane) {
 }
 
 // ------------------------------------------------------------ attentive pooling
-__global__ __launch_bounds__(NT) void pool_fwd_kernel(const bf16* t, const float* w2, const float* b2, const bf16* h,
-                                                    const int32_t* mask, int L, int Hh, int H, float* weights,
-                                                    float* pooled, bf16* pooled_bf16) {
-  extern __shared__ float sc[];  // L scores
-  __shared__ float red[8];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int l = w; l < L; l += NT / 64) {
+// Forward, three launches so the [B*L, H] read is spread over the chip (one block per sample
+// left 3/4 of the CUs idle and walked L rows serially):
+//   pool_score_kernel   s_l = t_l·w2 + b2 (masked -> -1e9), one wave per row   grid (B, ceil(L/16))
+//   pool_softmax_kernel w_l = softmax_l(s)                                     grid B
+//   pool_wsum_kernel    pooled[c] = Σ_l w_l h_l[c]: 8 waves split the rows,    grid (B, ceil(H/256))
+//                       partials summed in wave order (deterministic)
+constexpr int POOL_SC_ROWS = 16;
+constexpr int POOL_WS_NT = 512;
+
+__global__ __launch_bounds__(NT) void pool_score_kernel(const bf16* t, const float* w2, const float* b2,
+                                                      const int32_t* mask, int L, int Hh, float* sc) {
+  const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l1 = min(L, (int)(blockIdx.y + 1) * POOL_SC_ROWS);
+  for (int l = blockIdx.y * POOL_SC_ROWS + w; l < l1; l += NT / 64) {
     float s = dot_bf16_f32(t + (int64_t)(b * L + l) * Hh, w2, Hh, lane) + b2[0];
     if (mask && mask[b * L + l] == 0) s = -1e9f;
-    if (lane == 0) sc[l] = s;
-  }
-  __syncthreads();
-  float mx = -INFINITY;
-  for (int l = tid; l < L; l += NT) mx = fmaxf(mx, sc[l]);
-  mx = block_max(mx, red);
-  float sum = 0.f;
-  for (int l = tid; l < L; l += NT) { float e = __expf(sc[l] - mx); sc[l] = e; sum += e; }
-  sum = block_sum(sum, red);
-  const float inv = 1.0f / sum;
-  for (int l = tid; l < L; l += NT) { sc[l] *= inv; weights[b * L + l] = sc[l]; }
-  __syncthreads();
-  for (int c = tid * 4; c < H; c += NT * 4) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int l = 0; l < L; ++l) acc += load_bf16x4(h + (int64_t)(b * L + l) * H + c) * sc[l];
-    *reinterpret_cast<f32x4*>(pooled + (int64_t)b * H + c) = acc;
-    if (pooled_bf16) store_bf16x4(pooled_bf16 + (int64_t)b * H + c, acc);
+    if (lane == 0) sc[b * L + l] = s;
   }
 }
 
-// Backward, three launches spread over (batch, row chunks) so the [B*L, H] reads fill the chip:
+__global__ __launch_bounds__(NT) void pool_softmax_kernel(int L, float* sc) {
+  __shared__ float red[8];
+  float* r = sc + (int64_t)blockIdx.x * L;
+  const int tid = threadIdx.x;
+  float mx = -INFINITY;
+  for (int l = tid; l < L; l += NT) mx = fmaxf(mx, r[l]);
+  mx = block_max(mx, red);
+  float sum = 0.f;
+  for (int l = tid; l < L; l += NT) sum += __expf(r[l] - mx);
+  sum = block_sum(sum, red);
+  const float inv = 1.0f / sum;
+  for (int l = tid; l < L; l += NT) r[l] = __expf(r[l] - mx) * inv;
+}
+
+__global__ __launch_bounds__(POOL_WS_NT) void pool_wsum_kernel(const bf16* h, const float* weights, int L, int H,
+                                                             float* pooled, bf16* pooled_bf16) {
+  extern __shared__ float wl[];  // L weights
+  __shared__ f32x4 part[POOL_WS_NT / 64][64];
+  constexpr int NW = POOL_WS_NT / 64;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int l = tid; l < L; l += POOL_WS_NT) wl[l] = weights[b * L + l];
+  __syncthreads();
+  const int c = blockIdx.y * 256 + lane * 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (c < H) {
+    const bf16* hp = h + (int64_t)b * L * H + c;
+#pragma unroll 4
+    for (int l = w; l < L; l += NW) acc += load_bf16x4(hp + (int64_t)l * H) * wl[l];
+  }
+  part[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && c < H) {
+    f32x4 s = part[0][lane];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) s += part[i][lane];
+    *reinterpret_cast<f32x4*>(pooled + (int64_t)b * H + c) = s;
+    if (pooled_bf16) store_bf16x4(pooled_bf16 + (int64_t)b * H + c, s);
+  }
+}
+
+// Backward, four launches spread over (batch, row chunks) so the [B*L, H] reads fill the chip:
 //   pool_dp_kernel     dP[l] = h_l·dpooled                               grid (B, ceil(L/16))
 //   pool_dscore_kernel ds[l] = w_l (dP[l] - Σ_j w_j dP[j]), db2 += Σ ds   grid B
 //   pool_dz_kernel     dh_l += w_l dpooled;  dz_l = ds_l w2 (1 - t_l²) (bf16 hi [+ lo]);
-//                      dw2 += Σ_l ds_l t_l;  db1 += Σ_l dz_l in fp32     grid (B, ceil(L/32))
+//                      per-chunk partials of Σ_l ds_l t_l, Σ_l dz_l      grid (B, ceil(L/64|16))
+//   pool_dw_kernel     dw2 += Σ partials, db1 += Σ partials (chunk order) grid ceil(2Hh/64)
 // Σ_l ds_l = 0 (softmax), so the scorer's bias gradient Σ_l dz_l is a small difference of large
 // terms: it is summed from the fp32 dz here, never from the bf16-rounded copy, and the optional
-// low half dz_lo = bf16(dz - bf16(dz)) lets the weight-gradient GEMM see dz to ~16 bits.
+// low half dz_lo = bf16(dz - bf16(dz)) lets the weight-gradient GEMM see dz to ~16 bits.  The
+// column sums go through a partials buffer, not atomics: 2·Hh atomics per block onto the same
+// 2·Hh addresses serialised in L2 and made the audio launch atomic-bound (~180 µs); the
+// two-level sum is also run-to-run deterministic.
 constexpr int POOL_DP_ROWS = 16;
-constexpr int POOL_DZ_ROWS = 32;
+// row chunk of pool_dz: 64 rows, or 16 when that leaves fewer than 512 blocks (text: 128 x 64 rows)
+static int pool_dz_rows(int B, int L) { return (int64_t)B * ((L + 63) / 64) >= 512 ? 64 : 16; }
+constexpr int POOL_DW_NT = 1024;
 
 __global__ __launch_bounds__(NT) void pool_dp_kernel(const bf16* h, const float* dpooled, int L, int H, float* dp_out) {
   const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -112,22 +149,27 @@ __global__ __launch_bounds__(NT) void pool_dscore_kernel(const float* weights, i
 
 __global__ __launch_bounds__(NT) void pool_dz_kernel(const bf16* t, const float* w2, const float* weights,
                                                    const float* dpooled, const float* dsc, int L, int Hh, int H,
-                                                   float* dh, bf16* dz, bf16* dz_lo, float* dw2, float* db1) {
+                                                   float* dh, bf16* dz, bf16* dz_lo, float* part, int rows) {
+  __shared__ f32x4 red[2 * NT];
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int l0 = blockIdx.y * POOL_DZ_ROWS, l1 = min(L, l0 + POOL_DZ_ROWS);
+  const int l0 = blockIdx.y * rows, l1 = min(L, l0 + rows);
   // dh[l][c] += w[l] * dpooled[c]
   const float* dp = dpooled + (int64_t)b * H;
   for (int c = tid * 4; c < H; c += NT * 4) {
     const f32x4 d = *reinterpret_cast<const f32x4*>(dp + c);
+#pragma unroll 4
     for (int l = l0; l < l1; ++l) {
       f32x4* o = reinterpret_cast<f32x4*>(dh + (int64_t)(b * L + l) * H + c);
       *o = *o + d * weights[b * L + l];
     }
   }
-  for (int k = tid * 4; k < Hh; k += NT * 4) {
+  // dz rows: the block's threads are (groups x Hh/4 column quads); group g takes rows l0+g, +groups, ...
+  const int cq = Hh >> 2, groups = NT / cq, g = tid / cq, k = (tid - g * cq) * 4;
+  f32x4 g2 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
+  if (g < groups) {
     const f32x4 wv = *reinterpret_cast<const f32x4*>(w2 + k);
-    f32x4 g2 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
-    for (int l = l0; l < l1; ++l) {
+#pragma unroll 2
+    for (int l = l0 + g; l < l1; l += groups) {
       const int64_t off = (int64_t)(b * L + l) * Hh + k;
       const f32x4 tv = load_bf16x4(t + off);
       const float ds = dsc[b * L + l];
@@ -139,11 +181,38 @@ __global__ __launch_bounds__(NT) void pool_dz_kernel(const bf16* t, const float*
       if (dz_lo) store_bf16x4_split(dz + off, dz_lo + off, o);
       else store_bf16x4(dz + off, o);
     }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (dw2) atomicAdd(dw2 + k + e, g2[e]);
-      if (db1) atomicAdd(db1 + k + e, g1[e]);
-    }
+  }
+  red[2 * tid] = g2;
+  red[2 * tid + 1] = g1;
+  __syncthreads();
+  if (tid < cq) {
+    f32x4 s2 = red[2 * tid], s1 = red[2 * tid + 1];
+    for (int i = 1; i < groups; ++i) { s2 += red[2 * (i * cq + tid)]; s1 += red[2 * (i * cq + tid) + 1]; }
+    float* pr = part + (int64_t)(b * gridDim.y + blockIdx.y) * 2 * Hh;
+    *reinterpret_cast<f32x4*>(pr + k) = s2;
+    *reinterpret_cast<f32x4*>(pr + Hh + k) = s1;
+  }
+}
+
+// column sums of the [nrows, 2*Hh] partials: 16 waves stride the rows, one column per lane,
+// wave partials summed in order; dw2 (cols < Hh) and db1 (cols >= Hh) accumulated (+=).
+__global__ __launch_bounds__(POOL_DW_NT) void pool_dw_kernel(const float* part, int nrows, int Hh, float* dw2,
+                                                           float* db1) {
+  constexpr int NW = POOL_DW_NT / 64;
+  __shared__ float red[NW][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (col < 2 * Hh) {
+#pragma unroll 4
+    for (int r = w; r < nrows; r += NW) s += part[(int64_t)r * 2 * Hh + col];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && col < 2 * Hh) {
+    float tot = red[0][lane];
+    for (int i = 1; i < NW; ++i) tot += red[i][lane];
+    if (col < Hh) { if (dw2) dw2[col] += tot; }
+    else if (db1) db1[col - Hh] += tot;
   }
 }
 
@@ -601,25 +670,44 @@ extern "C" int ste_attn_pool_fwd(const void* t, const float* w2, const float* b2
                                  int B, int L, int Hh, int H, float* weights, float* pooled, void* pooled_bf16,
                                  void* stream) {
   if (B <= 0 || L <= 0 || (Hh & 3) || (H & 3) || L > 8192) return STE_ERR_SHAPE;
-  hipLaunchKernelGGL(pool_fwd_kernel, dim3(B), dim3(NT), L * sizeof(float), (hipStream_t)stream, (const bf16*)t, w2,
-                     b2, (const bf16*)h, mask, L, Hh, H, weights, pooled, (bf16*)pooled_bf16);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(pool_score_kernel, dim3(B, (L + POOL_SC_ROWS - 1) / POOL_SC_ROWS), dim3(NT), 0, s,
+                     (const bf16*)t, w2, b2, mask, L, Hh, weights);
+  STE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(pool_softmax_kernel, dim3(B), dim3(NT), 0, s, L, weights);
+  STE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(pool_wsum_kernel, dim3(B, (H + 255) / 256), dim3(POOL_WS_NT), L * sizeof(float), s,
+                     (const bf16*)h, weights, L, H, pooled, (bf16*)pooled_bf16);
   STE_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int ste_attn_pool_bwd_work_floats(int B, int L, int Hh) {
+  if (B <= 0 || L <= 0 || Hh <= 0) return STE_ERR_SHAPE;
+  const int rows = pool_dz_rows(B, L);
+  return B * L + B * ((L + rows - 1) / rows) * 2 * Hh;
 }
 
 extern "C" int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float* weights,
                                  const float* dpooled, int B, int L, int Hh, int H, float* dh, void* dt, void* dt_lo,
                                  float* dw2, float* db2, float* db1, float* work, void* stream) {
-  if (B <= 0 || L <= 0 || (Hh & 3) || (H & 3) || !work || !dt) return STE_ERR_SHAPE;
+  if (B <= 0 || L <= 0 || (Hh & 3) || (H & 3) || Hh > 4 * NT || !work || !dt) return STE_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
+  const int rows = pool_dz_rows(B, L), nchunk = (L + rows - 1) / rows;
+  float* part = work + (int64_t)B * L;
   hipLaunchKernelGGL(pool_dp_kernel, dim3(B, (L + POOL_DP_ROWS - 1) / POOL_DP_ROWS), dim3(NT), 0, s, (const bf16*)h,
                      dpooled, L, H, work);
   STE_CHECK_LAUNCH();
   hipLaunchKernelGGL(pool_dscore_kernel, dim3(B), dim3(NT), 0, s, weights, L, work, db2);
   STE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(pool_dz_kernel, dim3(B, (L + POOL_DZ_ROWS - 1) / POOL_DZ_ROWS), dim3(NT), 0, s, (const bf16*)t,
-                     w2, weights, dpooled, work, L, Hh, H, dh, (bf16*)dt, (bf16*)dt_lo, dw2, db1);
+  hipLaunchKernelGGL(pool_dz_kernel, dim3(B, nchunk), dim3(NT), 0, s, (const bf16*)t, w2, weights, dpooled, work, L,
+                     Hh, H, dh, (bf16*)dt, (bf16*)dt_lo, part, rows);
   STE_CHECK_LAUNCH();
+  if (dw2 || db1) {
+    hipLaunchKernelGGL(pool_dw_kernel, dim3((2 * Hh + 63) / 64), dim3(POOL_DW_NT), 0, s, part, B * nchunk, Hh, dw2,
+                       db1);
+    STE_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -490,9 +490,13 @@ def test_feature_extractor_api():
 
 
 # ---------------------------------------------------------------- heads
-def test_attn_pool(ops):
+@pytest.mark.parametrize("B,L,H,Hh", [(3, 50, 256, 128), (3, 64, 768, 384), (2, 499, 1024, 512),
+                                      (64, 499, 1024, 512)])
+def test_attn_pool(ops, B, L, H, Hh):
+    """Score/softmax/weighted-sum forward and the four-launch backward at a small case, the text
+    head's shape (Hh=384: ragged thread groups), the audio head's (L=499: partial row chunks) and
+    the c2 audio batch (64-row chunks instead of 16)."""
     torch.manual_seed(3)
-    B, L, H, Hh = 3, 50, 256, 128
     h = torch.randn(B * L, H, device=DEV).bfloat16()
     t = torch.tanh(torch.randn(B * L, Hh, device=DEV)).bfloat16()
     w2 = torch.randn(Hh, device=DEV) * 0.3
@@ -514,7 +518,7 @@ def test_attn_pool(ops):
     pref.backward(dp)
     dh = torch.zeros(B * L, H, device=DEV)
     dz = torch.empty(B * L, Hh, device=DEV, dtype=torch.bfloat16)
-    dw2 = torch.zeros(Hh, device=DEV)
+    dw2 = torch.full((Hh,), 0.5, device=DEV)      # accumulated into (+=)
     db2 = torch.zeros(1, device=DEV)
     db1 = torch.zeros(Hh, device=DEV)
     dz_lo = torch.empty_like(dz)
@@ -524,7 +528,10 @@ def test_attn_pool(ops):
     assert rel_err(dz, dz_ref) < 5e-3
     assert rel_err(dz.float() + dz_lo.float(), dz_ref) < 2e-5   # hi + lo: ~fp32
     assert rel_err(db1, dz_ref.sum(0)) < 1e-5                   # fp32 column sums (Σ dscore = 0 cancellation)
-    assert rel_err(dw2, w2r.grad) < 1e-4
+    assert rel_err(dw2 - 0.5, w2r.grad) < 1e-4
+    db1_again = torch.zeros(Hh, device=DEV)                     # column sums without atomics: bitwise repeatable
+    ops.attn_pool_bwd(t, w2, h, weights, dp, B, L, torch.zeros_like(dh), dz, None, None, db1=db1_again)
+    assert torch.equal(db1_again, db1)
     assert abs(db2.item() - b2r.grad.item()) < 1e-4
 
 
