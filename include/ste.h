@@ -285,6 +285,13 @@ int ste_xattn_fwd(const float* q, const void* k, const void* v, int64_t ldkv, co
 int ste_xattn_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs, const float* dout,
                   int B, int S, int P, int nh, int nq, float scale, float drop_p, uint64_t seed0, uint64_t seed1,
                   float* dq, float* dk, float* dv, int64_t lddkv, void* stream);
+/* As ste_xattn_bwd, but dk/dv are bf16 and WRITTEN (not accumulated), and colsum_part fp32
+ * [B, 2P] receives per-sample column sums of dk (cols [0,P)) and dv (cols [P,2P)) in fp32, for the
+ * key/value bias gradient; lddkv % 8 == 0. */
+int ste_xattn_bwd_bf16(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
+                       const float* dout, int B, int S, int P, int nh, int nq, float scale, float drop_p,
+                       uint64_t seed0, uint64_t seed1, float* dq, void* dk, void* dv, int64_t lddkv,
+                       float* colsum_part, void* stream);
 
 /* WordLevelAlignmentModule attention core (ref:training/trainer_unfreeze.py:214-310, the
  * nn.MultiheadAttention(P, nh=4, batch_first) of :237-242 with key_padding_mask, probs

@@ -361,12 +361,18 @@ __global__ __launch_bounds__(NT) void xattn_fwd_kernel(const float* q, const bf1
   }
 }
 
-// dk, dv are fp32 and ACCUMULATED (+=) once for all NQ queries; dq is written.
-template <int NQ>
+// OUT_BF16 = false: dk, dv are fp32 and ACCUMULATED (+=) once for all NQ queries.
+// OUT_BF16 = true:  dk, dv are bf16 and WRITTEN (the block is their only writer), and the fp32
+//   column sums of this block's dk / dv rows go to part[b][c0 + c] / part[b][P + c0 + c]
+//   (row-group partials summed in order), so the key/value bias gradient is a [B, 2P] column
+//   sum instead of a zero-fill + RMW + cast + colsum pass over fp32 [B*S, 2P].
+// dq is written.
+template <int NQ, bool OUT_BF16>
 __global__ __launch_bounds__(NT) void xattn_bwd_kernel(const float* q, const bf16* k, const bf16* v, int64_t ldkv,
                                                      const float* probs, const float* dout, int B, int S, int P,
                                                      int nh, float scale, float drop_p, uint64_t seed0,
-                                                     uint64_t seed1, float* dq, float* dk, float* dv, int64_t lddkv) {
+                                                     uint64_t seed1, float* dq, void* dk_, void* dv_, int64_t lddkv,
+                                                     float* part) {
   extern __shared__ float sds[];  // NQ * S: dp, then ds
   __shared__ float sq[NQ][256], sdo[NQ][256], red[NQ][NT / 64];
   __shared__ f32x4 racc[NT];
@@ -425,6 +431,7 @@ __global__ __launch_bounds__(NT) void xattn_bwd_kernel(const float* q, const bf1
   f32x4 dqa[NQ];
 #pragma unroll
   for (int qi = 0; qi < NQ; ++qi) dqa[qi] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 csk = {0.f, 0.f, 0.f, 0.f}, csv = {0.f, 0.f, 0.f, 0.f};
   if (rg < RG) {
     f32x4 qv[NQ], dov[NQ];
 #pragma unroll
@@ -444,10 +451,29 @@ __global__ __launch_bounds__(NT) void xattn_bwd_kernel(const float* q, const bf1
         dkv += qv[qi] * ds;
         dvv += dov[qi] * pd;
       }
-      f32x4* dkr = reinterpret_cast<f32x4*>(dk + (int64_t)(b * S + s) * lddkv + c0 + cc);
-      f32x4* dvr = reinterpret_cast<f32x4*>(dv + (int64_t)(b * S + s) * lddkv + c0 + cc);
-      *dkr += dkv;
-      *dvr += dvv;
+      const int64_t off = (int64_t)(b * S + s) * lddkv + c0 + cc;
+      if constexpr (OUT_BF16) {
+        store_bf16x4((bf16*)dk_ + off, dkv);
+        store_bf16x4((bf16*)dv_ + off, dvv);
+        csk += dkv;
+        csv += dvv;
+      } else {
+        *reinterpret_cast<f32x4*>((float*)dk_ + off) += dkv;
+        *reinterpret_cast<f32x4*>((float*)dv_ + off) += dvv;
+      }
+    }
+  }
+  if constexpr (OUT_BF16) {
+#pragma unroll
+    for (int kv = 0; kv < 2; ++kv) {
+      racc[tid] = kv ? csv : csk;
+      __syncthreads();
+      if (tid < nq4) {
+        f32x4 t = racc[tid];
+        for (int r = 1; r < RG; ++r) t += racc[r * nq4 + tid];
+        *reinterpret_cast<f32x4*>(part + (int64_t)b * 2 * P + kv * P + c0 + 4 * tid) = t;
+      }
+      __syncthreads();
     }
   }
 #pragma unroll
@@ -754,22 +780,42 @@ extern "C" int ste_xattn_fwd(const float* q, const void* k, const void* v, int64
   return 0;
 }
 
+template <bool OUT_BF16>
+static int xattn_bwd_launch(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
+                            const float* dout, int B, int S, int P, int nh, int nq, float scale, float drop_p,
+                            uint64_t seed0, uint64_t seed1, float* dq, void* dk, void* dv, int64_t lddkv, float* part,
+                            void* stream) {
+  if (!xattn_shape_ok(B, S, P, nh, nq) || (nq != 1 && nq != 2) || (ldkv & 7) || lddkv < P ||
+      (lddkv & (OUT_BF16 ? 7 : 3)) || (OUT_BF16 && !part) ||
+      (((uintptr_t)k | (uintptr_t)v | (uintptr_t)dq | (uintptr_t)dk | (uintptr_t)dv | (uintptr_t)part) & 15))
+    return STE_ERR_SHAPE;
+  const size_t lds = (size_t)nq * S * sizeof(float);
+  if (nq == 1)
+    hipLaunchKernelGGL((xattn_bwd_kernel<1, OUT_BF16>), dim3(B, nh), dim3(NT), lds, (hipStream_t)stream, q,
+                       (const bf16*)k, (const bf16*)v, ldkv, probs, dout, B, S, P, nh, scale, drop_p, seed0, seed1, dq,
+                       dk, dv, lddkv, part);
+  else
+    hipLaunchKernelGGL((xattn_bwd_kernel<2, OUT_BF16>), dim3(B, nh), dim3(NT), lds, (hipStream_t)stream, q,
+                       (const bf16*)k, (const bf16*)v, ldkv, probs, dout, B, S, P, nh, scale, drop_p, seed0, seed1, dq,
+                       dk, dv, lddkv, part);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int ste_xattn_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
                              const float* dout, int B, int S, int P, int nh, int nq, float scale, float drop_p,
                              uint64_t seed0, uint64_t seed1, float* dq, float* dk, float* dv, int64_t lddkv,
                              void* stream) {
-  if (!xattn_shape_ok(B, S, P, nh, nq) || (nq != 1 && nq != 2) || (ldkv & 7) || lddkv < P || (lddkv & 3) ||
-      (((uintptr_t)k | (uintptr_t)v | (uintptr_t)dq | (uintptr_t)dk | (uintptr_t)dv) & 15))
-    return STE_ERR_SHAPE;
-  const size_t lds = (size_t)nq * S * sizeof(float);
-  if (nq == 1)
-    hipLaunchKernelGGL(xattn_bwd_kernel<1>, dim3(B, nh), dim3(NT), lds, (hipStream_t)stream, q, (const bf16*)k,
-                       (const bf16*)v, ldkv, probs, dout, B, S, P, nh, scale, drop_p, seed0, seed1, dq, dk, dv, lddkv);
-  else
-    hipLaunchKernelGGL(xattn_bwd_kernel<2>, dim3(B, nh), dim3(NT), lds, (hipStream_t)stream, q, (const bf16*)k,
-                       (const bf16*)v, ldkv, probs, dout, B, S, P, nh, scale, drop_p, seed0, seed1, dq, dk, dv, lddkv);
-  STE_CHECK_LAUNCH();
-  return 0;
+  return xattn_bwd_launch<false>(q, k, v, ldkv, probs, dout, B, S, P, nh, nq, scale, drop_p, seed0, seed1, dq, dk, dv,
+                                 lddkv, nullptr, stream);
+}
+
+extern "C" int ste_xattn_bwd_bf16(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
+                                  const float* dout, int B, int S, int P, int nh, int nq, float scale, float drop_p,
+                                  uint64_t seed0, uint64_t seed1, float* dq, void* dk, void* dv, int64_t lddkv,
+                                  float* colsum_part, void* stream) {
+  return xattn_bwd_launch<true>(q, k, v, ldkv, probs, dout, B, S, P, nh, nq, scale, drop_p, seed0, seed1, dq, dk, dv,
+                                lddkv, colsum_part, stream);
 }
 
 extern "C" int ste_xattn1_fwd(const float* q, const void* k, const void* v, int64_t ldkv, const int32_t* mask, int B,

@@ -756,24 +756,25 @@ class Engine:
             self._dw(dattb, hs["att_tb"], "text_to_audio_attention.out_proj.weight")
             self._db(datt, "text_to_audio_attention.out_proj.bias")
             dqt = self._e(nb, P)
-            dkv = self._z(ab * T, 2 * P)
+            # dK/dV come out of the kernel in bf16 with their fp32 column sums (the fused key/value
+            # bias gradient); the K/V input gradient leaves its GEMM in bf16 with the
+            # audio_seq_to_projection bias gradient summed in the epilogue: no fp32 [ab*T, 2P]
+            # zero-fill / accumulate / cast / column-sum passes
+            dkvb = self._e(ab * T, 2 * P, dtype=BF16)
             ops.xattn_bwd(hs["qt"], hs["kva"][:, :P], hs["kva"][:, P:], hs["probs_t"], dq_in, b, T, nh, dqt,
-                          dkv[:, :P], dkv[:, P:], (_site_seed(hs["seed_t"], 0), _site_seed(hs["seed_t"], 1)),
-                          drop_p=hs["p_x"])
+                          dkvb[:, :P], dkvb[:, P:], (_site_seed(hs["seed_t"], 0), _site_seed(hs["seed_t"], 1)),
+                          drop_p=hs["p_x"], colsum=s.fused("text_to_audio_attention.key.bias", 2, "g"))
             dqtb = ops.cast_bf16(dqt, self._e(nb, P, dtype=BF16))
             ops.linear_dx(dqtb, s.w("text_to_audio_attention.query.weight"), out=d_tproj, beta=1.0)
             self._dw(dqtb, hs["tprojb"], "text_to_audio_attention.query.weight")
             self._db(dqt, "text_to_audio_attention.query.bias")
-            dkvb = ops.cast_bf16(dkv, self._e(ab * T, 2 * P, dtype=BF16))
-            daseq = self._dx(dkvb, "text_to_audio_attention.key.weight", 2)
+            daseqb = self._dx(dkvb, "text_to_audio_attention.key.weight", 2, out_bf16=True,
+                              colsum=s.g("audio_seq_to_projection.bias"))
             self._dw(dkvb, hs["aseqb"], "text_to_audio_attention.key.weight", fused=2)
-            self._db(dkv, "text_to_audio_attention.key.bias", fused=2)
-            del dkv, dkvb
-            daseqb = ops.cast_bf16(daseq, self._e(ab * T, P, dtype=BF16))
+            del dkvb
             self._dx(daseqb, "audio_seq_to_projection.weight", out=dah, beta=1.0)
             self._dw(daseqb, ctx["_ahb"], "audio_seq_to_projection.weight")
-            self._db(daseq, "audio_seq_to_projection.bias")
-            del daseq, daseqb
+            del daseqb
             # ---- audio->text attention (pos call)
             datta = dacat[:, P:].contiguous()
             dattab = ops.cast_bf16(datta, self._e(b, P, dtype=BF16))
@@ -781,21 +782,19 @@ class Engine:
             self._dw(dattab, hs["att_ab"], "audio_to_text_attention.out_proj.weight")
             self._db(datta, "audio_to_text_attention.out_proj.bias")
             dqa = self._e(b, P)
-            dkvt = self._z(b * L, 2 * P)
+            dkvtb = self._e(b * L, 2 * P, dtype=BF16)
             ops.xattn1_bwd(hs["qa"], hs["kvt"][:, :P], hs["kvt"][:, P:], hs["probs_a"], dqa_in, b, L, nh, dqa,
-                           dkvt[:, :P], dkvt[:, P:], drop_p=hs["p_x"], seed=hs["seed_a"])
+                           dkvtb[:, :P], dkvtb[:, P:], drop_p=hs["p_x"], seed=hs["seed_a"],
+                           colsum=s.fused("audio_to_text_attention.key.bias", 2, "g"))
             dqab = ops.cast_bf16(dqa, self._e(b, P, dtype=BF16))
             ops.linear_dx(dqab, s.w("audio_to_text_attention.query.weight"), out=d_aproj[:b], beta=1.0)
             self._dw(dqab, hs["aprojb"], "audio_to_text_attention.query.weight")
             self._db(dqa, "audio_to_text_attention.query.bias")
-            dkvtb = ops.cast_bf16(dkvt, self._e(b * L, 2 * P, dtype=BF16))
-            dtseq = ops.linear_dx(dkvtb, s.fused("audio_to_text_attention.key.weight", 2, "w"))
+            dtseqb = ops.linear_dx(dkvtb, s.fused("audio_to_text_attention.key.weight", 2, "w"), out_bf16=True,
+                                   colsum=s.g("text_seq_to_projection.bias"))
             self._dw(dkvtb, hs["tseqb"], "audio_to_text_attention.key.weight", fused=2)
-            self._db(dkvt, "audio_to_text_attention.key.bias", fused=2)
-            dtseqb = ops.cast_bf16(dtseq, self._e(b * L, P, dtype=BF16))
             ops.linear_dx(dtseqb, s.w("text_seq_to_projection.weight"), out=dth[: b * L], beta=1.0)
             self._dw(dtseqb, ctx["_thb"][: b * L], "text_seq_to_projection.weight")
-            self._db(dtseq, "text_seq_to_projection.bias")
         else:
             _add_(d_tproj, d_tfused)
             _add_(d_aproj[:b], d_afused)

@@ -644,6 +644,25 @@ def test_xattn_two_query_sets(ops, B, S, P, nh, drop_p):
     assert rel_err(dq, qr.grad) < 1e-5
     assert rel_err(dkv[:, :P], kr.grad) < 1e-5
     assert rel_err(dkv[:, P:], vr.grad) < 1e-5
+    # bf16 variant (engine path): dK/dV written in bf16, their fp32 column sums (the fused
+    # key/value bias gradient) added into a [2P] vector; nq=1 through xattn1_bwd the same way
+    dq2 = torch.empty_like(dq)
+    dkvb = torch.full((B * S, 2 * P), 7.0, device=DEV).bfloat16()   # written, not accumulated
+    cs = torch.full((2 * P,), 0.25, device=DEV)
+    ops.xattn_bwd(q, k, v, probs, do, B, S, nh, dq2, dkvb[:, :P], dkvb[:, P:], seeds, drop_p=drop_p, colsum=cs)
+    assert torch.equal(dq2, dq)
+    assert torch.equal(dkvb, dkv.bfloat16())
+    assert rel_err(cs - 0.25, dkv.sum(0)) < 1e-5
+    dq1 = torch.empty(B, P, device=DEV)
+    dkv1 = torch.zeros(B * S, 2 * P, device=DEV)
+    ops.xattn1_bwd(q[:B], k, v, probs[:B * nh * S], do[:B], B, S, nh, dq1, dkv1[:, :P], dkv1[:, P:], drop_p=drop_p,
+                   seed=seeds[0])
+    dkv1b = torch.empty(B * S, 2 * P, device=DEV).bfloat16()
+    cs1 = torch.zeros(2 * P, device=DEV)
+    ops.xattn1_bwd(q[:B], k, v, probs[:B * nh * S], do[:B], B, S, nh, dq1, dkv1b[:, :P], dkv1b[:, P:],
+                   drop_p=drop_p, seed=seeds[0], colsum=cs1)
+    assert torch.equal(dkv1b, dkv1.bfloat16())
+    assert rel_err(cs1, dkv1.sum(0)) < 1e-5
 
 
 @pytest.mark.parametrize("B,L,T,P,drop_p", [(2, 12, 49, 128, 0.0), (3, 64, 499, 768, 0.0), (2, 20, 130, 256, 0.1)])
