@@ -297,26 +297,34 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(ste_attn_args a) {
 }
 
 // ===================================================================== delta = rowsum(dO*O)
-__global__ void attn_delta_kernel(ste_attn_args a) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (b*T + q)*H + h
-  const int64_t total = (int64_t)a.B * a.T * a.H;
-  if (idx >= total) return;
-  const int h = idx % a.H;
-  const int64_t row = idx / a.H;
-  const int b = row / a.T, q = row % a.T;
-  const bf16* dO = (const bf16*)a.dout + row * a.lddo + h * HD;
-  const bf16* O = (const bf16*)a.o + row * a.ldo + h * HD;
-  const bf16* Ol = a.o_lo ? (const bf16*)a.o_lo + row * a.ldolo + h * HD : nullptr;
-  float acc = 0.f;
+// One wave per sequence row (b, q): its lanes read the row's H*HD columns of dO, O (and O_lo)
+// as contiguous 1-KB runs (8 bf16 a lane), the 8 lanes of each head sum by shuffles, and lane
+// 8j writes head h's delta.  (One thread per (row, head) walking its own 128-B slice made every
+// load instruction touch 64 cache lines: ~0.3 TB/s.)
+__global__ __launch_bounds__(256) void attn_delta_kernel(ste_attn_args a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // b*T + q
+  if (row >= (int64_t)a.B * a.T) return;
+  const int b = (int)(row / a.T), q = (int)(row % a.T);
+  const int HH = a.H * HD;
+  const bf16* dO = (const bf16*)a.dout + row * a.lddo;
+  const bf16* O = (const bf16*)a.o + row * a.ldo;
+  const bf16* Ol = a.o_lo ? (const bf16*)a.o_lo + row * a.ldolo : nullptr;
+  for (int c0 = 0; c0 < HH; c0 += 512) {
+    const int c = c0 + lane * 8;
+    float acc = 0.f;
+    if (c < HH) {
+      const bf16x8 x = *reinterpret_cast<const bf16x8*>(dO + c);
+      const bf16x8 y = *reinterpret_cast<const bf16x8*>(O + c);
+      const bf16x8 z = Ol ? *reinterpret_cast<const bf16x8*>(Ol + c) : bf16x8{};
 #pragma unroll
-  for (int c = 0; c < HD; c += 8) {
-    bf16x8 x = *reinterpret_cast<const bf16x8*>(dO + c);
-    bf16x8 y = *reinterpret_cast<const bf16x8*>(O + c);
-    bf16x8 z = Ol ? *reinterpret_cast<const bf16x8*>(Ol + c) : bf16x8{};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc += (float)x[e] * ((float)y[e] + (float)z[e]);
+      for (int e = 0; e < 8; ++e) acc += (float)x[e] * ((float)y[e] + (float)z[e]);
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if ((lane & 7) == 0 && c < HH) a.delta[(int64_t)(b * a.H + c / HD) * a.T + q] = acc;
   }
-  a.delta[(int64_t)(b * a.H + h) * a.T + q] = acc;
 }
 
 // ======================================================= backward: dQ (+ relative bins G)
@@ -2487,7 +2495,7 @@ extern "C" int ste_attention_bwd(const ste_attn_args* a, void* stream) {
     }
     return 0;
   }
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((nrow + 255) / 256)), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)(((int64_t)a->B * a->T + 3) / 4)), dim3(256), 0, s, *a);
   STE_CHECK_LAUNCH();
   dim3 grid((unsigned)(((a->T + TQ - 1) / TQ) * a->H * a->B));
   const bool rel = a->rel_E != nullptr, drop = a->drop_p > 0.f;
