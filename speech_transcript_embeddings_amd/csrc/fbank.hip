@@ -4,9 +4,9 @@
 // feature_extraction_seamless_m4t.py:112-138,240-301, tf:audio_utils.py:809-1017),
 // plus the collate padding of ref:training/trainer_unfreeze.py:880-921.
 //
-// Kernel 1 (one wavefront per 400-sample frame, 4 frames per block):
+// Kernel 1 (one wavefront per 400-sample frame, 4 waves per block, 4 frames per wave):
 //   x*2^15 -> remove frame mean -> pre-emphasis 0.97 (y0 *= 0.03) -> povey window
-//   -> 512-point radix-2 FFT in LDS (fp32, twiddles from double sincos) -> |X|^2
+//   -> 512-point radix-8 Stockham FFT in registers (fp32, twiddles from double sincos) -> |X|^2
 //   -> 80 kaldi-scale triangular mel filters built in mel space (sparse, per-block
 //   table) -> max(1.1920929e-7, .) -> natural log.
 // Kernel 2 (one block per clip): per-mel-bin mean and unbiased variance over the clip's
@@ -85,11 +85,44 @@ __global__ __launch_bounds__(256) void fbank_tables_kernel(float* __restrict__ t
 }
 
 constexpr int FRAMES_PER_WAVE = 4;
+constexpr int XPAD = NFFT + NFFT / 8;   // exchange buffer: one float2 of padding per 8
 
+STE_DEV int xpad(int i) { return i + (i >> 3); }
+STE_DEV float2 cmul(float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+STE_DEV float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+STE_DEV float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+
+// In-register 8-point DFT, natural order in and out (decimation in frequency: one radix-2 layer
+// with W8 twiddles, then two 4-point DFTs giving the even and the odd outputs).
+STE_DEV void dft8(float2 (&v)[8]) {
+  constexpr float C = 0.70710678118654752f;
+  float2 a[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { a[k] = cadd(v[k], v[k + 4]); a[k + 4] = csub(v[k], v[k + 4]); }
+  a[5] = make_float2(C * (a[5].x + a[5].y), C * (a[5].y - a[5].x));     // * W8^1
+  a[6] = make_float2(a[6].y, -a[6].x);                                  // * W8^2 = -i
+  a[7] = make_float2(C * (a[7].y - a[7].x), -C * (a[7].x + a[7].y));    // * W8^3
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float2 b0 = cadd(a[4 * h], a[4 * h + 2]), b2 = csub(a[4 * h], a[4 * h + 2]);
+    const float2 b1 = cadd(a[4 * h + 1], a[4 * h + 3]), d = csub(a[4 * h + 1], a[4 * h + 3]);
+    const float2 b3 = make_float2(d.y, -d.x);                           // * -i
+    v[h] = cadd(b0, b1);          // X[2k + h], k = 0..3
+    v[2 + h] = cadd(b2, b3);
+    v[4 + h] = csub(b0, b1);
+    v[6 + h] = csub(b2, b3);
+  }
+}
+
+// Frame -> 80 log-mel energies.  The 512-point FFT is a radix-8 Stockham transform held in
+// registers (lane j owns points j + 64 r): three passes of dft8, two exchanges through a padded
+// per-wave LDS buffer, twiddles e^{-2πik/512} from the fp64-built table; the input needs no
+// bit reversal and lane j ends with X[j + 64 r].  (The radix-2 version took 9 LDS round trips
+// per frame and half of the kernel's time.)
 __global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restrict__ wav, int64_t ld_wav,
                                                          const int32_t* __restrict__ lengths, int Fmax,
                                                          const float* __restrict__ tab, float* __restrict__ work) {
-  __shared__ float2 sbuf[4][NFFT];
+  __shared__ float2 sbuf[4][XPAD];
   __shared__ float2 stw[NFFT / 2];
   __shared__ float swin[FRAME];
   __shared__ int sm_start[NMEL], sm_len[NMEL], sm_off[NMEL];
@@ -111,72 +144,74 @@ __global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restri
 
   const int len = lengths[b];
   const int F = len >= FRAME ? 1 + (len - FRAME) / HOP : 0;
+  float2* buf = sbuf[w];
   for (int fi = 0; fi < FRAMES_PER_WAVE; ++fi) {
   const int f = (blockIdx.x * 4 + w) * FRAMES_PER_WAVE + fi;
   if (f >= F || f >= Fmax) return;  // whole wave exits; no block barrier follows
   const float* x = wav + (int64_t)b * ld_wav + (int64_t)f * HOP;
-  float v[7];
+  float c[7];
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     const int n = lane + 64 * i;
-    v[i] = n < FRAME ? x[n] * 32768.0f : 0.f;
-    s += v[i];
+    c[i] = n < FRAME ? x[n] * 32768.0f : 0.f;
+    s += c[i];
   }
   const float mean = wave_sum(s) * (1.0f / FRAME);
-  float2* buf = sbuf[w];
-  // write (x - mean) to LDS, then pre-emphasis + window into bit-reversed complex slots
 #pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const int n = lane + 64 * i;
-    if (n < FRAME) buf[n].x = v[i] - mean;
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  float y[8];
+  for (int i = 0; i < 7; ++i) c[i] = c[i] - mean;   // n >= FRAME: masked below
+  // pre-emphasis (x[n] - 0.97 x[n-1], x[0] * 0.03) and window: x[n-1] is lane-1's value, or
+  // lane 63's of the previous row for lane 0
+  float2 v[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int n = lane + 64 * i;
     float val = 0.f;
-    if (n < FRAME) {
-      const float cur = buf[n].x;
-      val = (n == 0) ? cur * (1.0f - 0.97f) : cur - 0.97f * buf[n - 1].x;
-      val *= swin[n];
+    if (i < 7) {
+      const float up = __shfl(c[i], (lane + 63) & 63, 64);
+      const float wrap = i > 0 ? __shfl(c[i - 1], 63, 64) : 0.f;
+      const float prev = lane > 0 ? up : wrap;
+      if (n < FRAME) {
+        val = (n == 0) ? c[i] * (1.0f - 0.97f) : c[i] - 0.97f * prev;
+        val *= swin[n];
+      }
     }
-    y[i] = val;
+    v[i] = make_float2(val, 0.f);
   }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
+  // Stockham radix-8: pass Ns in {1, 8, 64}; lane j reads points j + 64 r, twiddles by
+  // W512^(r (j mod Ns) 64/Ns), runs dft8 and writes (j/Ns) Ns 8 + (j mod Ns) + r Ns
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int n = lane + 64 * i;
-    const int rev = __builtin_bitreverse32((unsigned)n) >> (32 - 9);
-    buf[rev] = make_float2(y[i], 0.f);
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  // iterative radix-2 DIT, 256 butterflies per stage, 4 per lane
+  for (int pass = 0; pass < 3; ++pass) {
+    const int Ns = pass == 0 ? 1 : pass == 1 ? 8 : 64;
+    if (pass > 0) {
+      const int jm = lane & (Ns - 1), step = jm * (64 / Ns);
 #pragma unroll
-  for (int half = 1; half < NFFT; half <<= 1) {
-    const int tstride = (NFFT / 2) / half;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = lane + 64 * i;            // butterfly id 0..255
-      const int grp = j / half, pos = j % half;
-      const int i0 = grp * 2 * half + pos, i1 = i0 + half;
-      const float2 tw = stw[pos * tstride];
-      const float2 a = buf[i0], bb = buf[i1];
-      const float2 t = make_float2(bb.x * tw.x - bb.y * tw.y, bb.x * tw.y + bb.y * tw.x);
-      buf[i0] = make_float2(a.x + t.x, a.y + t.y);
-      buf[i1] = make_float2(a.x - t.x, a.y - t.y);
+      for (int r = 1; r < 8; ++r) {
+        const int k = r * step;                       // < 512
+        float2 tw = stw[k & 255];
+        if (k & 256) tw = make_float2(-tw.x, -tw.y);
+        v[r] = cmul(v[r], tw);
+      }
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+    dft8(v);
+    if (pass < 2) {
+      const int base = (lane / Ns) * Ns * 8 + (lane & (Ns - 1));
+#pragma unroll
+      for (int r = 0; r < 8; ++r) buf[xpad(base + r * Ns)] = v[r];
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = buf[xpad(lane + 64 * r)];
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
   }
+  // lane j holds X[j + 64 r]: power of bins 0..256
   float* pw = spow[w];
-  for (int k = lane; k < NBIN; k += 64) {
-    const float2 z = buf[k];
-    pw[k] = z.x * z.x + z.y * z.y;
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int k = lane + 64 * r;
+    if (k < NBIN) pw[k] = v[r].x * v[r].x + v[r].y * v[r].y;
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
