@@ -248,10 +248,13 @@ int ste_attn_pool_fwd(const void* t, const float* w2, const float* b2, const voi
  * two-pass weight-gradient GEMM), dw2 fp32 [Hh] (+=), db2 fp32 [1] (+=), db1 fp32 [Hh] (+=,
  * the first Linear's bias gradient Σ_l dt_l summed in fp32; may be NULL).
  * work: fp32 scratch of ste_attn_pool_bwd_work_floats(B, L, Hh) floats (dscore [B*L], then
- * per-row-chunk column-sum partials).  Hh <= 1024.  Replaces the autograd of ref:184-211. */
+ * per-row-chunk column-sum partials).  Hh <= 1024.  mask: the forward's int32 [B*L] mask or
+ * NULL; masked positions get no score gradient (masked_fill's backward, ref:199-200).  Replaces the
+ * autograd of ref:184-211. */
 int ste_attn_pool_bwd_work_floats(int B, int L, int Hh);
 int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float* weights, const float* dpooled,
-                      int B, int L, int Hh, int H, float* dh, void* dt, void* dt_lo, float* dw2, float* db2,
+                      const int32_t* mask, int B, int L, int Hh, int H, float* dh, void* dt, void* dt_lo, float* dw2,
+                      float* db2,
                       float* db1, float* work, void* stream);
 
 /* Pooling without the scorer, use_attentive_pooling=False

@@ -131,7 +131,10 @@ __global__ __launch_bounds__(NT) void pool_dp_kernel(const bf16* h, const float*
   }
 }
 
-__global__ __launch_bounds__(NT) void pool_dscore_kernel(const float* weights, int L, float* dsc, float* db2) {
+// masked positions get ds = 0 (the forward's masked_fill cuts their score gradient): that only
+// matters for an all-masked sample, whose weights are uniform rather than 0 at those positions
+__global__ __launch_bounds__(NT) void pool_dscore_kernel(const float* weights, const int32_t* mask, int L, float* dsc,
+                                                       float* db2) {
   __shared__ float red[8];
   const int b = blockIdx.x, tid = threadIdx.x;
   float acc = 0.f;
@@ -139,7 +142,8 @@ __global__ __launch_bounds__(NT) void pool_dscore_kernel(const float* weights, i
   const float tot = block_sum(acc, red);
   float dbs = 0.f;
   for (int l = tid; l < L; l += NT) {
-    const float ds = weights[b * L + l] * (dsc[b * L + l] - tot);
+    float ds = weights[b * L + l] * (dsc[b * L + l] - tot);
+    if (mask && mask[b * L + l] == 0) ds = 0.f;
     dsc[b * L + l] = ds;
     dbs += ds;
   }
@@ -715,7 +719,8 @@ extern "C" int ste_attn_pool_bwd_work_floats(int B, int L, int Hh) {
 }
 
 extern "C" int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float* weights,
-                                 const float* dpooled, int B, int L, int Hh, int H, float* dh, void* dt, void* dt_lo,
+                                 const float* dpooled, const int32_t* mask, int B, int L, int Hh, int H, float* dh,
+                                 void* dt, void* dt_lo,
                                  float* dw2, float* db2, float* db1, float* work, void* stream) {
   if (B <= 0 || L <= 0 || (Hh & 3) || (H & 3) || Hh > 4 * NT || !work || !dt) return STE_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
@@ -724,7 +729,7 @@ extern "C" int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, 
   hipLaunchKernelGGL(pool_dp_kernel, dim3(B, (L + POOL_DP_ROWS - 1) / POOL_DP_ROWS), dim3(NT), 0, s, (const bf16*)h,
                      dpooled, L, H, work);
   STE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(pool_dscore_kernel, dim3(B), dim3(NT), 0, s, weights, L, work, db2);
+  hipLaunchKernelGGL(pool_dscore_kernel, dim3(B), dim3(NT), 0, s, weights, mask, L, work, db2);
   STE_CHECK_LAUNCH();
   hipLaunchKernelGGL(pool_dz_kernel, dim3(B, nchunk), dim3(NT), 0, s, (const bf16*)t, w2, weights, dpooled, work, L,
                      Hh, H, dh, (bf16*)dt, (bf16*)dt_lo, part, rows);

@@ -626,7 +626,7 @@ class Engine:
         pooledb = self._e(nb, H, dtype=BF16)
         ops.attn_pool_fwd(t, s.p(name + ".attention.2.weight").view(-1), s.p(name + ".attention.2.bias"), hb, mask32,
                           nb, L, w, pooled, pooledb)
-        sv.update(t=t, w=w, hb=hb)
+        sv.update(t=t, w=w, hb=hb, mask=mask32)
         return pooled, pooledb
 
     def _pool_bwd(self, name, sv, dpooled, dh, nb, L):
@@ -644,7 +644,7 @@ class Engine:
         # dz = hi + lo (two GEMM passes)
         ops.attn_pool_bwd(t, s.p(name + ".attention.2.weight").view(-1), sv["hb"], sv["w"], dpooled, nb, L, dh, dz,
                           None if gw2 is None else gw2.view(-1), s.g(name + ".attention.2.bias"),
-                          db1=s.g(name + ".attention.0.bias"), dz_lo=dz_lo)
+                          db1=s.g(name + ".attention.0.bias"), dz_lo=dz_lo, mask=sv["mask"])
         ops.linear_dx(dz, s.w(name + ".attention.0.weight"), out=dh, beta=1.0)
         self._dw(dz, sv["hb"], name + ".attention.0.weight")
         if dz_lo is not None:

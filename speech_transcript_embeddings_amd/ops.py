@@ -344,15 +344,16 @@ def attn_pool_fwd(t, w2, b2, h, mask, B, L, weights, pooled, pooled_bf16=None):
          ptr(weights), ptr(pooled), ptr(pooled_bf16), _s())
 
 
-def attn_pool_bwd(t, w2, h, weights, dpooled, B, L, dh, dz, dw2=None, db2=None, db1=None, dz_lo=None):
+def attn_pool_bwd(t, w2, h, weights, dpooled, B, L, dh, dz, dw2=None, db2=None, db1=None, dz_lo=None, mask=None):
     """AttentivePooling backward: dh += ..., dz (bf16, + optional low half dz_lo), dw2/db2 and the
-    first Linear's bias gradient db1 (fp32 column sums of dz) accumulated."""
+    first Linear's bias gradient db1 (fp32 column sums of dz) accumulated.  mask: the forward's
+    int32 mask (masked positions get no score gradient, as masked_fill's backward)."""
     nwork = fn("ste_attn_pool_bwd_work_floats")(B, L, t.shape[-1])
     if nwork < 0:
         raise _lib.SteError(f"ste_attn_pool_bwd_work_floats failed with status {nwork}")
     work = torch.empty(nwork, device=t.device, dtype=F32)
-    call("ste_attn_pool_bwd", ptr(t), ptr(w2), ptr(h), ptr(weights), ptr(dpooled), B, L, t.shape[-1], h.shape[-1],
-         ptr(dh), ptr(dz), ptr(dz_lo), ptr(dw2), ptr(db2), ptr(db1), ptr(work), _s())
+    call("ste_attn_pool_bwd", ptr(t), ptr(w2), ptr(h), ptr(weights), ptr(dpooled), ptr(mask), B, L, t.shape[-1],
+         h.shape[-1], ptr(dh), ptr(dz), ptr(dz_lo), ptr(dw2), ptr(db2), ptr(db1), ptr(work), _s())
 
 
 def mean_pool_fwd(h, mask, B, L, cls, weights, pooled, pooled_bf16=None):

@@ -503,9 +503,15 @@ def test_attn_pool(ops, B, L, H, Hh):
     b2 = torch.randn(1, device=DEV)
     mask = torch.ones(B * L, dtype=torch.int32, device=DEV)
     mask[L - 7:L] = 0
+    if B > 2:   # ragged lengths (1 .. L) and one all-masked sample (uniform weights, as the -1e9 fill gives)
+        lens = torch.randint(1, L + 1, (B,), generator=torch.Generator().manual_seed(L))
+        lens[1] = 0
+        mask = (torch.arange(L)[None, :] < lens[:, None]).to(torch.int32).reshape(-1).to(DEV)
     weights = torch.empty(B * L, device=DEV)
     pooled = torch.empty(B, H, device=DEV)
     ops.attn_pool_fwd(t, w2, b2, h, mask, B, L, weights, pooled)
+    if B > 2:
+        assert torch.allclose(weights.view(B, L)[1], torch.full((L,), 1.0 / L, device=DEV))
     tr = t.float().clone().requires_grad_()
     hr = h.float().clone().requires_grad_()
     w2r = w2.clone().requires_grad_()
@@ -522,7 +528,7 @@ def test_attn_pool(ops, B, L, H, Hh):
     db2 = torch.zeros(1, device=DEV)
     db1 = torch.zeros(Hh, device=DEV)
     dz_lo = torch.empty_like(dz)
-    ops.attn_pool_bwd(t, w2, h, weights, dp, B, L, dh, dz, dw2, db2, db1=db1, dz_lo=dz_lo)
+    ops.attn_pool_bwd(t, w2, h, weights, dp, B, L, dh, dz, dw2, db2, db1=db1, dz_lo=dz_lo, mask=mask)
     dz_ref = tr.grad * (1 - t.float() ** 2)
     assert rel_err(dh, hr.grad) < 1e-5
     assert rel_err(dz, dz_ref) < 5e-3
@@ -530,7 +536,7 @@ def test_attn_pool(ops, B, L, H, Hh):
     assert rel_err(db1, dz_ref.sum(0)) < 1e-5                   # fp32 column sums (Σ dscore = 0 cancellation)
     assert rel_err(dw2 - 0.5, w2r.grad) < 1e-4
     db1_again = torch.zeros(Hh, device=DEV)                     # column sums without atomics: bitwise repeatable
-    ops.attn_pool_bwd(t, w2, h, weights, dp, B, L, torch.zeros_like(dh), dz, None, None, db1=db1_again)
+    ops.attn_pool_bwd(t, w2, h, weights, dp, B, L, torch.zeros_like(dh), dz, None, None, db1=db1_again, mask=mask)
     assert torch.equal(db1_again, db1)
     assert abs(db2.item() - b2r.grad.item()) < 1e-4
 
