@@ -274,9 +274,11 @@ int ste_weighted_pool_bwd(const float* weights, const float* dpooled, int B, int
  * probs fp32 [B*nh*S] saved for backward. */
 int ste_xattn1_fwd(const float* q, const void* k, const void* v, int64_t ldkv, const int32_t* mask, int B, int S,
                    int P, int nh, float scale, float drop_p, uint64_t seed, float* probs, float* out, void* stream);
+/* backward: mask = the forward's key mask (NULL = none); masked keys get no score gradient
+ * (masked_fill's backward, ref:148-153) — only visible for an all-masked sample */
 int ste_xattn1_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs, const float* dout,
-                   int B, int S, int P, int nh, float scale, float drop_p, uint64_t seed, float* dq, float* dk,
-                   float* dv, int64_t lddkv, void* stream);  /* dk/dv: fp32 rows of stride lddkv, += */
+                   const int32_t* mask, int B, int S, int P, int nh, float scale, float drop_p, uint64_t seed,
+                   float* dq, float* dk, float* dv, int64_t lddkv, void* stream);  /* dk/dv: fp32, += */
 /* nq (1 or 2) query sets sharing one K/V (the positive and corrupted transcripts' text->audio
  * calls, ref:training/trainer_unfreeze.py:525-542): query qi of sample b is row qi*B+b of q / out /
  * dout / dq and of probs [(qi*B+b)*nh + head]*S; query set qi drops with seed_qi, exactly as an
@@ -286,13 +288,14 @@ int ste_xattn_fwd(const float* q, const void* k, const void* v, int64_t ldkv, co
                   int nh, int nq, float scale, float drop_p, uint64_t seed0, uint64_t seed1, float* probs, float* out,
                   void* stream);
 int ste_xattn_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs, const float* dout,
-                  int B, int S, int P, int nh, int nq, float scale, float drop_p, uint64_t seed0, uint64_t seed1,
-                  float* dq, float* dk, float* dv, int64_t lddkv, void* stream);
+                  const int32_t* mask, int B, int S, int P, int nh, int nq, float scale, float drop_p,
+                  uint64_t seed0, uint64_t seed1, float* dq, float* dk, float* dv, int64_t lddkv, void* stream);
 /* As ste_xattn_bwd, but dk/dv are bf16 and WRITTEN (not accumulated), and colsum_part fp32
  * [B, 2P] receives per-sample column sums of dk (cols [0,P)) and dv (cols [P,2P)) in fp32, for the
  * key/value bias gradient; lddkv % 8 == 0. */
 int ste_xattn_bwd_bf16(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
-                       const float* dout, int B, int S, int P, int nh, int nq, float scale, float drop_p,
+                       const float* dout, const int32_t* mask, int B, int S, int P, int nh, int nq, float scale,
+                       float drop_p,
                        uint64_t seed0, uint64_t seed1, float* dq, void* dk, void* dv, int64_t lddkv,
                        float* colsum_part, void* stream);
 

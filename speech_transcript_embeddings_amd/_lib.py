@@ -138,16 +138,17 @@ _SIGS = {
     "ste_weighted_pool_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "ste_xattn1_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                c_float, c_uint64, c_void_p, c_void_p, c_void_p]),
-    "ste_xattn1_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                               c_float, c_float, c_uint64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "ste_xattn1_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                               c_int, c_int, c_float, c_float, c_uint64, c_void_p, c_void_p, c_void_p, c_int64,
+                               c_void_p]),
     "ste_xattn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
                               c_float, c_float, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
-    "ste_xattn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                              c_int, c_float, c_float, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_int64,
-                              c_void_p]),
-    "ste_xattn_bwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_int,
-                                   c_int, c_int, c_float, c_float, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p,
-                                   c_int64, c_void_p, c_void_p]),
+    "ste_xattn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                              c_int, c_int, c_int, c_float, c_float, c_uint64, c_uint64, c_void_p, c_void_p,
+                              c_void_p, c_int64, c_void_p]),
+    "ste_xattn_bwd_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int,
+                                   c_int, c_int, c_int, c_int, c_float, c_float, c_uint64, c_uint64, c_void_p,
+                                   c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "ste_align_attn_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                    c_float, c_uint64, c_void_p, c_void_p, c_int64, c_void_p]),
     "ste_align_attn_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int,

@@ -373,10 +373,10 @@ __global__ __launch_bounds__(NT) void xattn_fwd_kernel(const float* q, const bf1
 // dq is written.
 template <int NQ, bool OUT_BF16>
 __global__ __launch_bounds__(NT) void xattn_bwd_kernel(const float* q, const bf16* k, const bf16* v, int64_t ldkv,
-                                                     const float* probs, const float* dout, int B, int S, int P,
-                                                     int nh, float scale, float drop_p, uint64_t seed0,
-                                                     uint64_t seed1, float* dq, void* dk_, void* dv_, int64_t lddkv,
-                                                     float* part) {
+                                                     const float* probs, const float* dout, const int32_t* mask,
+                                                     int B, int S, int P, int nh, float scale, float drop_p,
+                                                     uint64_t seed0, uint64_t seed1, float* dq, void* dk_, void* dv_,
+                                                     int64_t lddkv, float* part) {
   extern __shared__ float sds[];  // NQ * S: dp, then ds
   __shared__ float sq[NQ][256], sdo[NQ][256], red[NQ][NT / 64];
   __shared__ f32x4 racc[NT];
@@ -426,7 +426,8 @@ __global__ __launch_bounds__(NT) void xattn_bwd_kernel(const float* q, const bf1
 #pragma unroll
   for (int qi = 0; qi < NQ; ++qi) {
     const float* pr = probs + ((int64_t)(qi * B + b) * nh + hh) * S;
-    for (int s = tid; s < S; s += NT) sds[qi * S + s] = pr[s] * (sds[qi * S + s] - rs[qi]) * scale;
+    for (int s = tid; s < S; s += NT)   // masked keys: no score gradient (masked_fill's backward)
+      sds[qi * S + s] = (mask && mask[b * S + s] == 0) ? 0.f : pr[s] * (sds[qi * S + s] - rs[qi]) * scale;
   }
   __syncthreads();
   // dq[qi] = Σ_s ds k[s];  dk[s] += Σ_qi ds q_qi;  dv[s] += Σ_qi p' dout_qi  (4 columns per lane)
@@ -787,7 +788,8 @@ extern "C" int ste_xattn_fwd(const float* q, const void* k, const void* v, int64
 
 template <bool OUT_BF16>
 static int xattn_bwd_launch(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
-                            const float* dout, int B, int S, int P, int nh, int nq, float scale, float drop_p,
+                            const float* dout, const int32_t* mask, int B, int S, int P, int nh, int nq, float scale,
+                            float drop_p,
                             uint64_t seed0, uint64_t seed1, float* dq, void* dk, void* dv, int64_t lddkv, float* part,
                             void* stream) {
   if (!xattn_shape_ok(B, S, P, nh, nq) || (nq != 1 && nq != 2) || (ldkv & 7) || lddkv < P ||
@@ -797,29 +799,29 @@ static int xattn_bwd_launch(const float* q, const void* k, const void* v, int64_
   const size_t lds = (size_t)nq * S * sizeof(float);
   if (nq == 1)
     hipLaunchKernelGGL((xattn_bwd_kernel<1, OUT_BF16>), dim3(B, nh), dim3(NT), lds, (hipStream_t)stream, q,
-                       (const bf16*)k, (const bf16*)v, ldkv, probs, dout, B, S, P, nh, scale, drop_p, seed0, seed1, dq,
-                       dk, dv, lddkv, part);
+                       (const bf16*)k, (const bf16*)v, ldkv, probs, dout, mask, B, S, P, nh, scale, drop_p, seed0,
+                       seed1, dq, dk, dv, lddkv, part);
   else
     hipLaunchKernelGGL((xattn_bwd_kernel<2, OUT_BF16>), dim3(B, nh), dim3(NT), lds, (hipStream_t)stream, q,
-                       (const bf16*)k, (const bf16*)v, ldkv, probs, dout, B, S, P, nh, scale, drop_p, seed0, seed1, dq,
-                       dk, dv, lddkv, part);
+                       (const bf16*)k, (const bf16*)v, ldkv, probs, dout, mask, B, S, P, nh, scale, drop_p, seed0,
+                       seed1, dq, dk, dv, lddkv, part);
   STE_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int ste_xattn_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
-                             const float* dout, int B, int S, int P, int nh, int nq, float scale, float drop_p,
-                             uint64_t seed0, uint64_t seed1, float* dq, float* dk, float* dv, int64_t lddkv,
-                             void* stream) {
-  return xattn_bwd_launch<false>(q, k, v, ldkv, probs, dout, B, S, P, nh, nq, scale, drop_p, seed0, seed1, dq, dk, dv,
+                             const float* dout, const int32_t* mask, int B, int S, int P, int nh, int nq, float scale,
+                             float drop_p, uint64_t seed0, uint64_t seed1, float* dq, float* dk, float* dv,
+                             int64_t lddkv, void* stream) {
+  return xattn_bwd_launch<false>(q, k, v, ldkv, probs, dout, mask, B, S, P, nh, nq, scale, drop_p, seed0, seed1, dq, dk, dv,
                                  lddkv, nullptr, stream);
 }
 
 extern "C" int ste_xattn_bwd_bf16(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
-                                  const float* dout, int B, int S, int P, int nh, int nq, float scale, float drop_p,
-                                  uint64_t seed0, uint64_t seed1, float* dq, void* dk, void* dv, int64_t lddkv,
-                                  float* colsum_part, void* stream) {
-  return xattn_bwd_launch<true>(q, k, v, ldkv, probs, dout, B, S, P, nh, nq, scale, drop_p, seed0, seed1, dq, dk, dv,
+                                  const float* dout, const int32_t* mask, int B, int S, int P, int nh, int nq,
+                                  float scale, float drop_p, uint64_t seed0, uint64_t seed1, float* dq, void* dk,
+                                  void* dv, int64_t lddkv, float* colsum_part, void* stream) {
+  return xattn_bwd_launch<true>(q, k, v, ldkv, probs, dout, mask, B, S, P, nh, nq, scale, drop_p, seed0, seed1, dq, dk, dv,
                                 lddkv, colsum_part, stream);
 }
 
@@ -830,9 +832,10 @@ extern "C" int ste_xattn1_fwd(const float* q, const void* k, const void* v, int6
 }
 
 extern "C" int ste_xattn1_bwd(const float* q, const void* k, const void* v, int64_t ldkv, const float* probs,
-                              const float* dout, int B, int S, int P, int nh, float scale, float drop_p, uint64_t seed,
-                              float* dq, float* dk, float* dv, int64_t lddkv, void* stream) {
-  return ste_xattn_bwd(q, k, v, ldkv, probs, dout, B, S, P, nh, 1, scale, drop_p, seed, seed, dq, dk, dv, lddkv,
+                              const float* dout, const int32_t* mask, int B, int S, int P, int nh, float scale,
+                              float drop_p, uint64_t seed, float* dq, float* dk, float* dv, int64_t lddkv,
+                              void* stream) {
+  return ste_xattn_bwd(q, k, v, ldkv, probs, dout, mask, B, S, P, nh, 1, scale, drop_p, seed, seed, dq, dk, dv, lddkv,
                        stream);
 }
 

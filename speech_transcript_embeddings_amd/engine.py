@@ -763,7 +763,8 @@ class Engine:
             dkvb = self._e(ab * T, 2 * P, dtype=BF16)
             ops.xattn_bwd(hs["qt"], hs["kva"][:, :P], hs["kva"][:, P:], hs["probs_t"], dq_in, b, T, nh, dqt,
                           dkvb[:, :P], dkvb[:, P:], (_site_seed(hs["seed_t"], 0), _site_seed(hs["seed_t"], 1)),
-                          drop_p=hs["p_x"], colsum=s.fused("text_to_audio_attention.key.bias", 2, "g"))
+                          drop_p=hs["p_x"], colsum=s.fused("text_to_audio_attention.key.bias", 2, "g"),
+                          mask=ctx["a_mask32"])
             dqtb = ops.cast_bf16(dqt, self._e(nb, P, dtype=BF16))
             ops.linear_dx(dqtb, s.w("text_to_audio_attention.query.weight"), out=d_tproj, beta=1.0)
             self._dw(dqtb, hs["tprojb"], "text_to_audio_attention.query.weight")
@@ -785,7 +786,7 @@ class Engine:
             dkvtb = self._e(b * L, 2 * P, dtype=BF16)
             ops.xattn1_bwd(hs["qa"], hs["kvt"][:, :P], hs["kvt"][:, P:], hs["probs_a"], dqa_in, b, L, nh, dqa,
                            dkvtb[:, :P], dkvtb[:, P:], drop_p=hs["p_x"], seed=hs["seed_a"],
-                           colsum=s.fused("audio_to_text_attention.key.bias", 2, "g"))
+                           colsum=s.fused("audio_to_text_attention.key.bias", 2, "g"), mask=ctx["t_mask32"][: b * L])
             dqab = ops.cast_bf16(dqa, self._e(b, P, dtype=BF16))
             ops.linear_dx(dqab, s.w("audio_to_text_attention.query.weight"), out=d_aproj[:b], beta=1.0)
             self._dw(dqab, hs["aprojb"], "audio_to_text_attention.query.weight")
@@ -872,7 +873,8 @@ class Engine:
         st_a = self._ln(ya, "audio_fusion.1", 1e-5, y=afused)
         sv = dict(b=b, L=L, T=T, thb=thb, ahb=ahb, tprojb=tprojb, aprojb=aprojb, aseqb=aseqb, kva=kva, qt=qt,
                   probs_t=probs_t, att_tb=att_tb, seed_t=seed_t, tseqb=tseqb, kvt=kvt, qa=qa, probs_a=probs_a,
-                  att_ab=att_ab, seed_a=seed_a, p_x=p_x, tcat=tcat, acat=acat, yt=yt, st_t=st_t, ya=ya, st_a=st_a)
+                  att_ab=att_ab, seed_a=seed_a, p_x=p_x, tcat=tcat, acat=acat, yt=yt, st_t=st_t, ya=ya, st_a=st_a,
+                  am32=am32, tm32=tm32)
         return tfused, afused, sv
 
     def cross_backward(self, sv, d_tf, d_af):
@@ -905,7 +907,7 @@ class Engine:
         dqt = self._e(b, P)
         dkv = self._z(b * T, 2 * P)
         ops.xattn1_bwd(sv["qt"], sv["kva"][:, :P], sv["kva"][:, P:], sv["probs_t"], dq_in, b, T, nh, dqt, dkv[:, :P],
-                       dkv[:, P:], drop_p=sv["p_x"], seed=sv["seed_t"])
+                       dkv[:, P:], drop_p=sv["p_x"], seed=sv["seed_t"], mask=sv["am32"])
         dqtb = ops.cast_bf16(dqt, self._e(b, P, dtype=BF16))
         ops.linear_dx(dqtb, s.w("text_to_audio_attention.query.weight"), out=d_tproj, beta=1.0)
         self._dw(dqtb, sv["tprojb"], "text_to_audio_attention.query.weight")
@@ -927,7 +929,7 @@ class Engine:
         dqa = self._e(b, P)
         dkvt = self._z(b * L, 2 * P)
         ops.xattn1_bwd(sv["qa"], sv["kvt"][:, :P], sv["kvt"][:, P:], sv["probs_a"], dqa_in, b, L, nh, dqa,
-                       dkvt[:, :P], dkvt[:, P:], drop_p=sv["p_x"], seed=sv["seed_a"])
+                       dkvt[:, :P], dkvt[:, P:], drop_p=sv["p_x"], seed=sv["seed_a"], mask=sv["tm32"])
         dqab = ops.cast_bf16(dqa, self._e(b, P, dtype=BF16))
         ops.linear_dx(dqab, s.w("audio_to_text_attention.query.weight"), out=d_aproj, beta=1.0)
         self._dw(dqab, sv["aprojb"], "audio_to_text_attention.query.weight")

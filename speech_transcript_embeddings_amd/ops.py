@@ -371,14 +371,16 @@ def xattn1_fwd(q, k, v, mask, B, S, nh, probs, out, drop_p=0.0, seed=0):
          float(drop_p), int(seed) & (2**64 - 1), ptr(probs), ptr(out), _s())
 
 
-def xattn1_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, drop_p=0.0, seed=0, colsum=None):
+def xattn1_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, drop_p=0.0, seed=0, colsum=None, mask=None):
     """dk/dv fp32: accumulated (+=).  dk/dv bf16: written, and the fp32 column sums of [dk | dv]
-    are added into colsum [2P] (the fused key/value bias gradient) when given."""
+    are added into colsum [2P] (the fused key/value bias gradient) when given.  mask: the
+    forward's int32 key mask (masked keys get no score gradient)."""
     if dk.dtype == BF16:
-        return xattn_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, (seed,), drop_p=drop_p, colsum=colsum)
+        return xattn_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, (seed,), drop_p=drop_p, colsum=colsum,
+                         mask=mask)
     P = q.shape[-1]
     assert _ld(dk) == _ld(dv)
-    call("ste_xattn1_bwd", ptr(q), ptr(k), ptr(v), _ld(k), ptr(probs), ptr(dout), B, S, P, nh,
+    call("ste_xattn1_bwd", ptr(q), ptr(k), ptr(v), _ld(k), ptr(probs), ptr(dout), ptr(mask), B, S, P, nh,
          float((P // nh) ** -0.5), float(drop_p), int(seed) & (2**64 - 1), ptr(dq), ptr(dk), ptr(dv), _ld(dk), _s())
 
 
@@ -391,7 +393,7 @@ def xattn_fwd(q, k, v, mask, B, S, nh, probs, out, seeds, drop_p=0.0):
          float(drop_p), int(seeds[0]) & (2**64 - 1), int(seeds[-1]) & (2**64 - 1), ptr(probs), ptr(out), _s())
 
 
-def xattn_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, seeds, drop_p=0.0, colsum=None):
+def xattn_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, seeds, drop_p=0.0, colsum=None, mask=None):
     """dk/dv fp32: accumulated (+=).  dk/dv bf16: written (ste_xattn_bwd_bf16), and the fp32
     column sums of [dk | dv] are added into colsum [2P] when given."""
     P = q.shape[-1]
@@ -400,14 +402,14 @@ def xattn_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, seeds, drop_p=0.0, col
     if dk.dtype == BF16:
         assert dv.dtype == BF16
         part = torch.empty(B, 2 * P, device=q.device, dtype=F32)
-        call("ste_xattn_bwd_bf16", ptr(q), ptr(k), ptr(v), _ld(k), ptr(probs), ptr(dout), B, S, P, nh, nq,
+        call("ste_xattn_bwd_bf16", ptr(q), ptr(k), ptr(v), _ld(k), ptr(probs), ptr(dout), ptr(mask), B, S, P, nh, nq,
              float((P // nh) ** -0.5), float(drop_p), int(seeds[0]) & (2**64 - 1), int(seeds[-1]) & (2**64 - 1),
              ptr(dq), ptr(dk), ptr(dv), _ld(dk), ptr(part), _s())
         if colsum is not None:
             call("ste_colsum", ptr(part), 0, B, 2 * P, 2 * P, ptr(colsum), _s())
         return
     assert colsum is None
-    call("ste_xattn_bwd", ptr(q), ptr(k), ptr(v), _ld(k), ptr(probs), ptr(dout), B, S, P, nh, nq,
+    call("ste_xattn_bwd", ptr(q), ptr(k), ptr(v), _ld(k), ptr(probs), ptr(dout), ptr(mask), B, S, P, nh, nq,
          float((P // nh) ** -0.5), float(drop_p), int(seeds[0]) & (2**64 - 1), int(seeds[-1]) & (2**64 - 1),
          ptr(dq), ptr(dk), ptr(dv), _ld(dk), _s())
 

@@ -604,7 +604,7 @@ def test_xattn1(ops, drop_p):
     dq = torch.empty(B, P, device=DEV)
     dk = torch.zeros(B * S, P, device=DEV)
     dv = torch.zeros(B * S, P, device=DEV)
-    ops.xattn1_bwd(q, k, v, probs, do, B, S, nh, dq, dk, dv, drop_p=drop_p, seed=seed)
+    ops.xattn1_bwd(q, k, v, probs, do, B, S, nh, dq, dk, dv, drop_p=drop_p, seed=seed, mask=mask)
     assert rel_err(dq, qr.grad) < 1e-5
     assert rel_err(dk, kr.grad) < 1e-5
     assert rel_err(dv, vr.grad) < 1e-5
@@ -621,6 +621,7 @@ def test_xattn_two_query_sets(ops, B, S, P, nh, drop_p):
     k, v = kv[:, :P], kv[:, P:]
     mask = torch.ones(B * S, dtype=torch.int32, device=DEV)
     mask[S - 9:S] = 0
+    mask[S:2 * S] = 0   # an all-masked sample: uniform probabilities, no score gradient (masked_fill)
     probs = torch.empty(2 * B * nh * S, device=DEV)
     out = torch.empty(2 * B, P, device=DEV)
     seeds = (1234, 777)
@@ -646,7 +647,7 @@ def test_xattn_two_query_sets(ops, B, S, P, nh, drop_p):
     ref.backward(do)
     dq = torch.empty(2 * B, P, device=DEV)
     dkv = torch.zeros(B * S, 2 * P, device=DEV)
-    ops.xattn_bwd(q, k, v, probs, do, B, S, nh, dq, dkv[:, :P], dkv[:, P:], seeds, drop_p=drop_p)
+    ops.xattn_bwd(q, k, v, probs, do, B, S, nh, dq, dkv[:, :P], dkv[:, P:], seeds, drop_p=drop_p, mask=mask)
     assert rel_err(dq, qr.grad) < 1e-5
     assert rel_err(dkv[:, :P], kr.grad) < 1e-5
     assert rel_err(dkv[:, P:], vr.grad) < 1e-5
@@ -655,18 +656,19 @@ def test_xattn_two_query_sets(ops, B, S, P, nh, drop_p):
     dq2 = torch.empty_like(dq)
     dkvb = torch.full((B * S, 2 * P), 7.0, device=DEV).bfloat16()   # written, not accumulated
     cs = torch.full((2 * P,), 0.25, device=DEV)
-    ops.xattn_bwd(q, k, v, probs, do, B, S, nh, dq2, dkvb[:, :P], dkvb[:, P:], seeds, drop_p=drop_p, colsum=cs)
+    ops.xattn_bwd(q, k, v, probs, do, B, S, nh, dq2, dkvb[:, :P], dkvb[:, P:], seeds, drop_p=drop_p, colsum=cs,
+                  mask=mask)
     assert torch.equal(dq2, dq)
     assert torch.equal(dkvb, dkv.bfloat16())
     assert rel_err(cs - 0.25, dkv.sum(0)) < 1e-5
     dq1 = torch.empty(B, P, device=DEV)
     dkv1 = torch.zeros(B * S, 2 * P, device=DEV)
     ops.xattn1_bwd(q[:B], k, v, probs[:B * nh * S], do[:B], B, S, nh, dq1, dkv1[:, :P], dkv1[:, P:], drop_p=drop_p,
-                   seed=seeds[0])
+                   seed=seeds[0], mask=mask)
     dkv1b = torch.empty(B * S, 2 * P, device=DEV).bfloat16()
     cs1 = torch.zeros(2 * P, device=DEV)
     ops.xattn1_bwd(q[:B], k, v, probs[:B * nh * S], do[:B], B, S, nh, dq1, dkv1b[:, :P], dkv1b[:, P:],
-                   drop_p=drop_p, seed=seeds[0], colsum=cs1)
+                   drop_p=drop_p, seed=seeds[0], colsum=cs1, mask=mask)
     assert torch.equal(dkv1b, dkv1.bfloat16())
     assert rel_err(cs1, dkv1.sum(0)) < 1e-5
 
