@@ -80,9 +80,21 @@ typedef struct {
   int act;
   float drop_p; uint64_t seed; int64_t drop_ld;
   float* ws; int64_t ws_bytes;      /* split-K workspace for weight gradients (optional) */
+  int c3_lo;                        /* C3 <- bf16(v - bf16(v)), the low half, instead of bf16(v):
+                                       with C = bf16(v) the two make the [hi | lo] split image the
+                                       next precise-forward GEMM reads (see ste_split_bf16) */
 } ste_gemm_args;
 
 int ste_gemm(const ste_gemm_args* args, void* stream);
+
+/* The same contract with fp32 A, B (and fp32 C2 / Z) on the exact-f32 matrix core
+ * (v_mfma_f32_16x16x4_f32): the projection, cross-attention query / output, fusion and text
+ * pooling-scorer Linears of the heads (ref:training/trainer_unfreeze.py:66-99,125-168,171-211,
+ * 470-477), computed in fp32 as the reference does.  KC operands need K % 4 == 0 and
+ * ld % 4 == 0, KM operands (M or N) % 4 == 0; A, B 16-B aligned; batch 1.  A weight gradient
+ * (plain epilogue, fp32 C) with K >= 1024 whose tiles cannot fill the chip is split along K
+ * into slabs of ws (when given) summed in slab order. */
+int ste_gemm_f32(const ste_gemm_args* args, void* stream);
 
 /* Which kernel ste_gemm would launch for these args (no launch, host-only):
  * STE_GEMM_KERNEL_SMALL/BIG/8PH + variant, variant = (a_kc ? 0 : 2) + (b_kc ? 0 : 1).
@@ -133,6 +145,8 @@ typedef struct {
   float drop_p; uint64_t seed;      /* dropout on the output (index row*cols+col) */
   void* q8; void* q8s; int64_t ldq8; /* MX-fp8 output (optional, cols % 128 == 0): e4m3 [rows][ldq8]
                                         + E8M0 [rows][cols/32], the input of ste_gemm_mx8 */
+  void* ylo; int64_t ldylo;         /* bf16 low half bf16(y - bf16(y)) (optional): with yb, the
+                                       [hi | lo] split image of y (see ste_split_bf16) */
 } ste_ln_fwd_args;
 int ste_layernorm_fwd(const ste_ln_fwd_args* a, void* stream);
 
@@ -207,6 +221,11 @@ typedef struct {
   void* o_lo; int64_t ldolo;
 } ste_attn_args;
 int ste_attention_fwd(const ste_attn_args* a, void* stream);
+/* fp32 forward of the text encoder's attention (the precise text forward, see ste_split_bf16):
+ * q/k/v fp32 (row strides ld*, head h at columns h*64..), rel_E must be NULL; o32 fp32 [B*T, ldo32]
+ * (optional) receives O; a->o / a->o_lo (bf16, optional) its hi / lo halves and a->lse the LSE, in the
+ * conventions of ste_attention_fwd, so ste_attention_bwd runs on bf16 copies of q/k/v. */
+int ste_attention_fwd_f32(const ste_attn_args* a, float* o32, int64_t ldo32, void* stream);
 int ste_attention_bwd(const ste_attn_args* a, void* stream);
 
 /* ----------------------------------------------- Conformer conv module core --
@@ -256,6 +275,14 @@ int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float
                       const int32_t* mask, int B, int L, int Hh, int H, float* dh, void* dt, void* dt_lo, float* dw2,
                       float* db2,
                       float* db1, float* work, void* stream);
+/* The same pooling on fp32 states (t fp32 [B*L, Hh] from ste_gemm_f32, h fp32 [B*L, H]; dt fp32,
+ * no low half): the text side, whose positive and corrupted transcripts' pooled vectors are
+ * differenced by the loss gradient (see ste_gemm_f32). */
+int ste_attn_pool_fwd_f32(const float* t, const float* w2, const float* b2, const float* h, const int32_t* mask,
+                          int B, int L, int Hh, int H, float* weights, float* pooled, void* pooled_bf16, void* stream);
+int ste_attn_pool_bwd_f32(const float* t, const float* w2, const float* h, const float* weights, const float* dpooled,
+                          const int32_t* mask, int B, int L, int Hh, int H, float* dh, float* dt, float* dw2,
+                          float* db2, float* db1, float* work, void* stream);
 
 /* Pooling without the scorer, use_attentive_pooling=False
  * (ref:training/trainer_unfreeze.py:578-580 text `last_hidden_state[:, 0, :]`, :621-636 audio
@@ -264,6 +291,9 @@ int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float
  * weights, read by the backward), pooled fp32 [B,H] and bf16 [B,H] (optional). */
 int ste_mean_pool_fwd(const void* h, const int32_t* mask, int B, int L, int H, int cls, float* weights, float* pooled,
                       void* pooled_bf16, void* stream);
+/* The same on fp32 states h [B*L, H]. */
+int ste_mean_pool_fwd_f32(const float* h, const int32_t* mask, int B, int L, int H, int cls, float* weights,
+                          float* pooled, void* pooled_bf16, void* stream);
 /* Backward of any fixed-weight pooling: dh fp32 [B*L,H] += weights[b,l] * dpooled fp32 [B,H]. */
 int ste_weighted_pool_bwd(const float* weights, const float* dpooled, int B, int L, int H, float* dh, void* stream);
 
@@ -392,6 +422,14 @@ int ste_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_
               float beta2, float eps, float wd, int step, const double* sumsq, float max_norm, void* stream);
 
 /* ------------------------------------------------------------ elementwise -- */
+/* Split-bf16 operand image: y [rows][nblk*K] bf16 (nblk 1-3) gets nblk copies of x [rows][K] fp32,
+ * copy i the high half bf16(x) or, when bit i of lo_mask is set, the low half bf16(x - bf16(x)).
+ * ste_gemm on A = [x_hi | x_lo] (nblk 2, mask 2) and B = [W | W] (the bf16 weight twice, K' = 2K)
+ * computes X·W_bf16ᵀ with the activations to ~16 mantissa bits: the text encoder's precise
+ * forward (every XLM-R Linear, tf:…xlm_roberta…:186-398).  The weight's own rounding is shared by
+ * the positive and corrupted transcripts, so it is not differenced by the loss gradient; the
+ * activations' is.  nblk 3 ([hi|lo|hi]·[hi|hi|lo]) adds the weight's low half. */
+int ste_split_bf16(const float* x, int64_t ldx, int64_t rows, int K, void* y, int nblk, int lo_mask, void* stream);
 int ste_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 /* y = alpha*x + beta*y over strided fp32 rows (gradient accumulation of head branches). */
 int ste_axpby2d(float* y, int64_t ldy, const float* x, int64_t ldx, int64_t rows, int cols, float alpha, float beta,

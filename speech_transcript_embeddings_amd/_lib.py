@@ -45,6 +45,7 @@ class GemmArgs(C.Structure):
         ("act", c_int),
         ("drop_p", c_float), ("seed", c_uint64), ("drop_ld", c_int64),
         ("ws", c_void_p), ("ws_bytes", c_int64),
+        ("c3_lo", c_int),
     ]
 
 
@@ -60,6 +61,7 @@ class LnFwdArgs(C.Structure):
         ("act", c_int),
         ("drop_p", c_float), ("seed", c_uint64),
         ("q8", c_void_p), ("q8s", c_void_p), ("ldq8", c_int64),
+        ("ylo", c_void_p), ("ldylo", c_int64),
     ]
 
 
@@ -109,6 +111,7 @@ class AttnArgs(C.Structure):
 # name -> (restype, argtypes); every symbol declared in include/ste.h
 _SIGS = {
     "ste_gemm": (c_int, [C.POINTER(GemmArgs), c_void_p]),
+    "ste_gemm_f32": (c_int, [C.POINTER(GemmArgs), c_void_p]),
     "ste_gemm_kernel": (c_int, [C.POINTER(GemmArgs)]),
     "ste_gemm_kernel_name": (c_int, [C.POINTER(GemmArgs), c_char_p, c_int]),
     "ste_rows_extract": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
@@ -120,6 +123,8 @@ _SIGS = {
     "ste_layernorm_bwd_pair": (c_int, [C.POINTER(LnBwdArgs), C.POINTER(LnBwdArgs), c_void_p]),
     "ste_attention_fwd": (c_int, [C.POINTER(AttnArgs), c_void_p]),
     "ste_attention_bwd": (c_int, [C.POINTER(AttnArgs), c_void_p]),
+    "ste_attention_fwd_f32": (c_int, [C.POINTER(AttnArgs), c_void_p, c_int64, c_void_p]),
+    "ste_split_bf16": (c_int, [c_void_p, c_int64, c_int64, c_int, c_void_p, c_int, c_int, c_void_p]),
     "ste_glu_dwconv_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "ste_glu_dwconv_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                    c_void_p]),
@@ -133,8 +138,15 @@ _SIGS = {
                                   c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),
     "ste_attn_pool_bwd_work_floats": (c_int, [c_int, c_int, c_int]),
+    "ste_attn_pool_fwd_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                      c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ste_attn_pool_bwd_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                      c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p]),
     "ste_mean_pool_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),
+    "ste_mean_pool_fwd_f32": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                      c_void_p]),
     "ste_weighted_pool_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "ste_xattn1_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                c_float, c_uint64, c_void_p, c_void_p, c_void_p]),

@@ -292,7 +292,10 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(ste_attn_args a) {
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) store_bf16x4(O + 16 * dt + 4 * g, o[dt] * inv_l);
     }
-    if (g == 0) a.lse[(int64_t)(b * H + h) * T + myq] = m + logf(l);
+    // an all-masked row (every score at the finfo.min fill: uniform weights) saves -inf, as the
+    // relative-key kernels do; the backward then uses p = 1/T there (m + log l would round to
+    // the fill itself and give p = 1)
+    if (g == 0) a.lse[(int64_t)(b * H + h) * T + myq] = m == NEG_MASK ? -INFINITY : m + logf(l);
   }
 }
 
@@ -421,7 +424,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(ste_attn_args a) {
         float v = (s[t][r] + bias) * a.scale;
         const float f = sMask[kl];
         float p = 0.f;
-        if (qvalid && f > -0.5f) p = __expf((f > 0.5f ? v : NEG_MASK) - lse);
+        if (qvalid && f > -0.5f) p = lse == -INFINITY ? 1.0f / T : __expf((f > 0.5f ? v : NEG_MASK) - lse);
         float dpv = dp[t][r];
         if (DROP) dpv *= drop_scale(a.seed, drow + (uint64_t)key, thresh, inv_keep);
         const float ds = p * (dpv - dl);
@@ -577,7 +580,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(ste_attn_args a) {
         }
         float v = (s[n][r] + bias) * a.scale;
         if (kmasked) v = NEG_MASK;
-        float p = (kvalid && q < T) ? __expf(v - sL[ql]) : 0.f;
+        float p = (kvalid && q < T) ? (sL[ql] == -INFINITY ? 1.0f / T : __expf(v - sL[ql])) : 0.f;
         float dpv = dp[n][r];
         float pd = p;
         if (DROP) {

@@ -100,6 +100,12 @@ STE_DEV void store_part(void* p, bool is_bf16, f32x8 v, int nval) {
       else ((float*)p)[e] = v[e];
     }
 }
+// the low half v - bf16(v) of 8 values (the C3 copy of a [hi | lo] split output, c3_lo)
+STE_DEV f32x8 lo8(f32x8 v) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] -= (float)(bf16)v[e];
+  return v;
+}
 STE_DEV f32x8 ld8(const void* p, bool is_bf16, bool full, int nval) {
   if (!full) return load_part(p, is_bf16, nval);
   return is_bf16 ? load_bf16x8((const bf16*)p) : load_f32x8((const float*)p);
@@ -196,7 +202,7 @@ STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, 
     if (q8) mx8_block_store(v, q8->q + (int64_t)row * q8->ldq + col, q8->s + (int64_t)row * (q8->ldq >> 5) + (col >> 5),
                             lane);
     if (p.C) st8(cp, p.c_bf16, v, full, nval);
-    if (p.C3) st8((bf16*)p.C3 + offC + (int64_t)row * p.ldc3 + col, true, v, full, nval);
+    if (p.C3) st8((bf16*)p.C3 + offC + (int64_t)row * p.ldc3 + col, true, p.c3_lo ? lo8(v) : v, full, nval);
   }
 }
 
@@ -402,7 +408,7 @@ STE_DEV void epi_store16(const ste_gemm_args& p, const float* epi, int row0, int
     if (f.f_r) x += L.r[k];
     if (f.f_beta) x += L.c[k] * p.beta;
     st8((char*)p.C + (offC + row * p.ldc + col) * (f.c_bf ? 2 : 4), f.c_bf, x, full, nval);
-    if (f.f_c3) st8((bf16*)p.C3 + offC + row * p.ldc3 + col, true, x, full, nval);
+    if (f.f_c3) st8((bf16*)p.C3 + offC + row * p.ldc3 + col, true, p.c3_lo ? lo8(x) : x, full, nval);
   }
 }
 

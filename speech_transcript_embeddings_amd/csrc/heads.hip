@@ -33,10 +33,18 @@ STE_DEV float block_max(float v, float* red) {
   return s;
 }
 
-STE_DEV float dot_bf16_f32(const bf16* a, const float* b, int n, int lane) {
+// 4 consecutive elements of a bf16 or fp32 row (the pooling kernels run on the bf16 audio states
+// and on the fp32 text states, see ste_attn_pool_fwd_f32)
+STE_DEV f32x4 ld4(const bf16* p) { return load_bf16x4(p); }
+STE_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+STE_DEV void st4(bf16* p, f32x4 v) { store_bf16x4(p, v); }
+STE_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+template <typename T>
+STE_DEV float row_dot(const T* a, const float* b, int n, int lane) {
   float acc = 0.f;
   for (int c = lane * 4; c < n; c += 256) {
-    f32x4 x = load_bf16x4(a + c);
+    f32x4 x = ld4(a + c);
     f32x4 y = *reinterpret_cast<const f32x4*>(b + c);
     acc += x[0] * y[0] + x[1] * y[1] + x[2] * y[2] + x[3] * y[3];
   }
@@ -53,12 +61,13 @@ STE_DEV float dot_bf16_f32(const bf16* a, const float* b, int n, int lane) {
 constexpr int POOL_SC_ROWS = 16;
 constexpr int POOL_WS_NT = 512;
 
-__global__ __launch_bounds__(NT) void pool_score_kernel(const bf16* t, const float* w2, const float* b2,
+template <typename T>
+__global__ __launch_bounds__(NT) void pool_score_kernel(const T* t, const float* w2, const float* b2,
                                                       const int32_t* mask, int L, int Hh, float* sc) {
   const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int l1 = min(L, (int)(blockIdx.y + 1) * POOL_SC_ROWS);
   for (int l = blockIdx.y * POOL_SC_ROWS + w; l < l1; l += NT / 64) {
-    float s = dot_bf16_f32(t + (int64_t)(b * L + l) * Hh, w2, Hh, lane) + b2[0];
+    float s = row_dot(t + (int64_t)(b * L + l) * Hh, w2, Hh, lane) + b2[0];
     if (mask && mask[b * L + l] == 0) s = -1e9f;
     if (lane == 0) sc[b * L + l] = s;
   }
@@ -78,7 +87,8 @@ __global__ __launch_bounds__(NT) void pool_softmax_kernel(int L, float* sc) {
   for (int l = tid; l < L; l += NT) r[l] = __expf(r[l] - mx) * inv;
 }
 
-__global__ __launch_bounds__(POOL_WS_NT) void pool_wsum_kernel(const bf16* h, const float* weights, int L, int H,
+template <typename T>
+__global__ __launch_bounds__(POOL_WS_NT) void pool_wsum_kernel(const T* h, const float* weights, int L, int H,
                                                              float* pooled, bf16* pooled_bf16) {
   extern __shared__ float wl[];  // L weights
   __shared__ f32x4 part[POOL_WS_NT / 64][64];
@@ -89,9 +99,9 @@ __global__ __launch_bounds__(POOL_WS_NT) void pool_wsum_kernel(const bf16* h, co
   const int c = blockIdx.y * 256 + lane * 4;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (c < H) {
-    const bf16* hp = h + (int64_t)b * L * H + c;
+    const T* hp = h + (int64_t)b * L * H + c;
 #pragma unroll 4
-    for (int l = w; l < L; l += NW) acc += load_bf16x4(hp + (int64_t)l * H) * wl[l];
+    for (int l = w; l < L; l += NW) acc += ld4(hp + (int64_t)l * H) * wl[l];
   }
   part[w][lane] = acc;
   __syncthreads();
@@ -121,12 +131,13 @@ constexpr int POOL_DP_ROWS = 16;
 static int pool_dz_rows(int B, int L) { return (int64_t)B * ((L + 63) / 64) >= 512 ? 64 : 16; }
 constexpr int POOL_DW_NT = 1024;
 
-__global__ __launch_bounds__(NT) void pool_dp_kernel(const bf16* h, const float* dpooled, int L, int H, float* dp_out) {
+template <typename T>
+__global__ __launch_bounds__(NT) void pool_dp_kernel(const T* h, const float* dpooled, int L, int H, float* dp_out) {
   const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float* dp = dpooled + (int64_t)b * H;
   const int l1 = min(L, (int)(blockIdx.y + 1) * POOL_DP_ROWS);
   for (int l = blockIdx.y * POOL_DP_ROWS + w; l < l1; l += NT / 64) {
-    const float s = dot_bf16_f32(h + (int64_t)(b * L + l) * H, dp, H, lane);
+    const float s = row_dot(h + (int64_t)(b * L + l) * H, dp, H, lane);
     if (lane == 0) dp_out[b * L + l] = s;
   }
 }
@@ -151,9 +162,10 @@ __global__ __launch_bounds__(NT) void pool_dscore_kernel(const float* weights, c
   if (tid == 0 && db2) atomicAdd(db2, dbs);
 }
 
-__global__ __launch_bounds__(NT) void pool_dz_kernel(const bf16* t, const float* w2, const float* weights,
+template <typename T>
+__global__ __launch_bounds__(NT) void pool_dz_kernel(const T* t, const float* w2, const float* weights,
                                                    const float* dpooled, const float* dsc, int L, int Hh, int H,
-                                                   float* dh, bf16* dz, bf16* dz_lo, float* part, int rows) {
+                                                   float* dh, T* dz, bf16* dz_lo, float* part, int rows) {
   __shared__ f32x4 red[2 * NT];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int l0 = blockIdx.y * rows, l1 = min(L, l0 + rows);
@@ -175,15 +187,19 @@ __global__ __launch_bounds__(NT) void pool_dz_kernel(const bf16* t, const float*
 #pragma unroll 2
     for (int l = l0 + g; l < l1; l += groups) {
       const int64_t off = (int64_t)(b * L + l) * Hh + k;
-      const f32x4 tv = load_bf16x4(t + off);
+      const f32x4 tv = ld4(t + off);
       const float ds = dsc[b * L + l];
       g2 += tv * ds;
       f32x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = ds * wv[e] * (1.f - tv[e] * tv[e]);
       g1 += o;
-      if (dz_lo) store_bf16x4_split(dz + off, dz_lo + off, o);
-      else store_bf16x4(dz + off, o);
+      if constexpr (sizeof(T) == 2) {
+        if (dz_lo) store_bf16x4_split((bf16*)dz + off, dz_lo + off, o);
+        else st4(dz + off, o);
+      } else {
+        st4(dz + off, o);
+      }
     }
   }
   red[2 * tid] = g2;
@@ -223,7 +239,8 @@ __global__ __launch_bounds__(POOL_DW_NT) void pool_dw_kernel(const float* part, 
 // ------------------------------------------- CLS / masked-mean pooling (no scorer)
 // use_attentive_pooling=False (ref:578-580 text CLS, :621-636 audio masked mean).
 // weights[b][l] = CLS: [l == 0];  mean: mask[l] / max(sum(mask), 1e-9) (all-masked rows pool to 0).
-__global__ __launch_bounds__(NT) void mean_pool_fwd_kernel(const bf16* h, const int32_t* mask, int L, int H, int cls,
+template <typename T>
+__global__ __launch_bounds__(NT) void mean_pool_fwd_kernel(const T* h, const int32_t* mask, int L, int H, int cls,
                                                          float* weights, float* pooled, bf16* pooled_bf16) {
   extern __shared__ float sc[];  // L weights
   __shared__ float red[8];
@@ -241,7 +258,7 @@ __global__ __launch_bounds__(NT) void mean_pool_fwd_kernel(const bf16* h, const 
   for (int c = tid * 4; c < H; c += NT * 4) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int l = 0; l < Lr; ++l)
-      if (sc[l] != 0.f) acc += load_bf16x4(h + (int64_t)(b * L + l) * H + c);
+      if (sc[l] != 0.f) acc += ld4(h + (int64_t)(b * L + l) * H + c);
     acc *= inv;
     *reinterpret_cast<f32x4*>(pooled + (int64_t)b * H + c) = acc;
     if (pooled_bf16) store_bf16x4(pooled_bf16 + (int64_t)b * H + c, acc);
@@ -697,20 +714,32 @@ __global__ __launch_bounds__(NT) void rowmat_f32_kernel(const float* X, int64_t 
 
 }  // namespace
 
-extern "C" int ste_attn_pool_fwd(const void* t, const float* w2, const float* b2, const void* h, const int32_t* mask,
-                                 int B, int L, int Hh, int H, float* weights, float* pooled, void* pooled_bf16,
-                                 void* stream) {
+template <typename T>
+static int attn_pool_fwd(const T* t, const float* w2, const float* b2, const T* h, const int32_t* mask, int B, int L,
+                         int Hh, int H, float* weights, float* pooled, bf16* pooled_bf16, hipStream_t s) {
   if (B <= 0 || L <= 0 || (Hh & 3) || (H & 3) || L > 8192) return STE_ERR_SHAPE;
-  hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(pool_score_kernel, dim3(B, (L + POOL_SC_ROWS - 1) / POOL_SC_ROWS), dim3(NT), 0, s,
-                     (const bf16*)t, w2, b2, mask, L, Hh, weights);
+  hipLaunchKernelGGL(pool_score_kernel<T>, dim3(B, (L + POOL_SC_ROWS - 1) / POOL_SC_ROWS), dim3(NT), 0, s, t, w2, b2,
+                     mask, L, Hh, weights);
   STE_CHECK_LAUNCH();
   hipLaunchKernelGGL(pool_softmax_kernel, dim3(B), dim3(NT), 0, s, L, weights);
   STE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(pool_wsum_kernel, dim3(B, (H + 255) / 256), dim3(POOL_WS_NT), L * sizeof(float), s,
-                     (const bf16*)h, weights, L, H, pooled, (bf16*)pooled_bf16);
+  hipLaunchKernelGGL(pool_wsum_kernel<T>, dim3(B, (H + 255) / 256), dim3(POOL_WS_NT), L * sizeof(float), s, h, weights,
+                     L, H, pooled, pooled_bf16);
   STE_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int ste_attn_pool_fwd(const void* t, const float* w2, const float* b2, const void* h, const int32_t* mask,
+                                 int B, int L, int Hh, int H, float* weights, float* pooled, void* pooled_bf16,
+                                 void* stream) {
+  return attn_pool_fwd((const bf16*)t, w2, b2, (const bf16*)h, mask, B, L, Hh, H, weights, pooled, (bf16*)pooled_bf16,
+                       (hipStream_t)stream);
+}
+
+extern "C" int ste_attn_pool_fwd_f32(const float* t, const float* w2, const float* b2, const float* h,
+                                     const int32_t* mask, int B, int L, int Hh, int H, float* weights, float* pooled,
+                                     void* pooled_bf16, void* stream) {
+  return attn_pool_fwd(t, w2, b2, h, mask, B, L, Hh, H, weights, pooled, (bf16*)pooled_bf16, (hipStream_t)stream);
 }
 
 extern "C" int ste_attn_pool_bwd_work_floats(int B, int L, int Hh) {
@@ -719,21 +748,20 @@ extern "C" int ste_attn_pool_bwd_work_floats(int B, int L, int Hh) {
   return B * L + B * ((L + rows - 1) / rows) * 2 * Hh;
 }
 
-extern "C" int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float* weights,
-                                 const float* dpooled, const int32_t* mask, int B, int L, int Hh, int H, float* dh,
-                                 void* dt, void* dt_lo,
-                                 float* dw2, float* db2, float* db1, float* work, void* stream) {
+template <typename T>
+static int attn_pool_bwd(const T* t, const float* w2, const T* h, const float* weights, const float* dpooled,
+                         const int32_t* mask, int B, int L, int Hh, int H, float* dh, T* dt, bf16* dt_lo, float* dw2,
+                         float* db2, float* db1, float* work, hipStream_t s) {
   if (B <= 0 || L <= 0 || (Hh & 3) || (H & 3) || Hh > 4 * NT || !work || !dt) return STE_ERR_SHAPE;
-  hipStream_t s = (hipStream_t)stream;
   const int rows = pool_dz_rows(B, L), nchunk = (L + rows - 1) / rows;
   float* part = work + (int64_t)B * L;
-  hipLaunchKernelGGL(pool_dp_kernel, dim3(B, (L + POOL_DP_ROWS - 1) / POOL_DP_ROWS), dim3(NT), 0, s, (const bf16*)h,
-                     dpooled, L, H, work);
+  hipLaunchKernelGGL(pool_dp_kernel<T>, dim3(B, (L + POOL_DP_ROWS - 1) / POOL_DP_ROWS), dim3(NT), 0, s, h, dpooled, L,
+                     H, work);
   STE_CHECK_LAUNCH();
   hipLaunchKernelGGL(pool_dscore_kernel, dim3(B), dim3(NT), 0, s, weights, mask, L, work, db2);
   STE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(pool_dz_kernel, dim3(B, nchunk), dim3(NT), 0, s, (const bf16*)t, w2, weights, dpooled, work, L,
-                     Hh, H, dh, (bf16*)dt, (bf16*)dt_lo, part, rows);
+  hipLaunchKernelGGL(pool_dz_kernel<T>, dim3(B, nchunk), dim3(NT), 0, s, t, w2, weights, dpooled, work, L, Hh, H, dh,
+                     dt, dt_lo, part, rows);
   STE_CHECK_LAUNCH();
   if (dw2 || db1) {
     hipLaunchKernelGGL(pool_dw_kernel, dim3((2 * Hh + 63) / 64), dim3(POOL_DW_NT), 0, s, part, B * nchunk, Hh, dw2,
@@ -743,13 +771,38 @@ extern "C" int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, 
   return 0;
 }
 
-extern "C" int ste_mean_pool_fwd(const void* h, const int32_t* mask, int B, int L, int H, int cls, float* weights,
-                                 float* pooled, void* pooled_bf16, void* stream) {
+extern "C" int ste_attn_pool_bwd(const void* t, const float* w2, const void* h, const float* weights,
+                                 const float* dpooled, const int32_t* mask, int B, int L, int Hh, int H, float* dh,
+                                 void* dt, void* dt_lo, float* dw2, float* db2, float* db1, float* work, void* stream) {
+  return attn_pool_bwd((const bf16*)t, w2, (const bf16*)h, weights, dpooled, mask, B, L, Hh, H, dh, (bf16*)dt,
+                       (bf16*)dt_lo, dw2, db2, db1, work, (hipStream_t)stream);
+}
+
+extern "C" int ste_attn_pool_bwd_f32(const float* t, const float* w2, const float* h, const float* weights,
+                                     const float* dpooled, const int32_t* mask, int B, int L, int Hh, int H, float* dh,
+                                     float* dt, float* dw2, float* db2, float* db1, float* work, void* stream) {
+  return attn_pool_bwd(t, w2, h, weights, dpooled, mask, B, L, Hh, H, dh, dt, (bf16*)nullptr, dw2, db2, db1, work,
+                       (hipStream_t)stream);
+}
+
+template <typename T>
+static int mean_pool_fwd(const T* h, const int32_t* mask, int B, int L, int H, int cls, float* weights, float* pooled,
+                         bf16* pooled_bf16, hipStream_t s) {
   if (B <= 0 || L <= 0 || (H & 3) || L > 16384) return STE_ERR_SHAPE;
-  hipLaunchKernelGGL(mean_pool_fwd_kernel, dim3(B), dim3(NT), L * sizeof(float), (hipStream_t)stream, (const bf16*)h,
-                     mask, L, H, cls, weights, pooled, (bf16*)pooled_bf16);
+  hipLaunchKernelGGL(mean_pool_fwd_kernel<T>, dim3(B), dim3(NT), L * sizeof(float), s, h, mask, L, H, cls, weights,
+                     pooled, pooled_bf16);
   STE_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int ste_mean_pool_fwd(const void* h, const int32_t* mask, int B, int L, int H, int cls, float* weights,
+                                 float* pooled, void* pooled_bf16, void* stream) {
+  return mean_pool_fwd((const bf16*)h, mask, B, L, H, cls, weights, pooled, (bf16*)pooled_bf16, (hipStream_t)stream);
+}
+
+extern "C" int ste_mean_pool_fwd_f32(const float* h, const int32_t* mask, int B, int L, int H, int cls,
+                                     float* weights, float* pooled, void* pooled_bf16, void* stream) {
+  return mean_pool_fwd(h, mask, B, L, H, cls, weights, pooled, (bf16*)pooled_bf16, (hipStream_t)stream);
 }
 
 extern "C" int ste_weighted_pool_bwd(const float* weights, const float* dpooled, int B, int L, int H, float* dh,

@@ -79,7 +79,8 @@ STE_DEV void ln_fwd_row(const ste_ln_fwd_args& a, const LnParams<MAXC>& pr, int 
       v[c * 4 + e] = t;
     }
     if (a.y) *reinterpret_cast<f32x4*>(a.y + (int64_t)row * a.ldy + col) = y;
-    if (a.yb) store_bf16x4((bf16*)a.yb + (int64_t)row * a.ldyb + col, y);
+    if (a.ylo) store_bf16x4_split((bf16*)a.yb + (int64_t)row * a.ldyb + col, (bf16*)a.ylo + (int64_t)row * a.ldylo + col, y);
+    else if (a.yb) store_bf16x4((bf16*)a.yb + (int64_t)row * a.ldyb + col, y);
     if (a.q8) {  // MX-fp8 copy: 8 lanes x 4 columns = one 32-column block
       float am = fmaxf(fmaxf(fabsf(y[0]), fabsf(y[1])), fmaxf(fabsf(y[2]), fabsf(y[3])));
       am = fmaxf(am, __shfl_xor(am, 1));

@@ -9,6 +9,29 @@ __global__ void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, i
   for (; i + 3 < n; i += stride) store_bf16x4(y + i, *reinterpret_cast<const f32x4*>(x + i));
   if (i < n) for (; i < n; ++i) y[i] = (bf16)x[i];
 }
+// y [rows][nblk·K] bf16 = nblk blocks of x [rows][K] fp32: block i is hi = bf16(x) or, when bit i
+// of `lo_mask` is set, lo = bf16(x - hi).  A GEMM over the concatenated columns of A = [hi|lo] and
+// B = [W|W] sums a_hi·W + a_lo·W: the activation to ~16 mantissa bits against the bf16 weight,
+// with fp32 accumulation, on the bf16 MFMA (3 blocks, [hi|lo|hi]·[hi|hi|lo], add a_hi·w_lo).
+// 4 columns per thread.
+__global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows, int K,
+                                                   bf16* __restrict__ y, int nblk, int lo_mask) {
+  const int per_row = K >> 2;
+  const int64_t total = rows * per_row;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t r = t / per_row;
+    const int c = (int)(t - r * per_row) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + r * ldx + c);
+    bf16x4 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      hi[e] = (bf16)v[e];
+      lo[e] = (bf16)(v[e] - (float)hi[e]);
+    }
+    bf16* o = y + r * nblk * K + c;
+    for (int i = 0; i < nblk; ++i) *reinterpret_cast<bf16x4*>(o + (int64_t)i * K) = ((lo_mask >> i) & 1) ? lo : hi;
+  }
+}
 __global__ void scale_rows_kernel(float* x, const float* s, int64_t rows, int cols, int64_t ld) {
   int64_t r = blockIdx.x;
   float f = s[r];
@@ -227,6 +250,19 @@ extern "C" int ste_scale_rows(float* x, const float* scale, int64_t rows, int co
 extern "C" int ste_mask_i64_to_f32(const int64_t* m, float* f, int32_t* i32, int64_t n, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(mask_cvt_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, m, f, i32, n);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_split_bf16(const float* x, int64_t ldx, int64_t rows, int K, void* y, int nblk, int lo_mask,
+                              void* stream) {
+  if (rows <= 0 || K <= 0 || (K & 3) || (ldx & 3) || ((uintptr_t)x & 15) || ((uintptr_t)y & 7) || nblk < 1 ||
+      nblk > 3 || (lo_mask >> nblk))
+    return STE_ERR_SHAPE;
+  const int64_t work = rows * (K >> 2);
+  const unsigned blocks = (unsigned)((work + 255) / 256 < 8192 ? (work + 255) / 256 : 8192);
+  hipLaunchKernelGGL(split_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, ldx, rows, K, (bf16*)y, nblk,
+                     lo_mask);
   STE_CHECK_LAUNCH();
   return 0;
 }

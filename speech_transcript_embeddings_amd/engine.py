@@ -68,6 +68,11 @@ class Engine:
         # a Conformer layer's final LN and the next layer's FFN1 LN as one fused pass (forward and
         # backward, ste_layernorm_*_pair); STE_LN_PAIR=0: separate launches (A/B runs)
         self.ln_pair = os.environ.get("STE_LN_PAIR", "1") != "0"
+        # the text encoder's forward to ~fp32 accuracy (split-bf16 GEMMs, fp32 attention): the loss
+        # gradient differences the positive and corrupted transcripts' embeddings, so their bf16
+        # forward rounding reappeared in every gradient downstream.  STE_TEXT_PRECISE=0:
+        # the plain bf16 forward (A/B runs only)
+        self.precise_text = os.environ.get("STE_TEXT_PRECISE", "1") != "0"
 
     @property
     def fp8(self):
@@ -462,9 +467,14 @@ class Engine:
         hp = c.hidden_dropout_prob if train else 0.0
         ap = c.attention_probs_dropout_prob if train else 0.0
         x = self._e(M, D)
-        xb = self._e(M, D, dtype=BF16)
-        st = self._ln(emb, "text_encoder.embeddings.LayerNorm", c.layer_norm_eps, y=x, yb=xb, drop_p=hp,
-                      seed=_site_seed(base_seed, 1))
+        if self.precise_text:   # xb: the [hi | lo] split image [M, 2D] the precise forward's GEMMs read
+            xb = self._e(M, 2 * D, dtype=BF16)
+            st = self._ln(emb, "text_encoder.embeddings.LayerNorm", c.layer_norm_eps, y=x, yb=xb[:, :D], ylo=xb[:, D:],
+                          drop_p=hp, seed=_site_seed(base_seed, 1))
+        else:
+            xb = self._e(M, D, dtype=BF16)
+            st = self._ln(emb, "text_encoder.embeddings.LayerNorm", c.layer_norm_eps, y=x, yb=xb, drop_p=hp,
+                          seed=_site_seed(base_seed, 1))
         ctx.update(t_nb=nb, t_L=L, t_mask32=mask32, t_ids=ids, t_emb=emb, t_pos=pos_ids, t_st=st, t_hp=hp, t_ap=ap,
                    t_seed=base_seed)
         layers = []
@@ -472,9 +482,11 @@ class Engine:
             x, xb, sv = self._xlmr_fwd(i, x, xb, nb, L, mask32, hp, ap, _site_seed(base_seed, 10 + i), save)
             layers.append(sv if save else None)
         ctx["t_layers"] = layers
-        return x, xb
+        return x, (xb[:, :D] if self.precise_text else xb)
 
     def _xlmr_fwd(self, i, x, xb, nb, L, mask32, hp, ap, seed, save=True):
+        if self.precise_text:
+            return self._postln_fwd_x2(self.tcfg, XLMR_NAMES, i, x, xb, nb, L, mask32, hp, ap, seed, save)
         return self._postln_fwd(self.tcfg, XLMR_NAMES, i, x, xb, nb, L, mask32, hp, ap, seed, save)
 
     def _xlmr_bwd(self, i, sv, dx2, nb, L, mask32, hp, ap):
@@ -517,6 +529,52 @@ class Engine:
         if tr:
             sv.update(xb=xb, x1b=x1b, h=h)
         return x2, x2b, sv
+
+    def _postln_fwd_x2(self, c, nm, i, x, xs, nb, L, mask32, hp, ap, seed, save=True, act_p=0.0):
+        """_postln_fwd with the activations to ~fp32 accuracy.  Every Linear reads its input as the
+        [hi | lo] split image ([M, 2·in] bf16, hi = bf16(v), lo = bf16(v − hi)) against [W | W]
+        (ParamStore.w2): one bf16 MFMA GEMM over K' = 2·in computes the fp32 activations times the
+        bf16 weight — the weight's rounding is common to both transcripts, the activations' is what
+        the loss gradient differences.  The producers write the split images themselves (LayerNorm
+        hi + lo outputs, the FFN GEMM's bf16 output + low-half copy, the fp32 attention kernel's O +
+        O_lo), so no extra pass runs.  It saves what _postln_bwd reads, in the same dtypes (bf16
+        q/k/v, O + O_lo, pre-activation, the bf16 hi halves as the trained layers' dW operands), so
+        the backward is unchanged.  xs / the returned x2s: split images of x / x2."""
+        s = self.s
+        pre = nm["layer"].format(i=i)
+        M, D, F_ = x.shape[0], c.hidden_size, c.intermediate_size
+        H = c.num_attention_heads
+        eps = c.layer_norm_eps
+        tr = s.trainable_layer(pre + nm["q"] + ".weight")
+        sv = {"tr": tr, "seed": seed, "act_p": act_p}
+        qkvb = self._e(M, 3 * D, dtype=BF16) if save else None
+        qkv = ops.linear(xs, s.w2(pre + nm["q"] + ".weight", 3), s.fused(pre + nm["q"] + ".bias", 3, "p"),
+                         out_bf16_copy=qkvb)
+        os_ = self._e(M, 2 * D, dtype=BF16)   # [O | O_lo]: the O-proj input and the backward's O, O_lo
+        lse = self._e(nb * H * L)
+        ops.attention_fwd_f32(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B=nb, T=L, H=H, o32=None, lse=lse,
+                              o=os_[:, :D], o_lo=os_[:, D:], key_mask=mask32, scale=1.0 / math.sqrt(D // H),
+                              drop_p=ap, seed=_site_seed(seed, 1))
+        del qkv
+        y1 = ops.linear(os_, s.w2(pre + nm["o"] + ".weight"), s.p(pre + nm["o"] + ".bias"), residual=x, drop_p=hp,
+                        seed=_site_seed(seed, 2))
+        x1 = self._e(M, D)
+        x1s = self._e(M, 2 * D, dtype=BF16)
+        sv["st1"] = self._ln(y1, pre + nm["ln1"], eps, y=x1, yb=x1s[:, :D], ylo=x1s[:, D:])
+        zt = self._e(M, F_, dtype=BF16) if save else None  # GELU pre-activation, for backward only
+        hs_ = self._e(M, 2 * F_, dtype=BF16)              # [h | h_lo]
+        ops.linear(x1s, s.w2(pre + nm["fi"] + ".weight"), s.p(pre + nm["fi"] + ".bias"), act=ACT_GELU, pre_out=zt,
+                   drop_p=act_p, seed=_site_seed(seed, 4), out=hs_[:, :F_], out_bf16_copy=hs_[:, F_:], copy_lo=True)
+        y2 = ops.linear(hs_, s.w2(pre + nm["fo"] + ".weight"), s.p(pre + nm["fo"] + ".bias"), residual=x1, drop_p=hp,
+                        seed=_site_seed(seed, 3))
+        x2 = self._e(M, D)
+        x2s = self._e(M, 2 * D, dtype=BF16)
+        sv["st2"] = self._ln(y2, pre + nm["ln2"], eps, y=x2, yb=x2s[:, :D], ylo=x2s[:, D:])
+        if save:
+            sv.update(qkv=qkvb, o=os_[:, :D], o_lo=os_[:, D:], lse=lse, y1=y1, zt=zt, y2=y2)
+        if tr:
+            sv.update(xb=xs[:, :D], x1b=x1s[:, :D], h=hs_[:, :F_])
+        return x2, x2s, sv
 
     def _postln_bwd(self, c, nm, i, sv, dx2, nb, L, mask32, hp, ap):
         s = self.s
@@ -581,53 +639,80 @@ class Engine:
             ops.text_embed_bwd(ctx["t_ids"], ctx["t_pos"], demb, c.pad_token_id, gw, gp, gt)
 
     # ================================================================ heads
-    def _proj_fwd(self, name, xb, rows, train, seed, sv):
-        """EnhancedProjection ref:66-99 on bf16 input rows -> (fp32 [rows,P], bf16 copy)."""
+    # The heads run in fp32 (ste_gemm_f32, the fp32 pooling kernels) wherever the loss gradient
+    # differences their values: the text pooling, both projections, the cross-modal queries and
+    # outputs, and the fusion Linears.  The loss gradient w.r.t. the audio embedding is
+    # ds·(t_neg − t_pos) and every head gradient is a sum of nearly cancelling terms of the
+    # positive and the corrupted transcript (80 % shared tokens), so 2^-9 bf16 operand rounding
+    # there reappeared as 4–18 % gradient errors.  These GEMMs have M = batch rows
+    # (text pooling scorer: 2·b·L), so fp32 costs little.  The large audio-side GEMMs
+    # (audio_seq_to_projection, the text→audio K/V, the audio pooling scorer) stay bf16: the two
+    # transcripts attend to the same K/V, and the cross-attention backward sums both query sets'
+    # dK/dV in fp32 before its single rounding.
+    def _w32(self, name):
+        """fp32 master weight as a 2-D [out, in] matrix (the ste_gemm_f32 B operand)."""
+        w = self.s.p(name)
+        return w.view(w.shape[0], -1)
+
+    def _dw32(self, dy, x, wname):
+        """dW[N,K] += dyᵀ·x in fp32 (ste_gemm_f32) into the flat gradient buffer."""
+        g = self.s.g(wname)
+        if g is not None:
+            ops.linear_dw(dy, x, out=g.view(g.shape[0], -1), beta=1.0, ws=self.ws)
+
+    def _db32(self, dy, bname):
+        g = self.s.g(bname)
+        if g is not None:
+            ops.colsum(dy, g)
+
+    def _proj_fwd(self, name, x, rows, train, seed, sv):
+        """EnhancedProjection ref:66-99 in fp32: x [rows, H] -> [rows, P]."""
         s = self.s
         p_drop = self.m.dropout if train else 0.0
-        zp = self._e(rows, s.slots[name + ".projection.0.weight"].shape[0], dtype=BF16)
-        hb = ops.linear(xb, s.w(name + ".projection.0.weight"), s.p(name + ".projection.0.bias"), act=ACT_GELU,
-                        pre_out=zp, out_bf16=True, drop_p=p_drop, seed=seed)
-        y = ops.linear(hb, s.w(name + ".projection.3.weight"), s.p(name + ".projection.3.bias"))
-        P = y.shape[1]
-        out = self._e(rows, P)
+        zp = self._e(rows, s.slots[name + ".projection.0.weight"].shape[0])
+        h = ops.linear(x, self._w32(name + ".projection.0.weight"), s.p(name + ".projection.0.bias"), act=ACT_GELU,
+                       pre_out=zp, drop_p=p_drop, seed=seed)
+        y = ops.linear(h, self._w32(name + ".projection.3.weight"), s.p(name + ".projection.3.bias"))
+        out = self._e(rows, y.shape[1])
         st = self._ln(y, name + ".projection.4", 1e-5, y=out)
-        sv.update(xb=xb, zp=zp, hb=hb, y=y, st=st, p=p_drop, seed=seed)
+        sv.update(x=x, zp=zp, h=h, y=y, st=st, p=p_drop, seed=seed)
         return out
 
     def _proj_bwd(self, name, sv, dout, dx_out):
-        """returns nothing; writes d(input) into dx_out (fp32, +=)."""
+        """writes d(input) into dx_out (fp32, +=)."""
         s = self.s
-        rows, P = dout.shape
-        dyb = self._e(rows, P, dtype=BF16)
-        self._ln_bwd(dout, sv["y"], sv["st"], name + ".projection.4", dxb=dyb, dsum=s.g(name + ".projection.3.bias"))
-        dz = ops.linear_dx(dyb, s.w(name + ".projection.3.weight"), act=ACT_GELU_BWD, z=sv["zp"], out_bf16=True,
-                           drop_p=sv["p"], seed=sv["seed"], colsum=s.g(name + ".projection.0.bias"))
-        self._dw(dyb, sv["hb"], name + ".projection.3.weight")
-        ops.linear_dx(dz, s.w(name + ".projection.0.weight"), out=dx_out, beta=1.0)
-        self._dw(dz, sv["xb"], name + ".projection.0.weight")
+        dy = self._e(*dout.shape)
+        self._ln_bwd(dout, sv["y"], sv["st"], name + ".projection.4", dx=dy, dsum=s.g(name + ".projection.3.bias"))
+        dz = ops.linear_dx(dy, self._w32(name + ".projection.3.weight"), act=ACT_GELU_BWD, z=sv["zp"], drop_p=sv["p"],
+                           seed=sv["seed"], colsum=s.g(name + ".projection.0.bias"))
+        self._dw32(dy, sv["h"], name + ".projection.3.weight")
+        ops.linear_dx(dz, self._w32(name + ".projection.0.weight"), out=dx_out, beta=1.0)
+        self._dw32(dz, sv["x"], name + ".projection.0.weight")
 
-    def _pool_fwd(self, name, hb, mask32, nb, L, sv):
-        """AttentivePooling ref:171-211 -> pooled fp32 [nb, H] and bf16 copy.  With
-        use_attentive_pooling=False: text CLS row (ref:578-580) / audio masked mean (ref:621-636)."""
+    def _pool_fwd(self, name, h, hb, mask32, nb, L, sv):
+        """AttentivePooling ref:171-211 -> pooled fp32 [nb, H]: text on the fp32 states (scorer on
+        ste_gemm_f32), audio on the bf16 copy (hb; hb=None: fp32 as well).  With
+        use_attentive_pooling=False: text CLS row (ref:578-580) / audio masked mean (ref:621-636)
+        of the fp32 states."""
         s = self.s
-        H = hb.shape[1]
-        if not self.m.use_attentive_pooling:
-            w = self._e(nb * L)
-            pooled = self._e(nb, H)
-            pooledb = self._e(nb, H, dtype=BF16)
-            ops.mean_pool_fwd(hb, mask32, nb, L, name == "text_pooling", w, pooled, pooledb)
-            sv.update(w=w)
-            return pooled, pooledb
-        t = ops.linear(hb, s.w(name + ".attention.0.weight"), s.p(name + ".attention.0.bias"), act=ACT_TANH,
-                       out_bf16=True)
+        H = h.shape[1]
         w = self._e(nb * L)
         pooled = self._e(nb, H)
-        pooledb = self._e(nb, H, dtype=BF16)
-        ops.attn_pool_fwd(t, s.p(name + ".attention.2.weight").view(-1), s.p(name + ".attention.2.bias"), hb, mask32,
-                          nb, L, w, pooled, pooledb)
-        sv.update(t=t, w=w, hb=hb, mask=mask32)
-        return pooled, pooledb
+        if not self.m.use_attentive_pooling:
+            ops.mean_pool_fwd(h, mask32, nb, L, name == "text_pooling", w, pooled)
+            sv.update(w=w)
+            return pooled
+        f32 = name == "text_pooling" or hb is None
+        w2, b2 = s.p(name + ".attention.2.weight").view(-1), s.p(name + ".attention.2.bias")
+        if f32:
+            t = ops.linear(h, self._w32(name + ".attention.0.weight"), s.p(name + ".attention.0.bias"), act=ACT_TANH)
+            ops.attn_pool_fwd_f32(t, w2, b2, h, mask32, nb, L, w, pooled)
+        else:
+            t = ops.linear(hb, s.w(name + ".attention.0.weight"), s.p(name + ".attention.0.bias"), act=ACT_TANH,
+                           out_bf16=True)
+            ops.attn_pool_fwd(t, w2, b2, hb, mask32, nb, L, w, pooled)
+        sv.update(t=t, w=w, h=h if f32 else hb, mask=mask32, f32=f32)
+        return pooled
 
     def _pool_bwd(self, name, sv, dpooled, dh, nb, L):
         s = self.s
@@ -635,87 +720,122 @@ class Engine:
             ops.weighted_pool_bwd(sv["w"], dpooled, nb, L, dh)
             return
         t = sv["t"]
-        dz = self._e(*t.shape, dtype=BF16)
         gw1 = s.g(name + ".attention.0.weight")
-        dz_lo = self._e(*t.shape, dtype=BF16) if gw1 is not None else None
         gw2 = s.g(name + ".attention.2.weight")
+        w2 = s.p(name + ".attention.2.weight").view(-1)
+        dw2 = None if gw2 is None else gw2.view(-1)
+        if sv["f32"]:
+            dz = self._e(*t.shape)
+            ops.attn_pool_bwd_f32(t, w2, sv["h"], sv["w"], dpooled, nb, L, dh, dz, dw2, s.g(name + ".attention.2.bias"),
+                                  db1=s.g(name + ".attention.0.bias"), mask=sv["mask"])
+            ops.linear_dx(dz, self._w32(name + ".attention.0.weight"), out=dh, beta=1.0)
+            self._dw32(dz, sv["h"], name + ".attention.0.weight")
+            return
+        dz = self._e(*t.shape, dtype=BF16)
+        dz_lo = self._e(*t.shape, dtype=BF16) if gw1 is not None else None
         # Σ_l dscore_l = 0 makes the scorer's first-Linear gradients small differences of large
         # terms: the bias gradient is summed in fp32 by the kernel, the weight gradient runs on
         # dz = hi + lo (two GEMM passes)
-        ops.attn_pool_bwd(t, s.p(name + ".attention.2.weight").view(-1), sv["hb"], sv["w"], dpooled, nb, L, dh, dz,
-                          None if gw2 is None else gw2.view(-1), s.g(name + ".attention.2.bias"),
+        ops.attn_pool_bwd(t, w2, sv["h"], sv["w"], dpooled, nb, L, dh, dz, dw2, s.g(name + ".attention.2.bias"),
                           db1=s.g(name + ".attention.0.bias"), dz_lo=dz_lo, mask=sv["mask"])
         ops.linear_dx(dz, s.w(name + ".attention.0.weight"), out=dh, beta=1.0)
-        self._dw(dz, sv["hb"], name + ".attention.0.weight")
+        self._dw(dz, sv["h"], name + ".attention.0.weight")
         if dz_lo is not None:
-            self._dw(dz_lo, sv["hb"], name + ".attention.0.weight")
+            self._dw(dz_lo, sv["h"], name + ".attention.0.weight")
+
+    def _xq_fwd(self, name, qin, kv, mask32, B, S, seeds, p_x):
+        """CrossModalAttention (ref:125-168) for len(seeds) query sets of B rows sharing the
+        keys/values kv (bf16 [B*S, 2P]), then the fusion input [qin | out_proj(att)] (fp32,
+        ref:670-677).  Returns (cat [rows, 2P], saved)."""
+        s = self.s
+        rows, P = qin.shape
+        nh = self.m.xattn_heads
+        q = ops.linear(qin, self._w32(name + ".query.weight"), s.p(name + ".query.bias"))
+        probs = self._e(rows * nh * S)
+        att = self._e(rows, P)
+        ops.xattn_fwd(q, kv[:, :P], kv[:, P:], mask32, B, S, nh, probs, att, seeds, drop_p=p_x)
+        cat = self._e(rows, 2 * P)
+        ops.linear(att, self._w32(name + ".out_proj.weight"), s.p(name + ".out_proj.bias"), out=cat[:, P:])
+        ops.copy2d(cat[:, :P], qin)
+        return cat, dict(qin=qin, q=q, probs=probs, att=att, cat=cat, kv=kv, mask=mask32, B=B, S=S, seeds=seeds, p=p_x)
+
+    def _xq_bwd(self, name, xs, dcat, d_qin, dkvb):
+        """Backward of _xq_fwd from d cat: d_qin (fp32) +=; dkvb (bf16 [B*S, 2P]) written, the
+        key/value bias gradient summed in fp32 by the kernel (over both query sets)."""
+        s = self.s
+        P = d_qin.shape[1]
+        datt = dcat[:, P:]
+        _add_(d_qin, dcat[:, :P])
+        dq_in = ops.linear_dx(datt, self._w32(name + ".out_proj.weight"))
+        self._dw32(datt, xs["att"], name + ".out_proj.weight")
+        self._db32(datt, name + ".out_proj.bias")
+        dq = self._e(*xs["q"].shape)
+        kv = xs["kv"]
+        ops.xattn_bwd(xs["q"], kv[:, :P], kv[:, P:], xs["probs"], dq_in, xs["B"], xs["S"], self.m.xattn_heads, dq,
+                      dkvb[:, :P], dkvb[:, P:], xs["seeds"], drop_p=xs["p"], colsum=s.fused(name + ".key.bias", 2, "g"),
+                      mask=xs["mask"])
+        ops.linear_dx(dq, self._w32(name + ".query.weight"), out=d_qin, beta=1.0)
+        self._dw32(dq, xs["qin"], name + ".query.weight")
+        self._db32(dq, name + ".query.bias")
+
+    def _kv_src_bwd(self, name, src, dkvb, seqb, xb, dx):
+        """K/V = Linear_kv(Linear_src(x)) backward (bf16, the shared side): dkvb [rows, 2P] ->
+        dx (fp32 +=); the src bias gradient summed in the K/V input-gradient GEMM's epilogue."""
+        s = self.s
+        dseqb = self._dx(dkvb, name + ".key.weight", 2, out_bf16=True, colsum=s.g(src + ".bias"))
+        self._dw(dkvb, seqb, name + ".key.weight", fused=2)
+        self._dx(dseqb, src + ".weight", out=dx, beta=1.0)
+        self._dw(dseqb, xb, src + ".weight")
+
+    def _fuse_fwd(self, name, cat):
+        """text_fusion / audio_fusion (ref:470-477, :672-677): LN(Linear(cat)) in fp32."""
+        y = ops.linear(cat, self._w32(name + ".0.weight"), self.s.p(name + ".0.bias"))
+        out = self._e(*y.shape)
+        st = self._ln(y, name + ".1", 1e-5, y=out)
+        return out, (y, st, cat)
+
+    def _fuse_bwd(self, name, d_out, saved):
+        y, st, cat = saved
+        dy = self._e(*d_out.shape)
+        self._ln_bwd(d_out, y, st, name + ".1", dx=dy, dsum=self.s.g(name + ".0.bias"))
+        dcat = ops.linear_dx(dy, self._w32(name + ".0.weight"))
+        self._dw32(dy, cat, name + ".0.weight")
+        return dcat
+
+    def _kv(self, name, src, xb):
+        """bf16 K|V [rows, 2P] = Linear_kv(Linear_src(xb)) and the bf16 Linear_src output."""
+        s = self.s
+        seqb = ops.linear(xb, s.w(src + ".weight"), s.p(src + ".bias"), out_bf16=True)
+        kv = ops.linear(seqb, s.fused(name + ".key.weight", 2, "w"), s.fused(name + ".key.bias", 2, "p"), out_bf16=True)
+        return kv, seqb
 
     def heads_forward(self, th, thb, ah, ahb, train, base_seed, ctx):
-        s = self.s
         m = self.m
         nb, L = ctx["t_nb"], ctx["t_L"]
         b = nb // 2
         ab, T = ctx["a_b"], ctx["a_T"]
-        P = m.projection_dim
         hs = {}
-        # pooling + projection
         tpool_sv, apool_sv, tproj_sv, aproj_sv = {}, {}, {}, {}
-        tpooled, tpooledb = self._pool_fwd("text_pooling", thb, ctx["t_mask32"], nb, L, tpool_sv)
-        apooled, apooledb = self._pool_fwd("audio_pooling", ahb, ctx["a_mask32"], ab, T, apool_sv)
-        tcat = self._e(nb, 2 * P, dtype=BF16)   # [tproj | t_att] bf16, fusion GEMM input
-        acat = self._e(b, 2 * P, dtype=BF16)
-        tproj = self._proj_fwd("text_projection", tpooledb, nb, train, _site_seed(base_seed, 201), tproj_sv)
-        aproj = self._proj_fwd("audio_projection", apooledb, ab, train, _site_seed(base_seed, 202), aproj_sv)
-        tprojb =ops.cast_bf16(tproj, self._e(nb, P, dtype=BF16))
-        aprojb = ops.cast_bf16(aproj, self._e(ab, P, dtype=BF16))
-        hs.update(tpool=tpool_sv, apool=apool_sv, tproj=tproj_sv, aproj=aproj_sv, tprojb=tprojb, aprojb=aprojb)
+        tpooled = self._pool_fwd("text_pooling", th, thb, ctx["t_mask32"], nb, L, tpool_sv)
+        apooled = self._pool_fwd("audio_pooling", ah, ahb, ctx["a_mask32"], ab, T, apool_sv)
+        tproj = self._proj_fwd("text_projection", tpooled, nb, train, _site_seed(base_seed, 201), tproj_sv)
+        aproj = self._proj_fwd("audio_projection", apooled, ab, train, _site_seed(base_seed, 202), aproj_sv)
+        hs.update(tpool=tpool_sv, apool=apool_sv, tproj=tproj_sv, aproj=aproj_sv)
         if m.use_cross_modal:
             p_x = m.dropout if train else 0.0
-            # audio_seq_to_projection (identical for the pos and neg calls of ref:525-542: computed once)
-            aseqb = ops.linear(ahb, s.w("audio_seq_to_projection.weight"), s.p("audio_seq_to_projection.bias"),
-                               out_bf16=True)
-            # text->audio: K/V over the audio sequence shared by pos and neg queries
-            kva = ops.linear(aseqb, s.fused("text_to_audio_attention.key.weight", 2, "w"),
-                             s.fused("text_to_audio_attention.key.bias", 2, "p"), out_bf16=True)
-            qt = ops.linear(tprojb, s.w("text_to_audio_attention.query.weight"),
-                            s.p("text_to_audio_attention.query.bias"))
-            nh = m.xattn_heads
-            probs_t = self._e(nb * nh * T)
-            att_t = self._e(nb, P)
+            # audio_seq_to_projection + text->audio K/V: identical for the pos and neg calls of
+            # ref:525-542, computed once; pos and neg queries in one launch (each its own seed)
+            kva, aseqb = self._kv("text_to_audio_attention", "audio_seq_to_projection", ahb)
             seed_t = _site_seed(base_seed, 203)
-            # pos rows, neg rows: one launch over the shared audio keys (each half keeps its own seed)
-            ops.xattn_fwd(qt, kva[:, :P], kva[:, P:], ctx["a_mask32"], b, T, nh, probs_t, att_t,
-                          (_site_seed(seed_t, 0), _site_seed(seed_t, 1)), drop_p=p_x)
-            att_tb = ops.cast_bf16(att_t, self._e(nb, P, dtype=BF16))
-            ops.linear(att_tb, s.w("text_to_audio_attention.out_proj.weight"),
-                       s.p("text_to_audio_attention.out_proj.bias"), out=tcat[:, P:])
-            _copy_bf16(tprojb, tcat[:, :P])
+            tcat, hs["tx"] = self._xq_fwd("text_to_audio_attention", tproj, kva, ctx["a_mask32"], b, T,
+                                          (_site_seed(seed_t, 0), _site_seed(seed_t, 1)), p_x)
             # audio->text (pos call only: the neg call's audio output is discarded, ref:535)
-            tseqb = ops.linear(thb[: b * L], s.w("text_seq_to_projection.weight"), s.p("text_seq_to_projection.bias"),
-                               out_bf16=True)
-            kvt = ops.linear(tseqb, s.fused("audio_to_text_attention.key.weight", 2, "w"),
-                             s.fused("audio_to_text_attention.key.bias", 2, "p"), out_bf16=True)
-            qa = ops.linear(aprojb, s.w("audio_to_text_attention.query.weight"),
-                            s.p("audio_to_text_attention.query.bias"))
-            probs_a = self._e(b * nh * L)
-            att_a = self._e(b, P)
-            seed_a = _site_seed(base_seed, 204)
-            ops.xattn1_fwd(qa, kvt[:, :P], kvt[:, P:], ctx["t_mask32"][: b * L], b, L, nh, probs_a, att_a,
-                           drop_p=p_x, seed=seed_a)
-            att_ab = ops.cast_bf16(att_a, self._e(b, P, dtype=BF16))
-            ops.linear(att_ab, s.w("audio_to_text_attention.out_proj.weight"),
-                       s.p("audio_to_text_attention.out_proj.bias"), out_bf16=True, out=acat[:, P:])
-            _copy_bf16(aprojb, acat[:, :P])
-            # fusion Linear + LN
-            yt = ops.linear(tcat, s.w("text_fusion.0.weight"), s.p("text_fusion.0.bias"))
-            tfused = self._e(nb, P)
-            st_t = self._ln(yt, "text_fusion.1", 1e-5, y=tfused)
-            ya = ops.linear(acat, s.w("audio_fusion.0.weight"), s.p("audio_fusion.0.bias"))
-            afused = self._e(b, P)
-            st_a = self._ln(ya, "audio_fusion.1", 1e-5, y=afused)
-            hs.update(aseqb=aseqb, kva=kva, qt=qt, probs_t=probs_t, att_tb=att_tb, seed_t=seed_t, p_x=p_x,
-                      tseqb=tseqb, kvt=kvt, qa=qa, probs_a=probs_a, att_ab=att_ab, seed_a=seed_a, tcat=tcat,
-                      acat=acat, yt=yt, st_t=st_t, ya=ya, st_a=st_a)
+            kvt, tseqb = self._kv("audio_to_text_attention", "text_seq_to_projection", thb[: b * L])
+            acat, hs["ax"] = self._xq_fwd("audio_to_text_attention", aproj[:b], kvt, ctx["t_mask32"][: b * L], b, L,
+                                          (_site_seed(base_seed, 204),), p_x)
+            tfused, hs["tf"] = self._fuse_fwd("text_fusion", tcat)
+            afused, hs["af"] = self._fuse_fwd("audio_fusion", acat)
+            hs.update(aseqb=aseqb, tseqb=tseqb)
         else:
             tfused, afused = tproj, aproj[:b]
         align = None
@@ -725,7 +845,6 @@ class Engine:
         return tfused, afused, align
 
     def heads_backward(self, d_tfused, d_afused, d_align, ctx, dth, dah):
-        s = self.s
         m = self.m
         hs = ctx["heads"]
         nb, L = ctx["t_nb"], ctx["t_L"]
@@ -737,74 +856,27 @@ class Engine:
         if d_align is not None and m.use_word_alignment:
             self._align_bwd(d_align, hs, ctx, dth, dah)
         if m.use_cross_modal:
-            # fusion LNs + Linears
-            dyt = self._e(nb, P, dtype=BF16)
-            self._ln_bwd(d_tfused, hs["yt"], hs["st_t"], "text_fusion.1", dxb=dyt, dsum=s.g("text_fusion.0.bias"))
-            dtcat = ops.linear_dx(dyt, s.w("text_fusion.0.weight"))
-            self._dw(dyt, hs["tcat"], "text_fusion.0.weight")
-            dya = self._e(b, P, dtype=BF16)
-            self._ln_bwd(d_afused, hs["ya"], hs["st_a"], "audio_fusion.1", dxb=dya, dsum=s.g("audio_fusion.0.bias"))
-            dacat = ops.linear_dx(dya, s.w("audio_fusion.0.weight"))
-            self._dw(dya, hs["acat"], "audio_fusion.0.weight")
-            _add_(d_tproj, dtcat[:, :P])
-            _add_(d_aproj[:b], dacat[:, :P])
-            nh = m.xattn_heads
-            # ---- text->audio attention (pos + neg queries, shared audio K/V)
-            datt = dtcat[:, P:].contiguous()
-            dattb = ops.cast_bf16(datt, self._e(nb, P, dtype=BF16))
-            dq_in = ops.linear_dx(dattb, s.w("text_to_audio_attention.out_proj.weight"))
-            self._dw(dattb, hs["att_tb"], "text_to_audio_attention.out_proj.weight")
-            self._db(datt, "text_to_audio_attention.out_proj.bias")
-            dqt = self._e(nb, P)
-            # dK/dV come out of the kernel in bf16 with their fp32 column sums (the fused key/value
-            # bias gradient); the K/V input gradient leaves its GEMM in bf16 with the
-            # audio_seq_to_projection bias gradient summed in the epilogue: no fp32 [ab*T, 2P]
-            # zero-fill / accumulate / cast / column-sum passes
+            dtcat = self._fuse_bwd("text_fusion", d_tfused, hs["tf"])
+            dacat = self._fuse_bwd("audio_fusion", d_afused, hs["af"])
+            # text->audio: dK/dV leave the kernel in bf16 with their fp32 column sums (the fused
+            # key/value bias gradient); the K/V input gradient leaves its GEMM in bf16 with the
+            # audio_seq_to_projection bias gradient summed in the epilogue
             dkvb = self._e(ab * T, 2 * P, dtype=BF16)
-            ops.xattn_bwd(hs["qt"], hs["kva"][:, :P], hs["kva"][:, P:], hs["probs_t"], dq_in, b, T, nh, dqt,
-                          dkvb[:, :P], dkvb[:, P:], (_site_seed(hs["seed_t"], 0), _site_seed(hs["seed_t"], 1)),
-                          drop_p=hs["p_x"], colsum=s.fused("text_to_audio_attention.key.bias", 2, "g"),
-                          mask=ctx["a_mask32"])
-            dqtb = ops.cast_bf16(dqt, self._e(nb, P, dtype=BF16))
-            ops.linear_dx(dqtb, s.w("text_to_audio_attention.query.weight"), out=d_tproj, beta=1.0)
-            self._dw(dqtb, hs["tprojb"], "text_to_audio_attention.query.weight")
-            self._db(dqt, "text_to_audio_attention.query.bias")
-            daseqb = self._dx(dkvb, "text_to_audio_attention.key.weight", 2, out_bf16=True,
-                              colsum=s.g("audio_seq_to_projection.bias"))
-            self._dw(dkvb, hs["aseqb"], "text_to_audio_attention.key.weight", fused=2)
+            self._xq_bwd("text_to_audio_attention", hs["tx"], dtcat, d_tproj, dkvb)
+            self._kv_src_bwd("text_to_audio_attention", "audio_seq_to_projection", dkvb, hs["aseqb"], ctx["_ahb"],
+                             dah)
             del dkvb
-            self._dx(daseqb, "audio_seq_to_projection.weight", out=dah, beta=1.0)
-            self._dw(daseqb, ctx["_ahb"], "audio_seq_to_projection.weight")
-            del daseqb
-            # ---- audio->text attention (pos call)
-            datta = dacat[:, P:].contiguous()
-            dattab = ops.cast_bf16(datta, self._e(b, P, dtype=BF16))
-            dqa_in = ops.linear_dx(dattab, s.w("audio_to_text_attention.out_proj.weight"))
-            self._dw(dattab, hs["att_ab"], "audio_to_text_attention.out_proj.weight")
-            self._db(datta, "audio_to_text_attention.out_proj.bias")
-            dqa = self._e(b, P)
             dkvtb = self._e(b * L, 2 * P, dtype=BF16)
-            ops.xattn1_bwd(hs["qa"], hs["kvt"][:, :P], hs["kvt"][:, P:], hs["probs_a"], dqa_in, b, L, nh, dqa,
-                           dkvtb[:, :P], dkvtb[:, P:], drop_p=hs["p_x"], seed=hs["seed_a"],
-                           colsum=s.fused("audio_to_text_attention.key.bias", 2, "g"), mask=ctx["t_mask32"][: b * L])
-            dqab = ops.cast_bf16(dqa, self._e(b, P, dtype=BF16))
-            ops.linear_dx(dqab, s.w("audio_to_text_attention.query.weight"), out=d_aproj[:b], beta=1.0)
-            self._dw(dqab, hs["aprojb"], "audio_to_text_attention.query.weight")
-            self._db(dqa, "audio_to_text_attention.query.bias")
-            dtseqb = ops.linear_dx(dkvtb, s.fused("audio_to_text_attention.key.weight", 2, "w"), out_bf16=True,
-                                   colsum=s.g("text_seq_to_projection.bias"))
-            self._dw(dkvtb, hs["tseqb"], "audio_to_text_attention.key.weight", fused=2)
-            ops.linear_dx(dtseqb, s.w("text_seq_to_projection.weight"), out=dth[: b * L], beta=1.0)
-            self._dw(dtseqb, ctx["_thb"][: b * L], "text_seq_to_projection.weight")
+            self._xq_bwd("audio_to_text_attention", hs["ax"], dacat, d_aproj[:b], dkvtb)
+            self._kv_src_bwd("audio_to_text_attention", "text_seq_to_projection", dkvtb, hs["tseqb"],
+                             ctx["_thb"][: b * L], dth[: b * L])
         else:
             _add_(d_tproj, d_tfused)
             _add_(d_aproj[:b], d_afused)
-        # projections
         dtpooled = self._z(nb, self.tcfg.hidden_size)
         dapooled = self._z(ab, self.acfg.hidden_size)
         self._proj_bwd("text_projection", hs["tproj"], d_tproj, dtpooled)
         self._proj_bwd("audio_projection", hs["aproj"], d_aproj, dapooled)
-        # pooling
         self._pool_bwd("text_pooling", hs["tpool"], dtpooled, dth, nb, L)
         self._pool_bwd("audio_pooling", hs["apool"], dapooled, dah, ab, T)
 
@@ -818,18 +890,14 @@ class Engine:
         """apply_cross_modal_attention (ref:643-682) for one call: text [b,P] + hidden [b,L,Ht],
         audio [b,P] + hidden [b,T,Ha] -> (text_fused, audio_fused) [b,P] fp32 and the saved
         context.  The fused training step shares one audio K/V between the pos and neg calls
-        (heads_forward); this is the reference's per-call form behind the public method."""
-        s = self.s
+        (heads_forward); this is the reference's per-call form behind the public method, on the
+        same helpers."""
         m = self.m
         b, L, Ht = th.shape
         T, Ha = ah.shape[1], ah.shape[2]
-        P = m.projection_dim
-        nh = m.xattn_heads
         p_x = m.dropout if train else 0.0
         thb = ops.cast_bf16(th.contiguous(), self._e(b * L, Ht, dtype=BF16))
         ahb = ops.cast_bf16(ah.contiguous(), self._e(b * T, Ha, dtype=BF16))
-        tprojb = ops.cast_bf16(tproj.contiguous(), self._e(b, P, dtype=BF16))
-        aprojb = ops.cast_bf16(aproj.contiguous(), self._e(b, P, dtype=BF16))
         tm32 = self._mask32(tmask, b * L) if tmask is not None else None
         if amask is not None and self.raw_audio and amask.shape[-1] != T:
             # a sample-level wav2vec2 mask [b, N]: the frame mask of the conv stack
@@ -837,111 +905,33 @@ class Engine:
             am32 = frame_mask(self.acfg, amask, b, amask.shape[-1], T, self.s.device)[1]
         else:
             am32 = self._mask32(amask, b * T) if amask is not None else None
-        # text -> audio
-        aseqb = ops.linear(ahb, s.w("audio_seq_to_projection.weight"), s.p("audio_seq_to_projection.bias"),
-                           out_bf16=True)
-        kva = ops.linear(aseqb, s.fused("text_to_audio_attention.key.weight", 2, "w"),
-                         s.fused("text_to_audio_attention.key.bias", 2, "p"), out_bf16=True)
-        qt = ops.linear(tprojb, s.w("text_to_audio_attention.query.weight"), s.p("text_to_audio_attention.query.bias"))
-        probs_t, att_t = self._e(b * nh * T), self._e(b, P)
-        seed_t, seed_a = _site_seed(seed, 1), _site_seed(seed, 2)
-        ops.xattn1_fwd(qt, kva[:, :P], kva[:, P:], am32, b, T, nh, probs_t, att_t, drop_p=p_x, seed=seed_t)
-        att_tb = ops.cast_bf16(att_t, self._e(b, P, dtype=BF16))
-        tcat = self._e(b, 2 * P, dtype=BF16)
-        ops.linear(att_tb, s.w("text_to_audio_attention.out_proj.weight"), s.p("text_to_audio_attention.out_proj.bias"),
-                   out=tcat[:, P:])
-        _copy_bf16(tprojb, tcat[:, :P])
-        # audio -> text
-        tseqb = ops.linear(thb, s.w("text_seq_to_projection.weight"), s.p("text_seq_to_projection.bias"),
-                           out_bf16=True)
-        kvt = ops.linear(tseqb, s.fused("audio_to_text_attention.key.weight", 2, "w"),
-                         s.fused("audio_to_text_attention.key.bias", 2, "p"), out_bf16=True)
-        qa = ops.linear(aprojb, s.w("audio_to_text_attention.query.weight"), s.p("audio_to_text_attention.query.bias"))
-        probs_a, att_a = self._e(b * nh * L), self._e(b, P)
-        ops.xattn1_fwd(qa, kvt[:, :P], kvt[:, P:], tm32, b, L, nh, probs_a, att_a, drop_p=p_x, seed=seed_a)
-        att_ab = ops.cast_bf16(att_a, self._e(b, P, dtype=BF16))
-        acat = self._e(b, 2 * P, dtype=BF16)
-        ops.linear(att_ab, s.w("audio_to_text_attention.out_proj.weight"), s.p("audio_to_text_attention.out_proj.bias"),
-                   out=acat[:, P:])
-        _copy_bf16(aprojb, acat[:, :P])
-        # fusion Linear + LN
-        yt = ops.linear(tcat, s.w("text_fusion.0.weight"), s.p("text_fusion.0.bias"))
-        tfused = self._e(b, P)
-        st_t = self._ln(yt, "text_fusion.1", 1e-5, y=tfused)
-        ya = ops.linear(acat, s.w("audio_fusion.0.weight"), s.p("audio_fusion.0.bias"))
-        afused = self._e(b, P)
-        st_a = self._ln(ya, "audio_fusion.1", 1e-5, y=afused)
-        sv = dict(b=b, L=L, T=T, thb=thb, ahb=ahb, tprojb=tprojb, aprojb=aprojb, aseqb=aseqb, kva=kva, qt=qt,
-                  probs_t=probs_t, att_tb=att_tb, seed_t=seed_t, tseqb=tseqb, kvt=kvt, qa=qa, probs_a=probs_a,
-                  att_ab=att_ab, seed_a=seed_a, p_x=p_x, tcat=tcat, acat=acat, yt=yt, st_t=st_t, ya=ya, st_a=st_a,
-                  am32=am32, tm32=tm32)
+        kva, aseqb = self._kv("text_to_audio_attention", "audio_seq_to_projection", ahb)
+        tcat, tx = self._xq_fwd("text_to_audio_attention", tproj.float().contiguous(), kva, am32, b, T,
+                                (_site_seed(seed, 1),), p_x)
+        kvt, tseqb = self._kv("audio_to_text_attention", "text_seq_to_projection", thb)
+        acat, ax = self._xq_fwd("audio_to_text_attention", aproj.float().contiguous(), kvt, tm32, b, L,
+                                (_site_seed(seed, 2),), p_x)
+        tfused, tf = self._fuse_fwd("text_fusion", tcat)
+        afused, af = self._fuse_fwd("audio_fusion", acat)
+        sv = dict(b=b, L=L, T=T, thb=thb, ahb=ahb, aseqb=aseqb, tseqb=tseqb, tx=tx, ax=ax, tf=tf, af=af)
         return tfused, afused, sv
 
     def cross_backward(self, sv, d_tf, d_af):
         """-> (d text_projected [b,P], d text_hidden [b*L,Ht], d audio_projected [b,P],
-        d audio_hidden [b*T,Ha]) fp32; parameter gradients += into the flat buffer."""
-        s = self.s
-        m = self.m
+        d audio_hidden [b*T,Ha]) fp32; parameter gradients += into the flat gradient buffer."""
         b, L, T = sv["b"], sv["L"], sv["T"]
-        P = m.projection_dim
-        nh = m.xattn_heads
+        P = self.m.projection_dim
         Ht, Ha = sv["thb"].shape[1], sv["ahb"].shape[1]
         d_tproj, d_aproj = self._z(b, P), self._z(b, P)
         dth, dah = self._z(b * L, Ht), self._z(b * T, Ha)
-        dyt = self._e(b, P, dtype=BF16)
-        self._ln_bwd(d_tf.contiguous(), sv["yt"], sv["st_t"], "text_fusion.1", dxb=dyt, dsum=s.g("text_fusion.0.bias"))
-        dtcat = ops.linear_dx(dyt, s.w("text_fusion.0.weight"))
-        self._dw(dyt, sv["tcat"], "text_fusion.0.weight")
-        dya = self._e(b, P, dtype=BF16)
-        self._ln_bwd(d_af.contiguous(), sv["ya"], sv["st_a"], "audio_fusion.1", dxb=dya, dsum=s.g("audio_fusion.0.bias"))
-        dacat = ops.linear_dx(dya, s.w("audio_fusion.0.weight"))
-        self._dw(dya, sv["acat"], "audio_fusion.0.weight")
-        _add_(d_tproj, dtcat[:, :P])
-        _add_(d_aproj, dacat[:, :P])
-        # text -> audio
-        datt = dtcat[:, P:].contiguous()
-        dattb = ops.cast_bf16(datt, self._e(b, P, dtype=BF16))
-        dq_in = ops.linear_dx(dattb, s.w("text_to_audio_attention.out_proj.weight"))
-        self._dw(dattb, sv["att_tb"], "text_to_audio_attention.out_proj.weight")
-        self._db(datt, "text_to_audio_attention.out_proj.bias")
-        dqt = self._e(b, P)
-        dkv = self._z(b * T, 2 * P)
-        ops.xattn1_bwd(sv["qt"], sv["kva"][:, :P], sv["kva"][:, P:], sv["probs_t"], dq_in, b, T, nh, dqt, dkv[:, :P],
-                       dkv[:, P:], drop_p=sv["p_x"], seed=sv["seed_t"], mask=sv["am32"])
-        dqtb = ops.cast_bf16(dqt, self._e(b, P, dtype=BF16))
-        ops.linear_dx(dqtb, s.w("text_to_audio_attention.query.weight"), out=d_tproj, beta=1.0)
-        self._dw(dqtb, sv["tprojb"], "text_to_audio_attention.query.weight")
-        self._db(dqt, "text_to_audio_attention.query.bias")
-        dkvb = ops.cast_bf16(dkv, self._e(b * T, 2 * P, dtype=BF16))
-        daseq = self._dx(dkvb, "text_to_audio_attention.key.weight", 2)
-        self._dw(dkvb, sv["aseqb"], "text_to_audio_attention.key.weight", fused=2)
-        self._db(dkv, "text_to_audio_attention.key.bias", fused=2)
-        daseqb = ops.cast_bf16(daseq, self._e(b * T, P, dtype=BF16))
-        self._dx(daseqb, "audio_seq_to_projection.weight", out=dah, beta=1.0)
-        self._dw(daseqb, sv["ahb"], "audio_seq_to_projection.weight")
-        self._db(daseq, "audio_seq_to_projection.bias")
-        # audio -> text
-        datta = dacat[:, P:].contiguous()
-        dattab = ops.cast_bf16(datta, self._e(b, P, dtype=BF16))
-        dqa_in = ops.linear_dx(dattab, s.w("audio_to_text_attention.out_proj.weight"))
-        self._dw(dattab, sv["att_ab"], "audio_to_text_attention.out_proj.weight")
-        self._db(datta, "audio_to_text_attention.out_proj.bias")
-        dqa = self._e(b, P)
-        dkvt = self._z(b * L, 2 * P)
-        ops.xattn1_bwd(sv["qa"], sv["kvt"][:, :P], sv["kvt"][:, P:], sv["probs_a"], dqa_in, b, L, nh, dqa,
-                       dkvt[:, :P], dkvt[:, P:], drop_p=sv["p_x"], seed=sv["seed_a"], mask=sv["tm32"])
-        dqab = ops.cast_bf16(dqa, self._e(b, P, dtype=BF16))
-        ops.linear_dx(dqab, s.w("audio_to_text_attention.query.weight"), out=d_aproj, beta=1.0)
-        self._dw(dqab, sv["aprojb"], "audio_to_text_attention.query.weight")
-        self._db(dqa, "audio_to_text_attention.query.bias")
-        dkvtb = ops.cast_bf16(dkvt, self._e(b * L, 2 * P, dtype=BF16))
-        dtseq = ops.linear_dx(dkvtb, s.fused("audio_to_text_attention.key.weight", 2, "w"))
-        self._dw(dkvtb, sv["tseqb"], "audio_to_text_attention.key.weight", fused=2)
-        self._db(dkvt, "audio_to_text_attention.key.bias", fused=2)
-        dtseqb = ops.cast_bf16(dtseq, self._e(b * L, P, dtype=BF16))
-        ops.linear_dx(dtseqb, s.w("text_seq_to_projection.weight"), out=dth, beta=1.0)
-        self._dw(dtseqb, sv["thb"], "text_seq_to_projection.weight")
-        self._db(dtseq, "text_seq_to_projection.bias")
+        dtcat = self._fuse_bwd("text_fusion", d_tf.float().contiguous(), sv["tf"])
+        dacat = self._fuse_bwd("audio_fusion", d_af.float().contiguous(), sv["af"])
+        dkvb = self._e(b * T, 2 * P, dtype=BF16)
+        self._xq_bwd("text_to_audio_attention", sv["tx"], dtcat, d_tproj, dkvb)
+        self._kv_src_bwd("text_to_audio_attention", "audio_seq_to_projection", dkvb, sv["aseqb"], sv["ahb"], dah)
+        dkvtb = self._e(b * L, 2 * P, dtype=BF16)
+        self._xq_bwd("audio_to_text_attention", sv["ax"], dacat, d_aproj, dkvtb)
+        self._kv_src_bwd("audio_to_text_attention", "text_seq_to_projection", dkvtb, sv["tseqb"], sv["thb"], dth)
         return d_tproj, dth, d_aproj, dah
 
     # ------------------------------------------------------- word alignment
@@ -1019,11 +1009,6 @@ class Engine:
             if stage_done:
                 stage_done("text")
         ctx.clear()
-
-
-def _copy_bf16(src, dst):
-    """dst[:] = src (strided 2-D views) on the ste_copy2d kernel."""
-    ops.copy2d(dst, src)
 
 
 def _copy_f32(src, dst):

@@ -270,8 +270,8 @@ class EnhancedAudioTextModel(nn.Module):
             h, hb = e.audio_forward(x, mask, self.training, _call_seed(self.training), ctx, save=False)
             B, L = ctx["a_b"], ctx["a_T"]
             m32, pool, proj = ctx["a_mask32"], "audio_pooling", "audio_projection"
-        _, pb = e._pool_fwd(pool, hb, m32, B, L, {})
-        out = e._proj_fwd(proj, pb, B, self.training, _call_seed(self.training), {})
+        pooled = e._pool_fwd(pool, h, hb, m32, B, L, {})
+        out = e._proj_fwd(proj, pooled, B, self.training, _call_seed(self.training), {})
         return out, h.view(B, L, -1)
 
 
@@ -300,8 +300,8 @@ class _EncodeFn(torch.autograd.Function):
             B, L = ctx["a_b"], ctx["a_T"]
             m32, pool, proj = ctx["a_mask32"], "audio_pooling", "audio_projection"
         sv_pool, sv_proj = {}, {}
-        _, pb = e._pool_fwd(pool, hb, m32, B, L, sv_pool)
-        out = e._proj_fwd(proj, pb, B, train, _site(seed), sv_proj)
+        pooled = e._pool_fwd(pool, h, hb, m32, B, L, sv_pool)
+        out = e._proj_fwd(proj, pooled, B, train, _site(seed), sv_proj)
         fctx.model, fctx.kind, fctx.ctx = model, kind, ctx
         fctx.saved = (sv_pool, sv_proj, B, L, h.shape[-1], pool, proj)
         return out, h.view(B, L, -1)

@@ -89,8 +89,8 @@ class EnhancedAudioTextModel(nn.Module):
             attention_mask = torch.ones_like(input_ids)
         B, L = input_ids.shape
         h, hb = e.text_forward(input_ids.contiguous(), attention_mask.contiguous(), False, 0, ctx, save=False)
-        _, pb = e._pool_fwd("text_pooling", hb, ctx["t_mask32"], B, L, {})
-        return e._proj_fwd("text_projection", pb, B, False, 0, {}), h, hb, ctx["t_mask32"]
+        pooled = e._pool_fwd("text_pooling", h, hb, ctx["t_mask32"], B, L, {})
+        return e._proj_fwd("text_projection", pooled, B, False, 0, {}), h, hb, ctx["t_mask32"]
 
     def _audio(self, input_features, attention_mask):
         e, ctx = self.engine, {}
@@ -98,8 +98,8 @@ class EnhancedAudioTextModel(nn.Module):
         if attention_mask is None:
             attention_mask = torch.ones(B, T, dtype=torch.int64, device=input_features.device)
         h, hb = e.audio_forward(input_features.contiguous(), attention_mask.contiguous(), False, 0, ctx, save=False)
-        _, pb = e._pool_fwd("audio_pooling", hb, ctx["a_mask32"], B, T, {})
-        return e._proj_fwd("audio_projection", pb, B, False, 0, {}), h, hb, ctx["a_mask32"]
+        pooled = e._pool_fwd("audio_pooling", h, hb, ctx["a_mask32"], B, T, {})
+        return e._proj_fwd("audio_projection", pooled, B, False, 0, {}), h, hb, ctx["a_mask32"]
 
     def _attend(self, name, q_proj, kv_hb, mask32, B, S):
         """CrossModalAttention(q = q_proj as one token, k = v-source = kv_hb) (model.py:79-117)."""
@@ -107,23 +107,18 @@ class EnhancedAudioTextModel(nn.Module):
         P = self.projection_dim
         kv = ops.linear(kv_hb, s.fused(name + ".key.weight", 2, "w"), s.fused(name + ".key.bias", 2, "p"),
                         out_bf16=True)
-        qb = ops.cast_bf16(q_proj.contiguous(), e._e(B, P, dtype=BF16))
-        q = ops.linear(qb, s.w(name + ".query.weight"), s.p(name + ".query.bias"))
+        q = ops.linear(q_proj.float().contiguous(), e._w32(name + ".query.weight"), s.p(name + ".query.bias"))
         att = e._e(B, P)
         ops.xattn1_fwd(q, kv[:, :P], kv[:, P:], mask32, B, S, self.xattn_heads, e._e(B * self.xattn_heads * S), att)
-        attb = ops.cast_bf16(att, e._e(B, P, dtype=BF16))
-        return ops.linear(attb, s.w(name + ".out_proj.weight"), s.p(name + ".out_proj.bias"))
+        return ops.linear(att, e._w32(name + ".out_proj.weight"), s.p(name + ".out_proj.bias"))
 
     def _fuse(self, name, proj, att):
-        s, e = self.store, self.engine
+        e = self.engine
         B, P = proj.shape
-        cat = e._e(B, 2 * P, dtype=BF16)
-        ops.copy2d(cat[:, :P], ops.cast_bf16(proj.contiguous(), e._e(B, P, dtype=BF16)))
-        ops.copy2d(cat[:, P:], ops.cast_bf16(att.contiguous(), e._e(B, P, dtype=BF16)))
-        y = ops.linear(cat, s.w(name + ".0.weight"), s.p(name + ".0.bias"))
-        out = e._e(B, P)
-        e._ln(y, name + ".1", 1e-5, y=out)
-        return out
+        cat = e._e(B, 2 * P)
+        ops.copy2d(cat[:, :P], proj.float().contiguous())
+        ops.copy2d(cat[:, P:], att.float().contiguous())
+        return e._fuse_fwd(name, cat)[0]
 
     # ------------------------------------------------------------ reference API
     @torch.no_grad()

@@ -31,15 +31,21 @@ def _ld(t: torch.Tensor) -> int:
 def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf16=False, bias=None,
          act=_lib.ACT_NONE, pre_out=None, z=None, residual=None, alpha=1.0, beta=0.0, colsum=None,
          row_scale=None, drop_p=0.0, seed=0, out_bf16_copy=None, batch=1, stride_a=0, stride_b=0, stride_c=0,
-         stride_r=0, drop_ld=0, ws=None, mx8=None):
+         stride_r=0, drop_ld=0, ws=None, mx8=None, copy_lo=False):
     """out[M,N] = epilogue(alpha * A·B).  See include/ste.h for the epilogue order.
 
     a_kc: A is [M,K] row-major (else [K,M]);  b_kc: B is [N,K] row-major (else [K,N]).
+    bf16 operands run on ste_gemm; fp32 operands (pre_out / z fp32 too) on ste_gemm_f32, the
+    exact-f32 matrix-core GEMM of the heads.
     """
+    f32 = mx8 is None and a.dtype == F32
     if mx8 is not None:  # (a_scales, b_scales): e4m3 operands with E8M0 block scales (ste_gemm_mx8)
         assert a.dtype == torch.uint8 and b.dtype == torch.uint8 and a_kc and b_kc, "MX-fp8 GEMM operands"
+    elif f32:
+        assert b.dtype == F32 and batch == 1, "ste_gemm_f32: fp32 operands, batch 1"
+        assert (pre_out is None or pre_out.dtype == F32) and (z is None or z.dtype == F32)
     else:
-        assert a.dtype == BF16 and b.dtype == BF16, "GEMM operands are bf16"
+        assert a.dtype == BF16 and b.dtype == BF16, "GEMM operands are bf16 (or both fp32)"
     if M is None:
         M = a.shape[-2] if a_kc else a.shape[-1]
     if K is None:
@@ -61,8 +67,8 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
         args.ldc, args.c_bf16 = N, int(out_bf16)
     if pre_out is not None:
         args.C2, args.ldc2 = ptr(pre_out), _ld(pre_out)
-    if out_bf16_copy is not None:
-        args.C3, args.ldc3 = ptr(out_bf16_copy), _ld(out_bf16_copy)
+    if out_bf16_copy is not None:   # copy_lo: it receives bf16(v - bf16(v)) (a [hi | lo] split output)
+        args.C3, args.ldc3, args.c3_lo = ptr(out_bf16_copy), _ld(out_bf16_copy), int(bool(copy_lo))
     if bias is not None:
         assert bias.dtype == F32 and bias.is_contiguous()
         args.bias = ptr(bias)
@@ -88,6 +94,10 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
         def launch():
             call("ste_gemm_mx8", C.byref(args), ptr(mx8[0]), ptr(mx8[1]), ptr(q8[0]), ptr(q8[1]), _s())
         name = "gemm_mx8_kernel"
+    elif f32:
+        def launch():
+            call("ste_gemm_f32", C.byref(args), _s())
+        name = "gemm_f32_kernel"
     else:
         def launch():
             call("ste_gemm", C.byref(args), _s())
@@ -169,7 +179,7 @@ def linear_dw(dy, x, **kw):
 
 # -------------------------------------------------------------- LayerNorm
 def _ln_fwd_struct(x, gamma, beta, eps, y=None, yb=None, mean=None, rstd=None, row_scale=None, act=_lib.ACT_NONE,
-                   drop_p=0.0, seed=0, q8=None, rows=None, cols=None):
+                   drop_p=0.0, seed=0, q8=None, rows=None, cols=None, ylo=None):
     """-> (LnFwdArgs, mean, rstd, algorithmic bytes).  x may be None (pair kernels: the second
     LN's input is the first one's output in registers); then rows/cols are given."""
     if x is not None:
@@ -188,6 +198,9 @@ def _ln_fwd_struct(x, gamma, beta, eps, y=None, yb=None, mean=None, rstd=None, r
         a.y, a.ldy = ptr(y), _ld(y)
     if yb is not None:
         a.yb, a.ldyb = ptr(yb), _ld(yb)
+    if ylo is not None:   # the low half bf16(y - bf16(y)): with yb, a [hi | lo] split image
+        assert yb is not None
+        a.ylo, a.ldylo = ptr(ylo), _ld(ylo)
     a.mean, a.rstd = ptr(mean), ptr(rstd)
     a.row_scale = ptr(row_scale)
     a.act, a.drop_p, a.seed = int(act), float(drop_p), int(seed) & (2**64 - 1)
@@ -195,13 +208,15 @@ def _ln_fwd_struct(x, gamma, beta, eps, y=None, yb=None, mean=None, rstd=None, r
         a.q8, a.q8s, a.ldq8 = ptr(q8[0]), ptr(q8[1]), _ld(q8[0])
     # algorithmic bytes: read x, write every requested output, 8 B/row of statistics
     nbytes = rows * cols * ((x.element_size() if x is not None else 0) + (4 if y is not None else 0) +
-                            (2 if yb is not None else 0) + (1 + 1 / 32 if q8 is not None else 0)) + 8 * rows + 8 * cols
+                            (2 if yb is not None else 0) + (2 if ylo is not None else 0) +
+                            (1 + 1 / 32 if q8 is not None else 0)) + 8 * rows + 8 * cols
     return a, mean, rstd, nbytes
 
 
 def layernorm_fwd(x, gamma, beta, eps, *, y=None, yb=None, mean=None, rstd=None, row_scale=None,
-                  act=_lib.ACT_NONE, drop_p=0.0, seed=0, q8=None):
-    a, mean, rstd, nbytes = _ln_fwd_struct(x, gamma, beta, eps, y, yb, mean, rstd, row_scale, act, drop_p, seed, q8)
+                  act=_lib.ACT_NONE, drop_p=0.0, seed=0, q8=None, ylo=None):
+    a, mean, rstd, nbytes = _ln_fwd_struct(x, gamma, beta, eps, y, yb, mean, rstd, row_scale, act, drop_p, seed, q8,
+                                           ylo=ylo)
     _traced("layernorm_fwd", nbytes, lambda: call("ste_layernorm_fwd", C.byref(a), _s()))
     return mean, rstd
 
@@ -285,6 +300,43 @@ def attention_fwd(q, k, v, *, B, T, H, o, lse, key_mask=None, rel_E=None, rel_le
     return a
 
 
+def attention_fwd_f32(q, k, v, *, B, T, H, o32, lse, o=None, o_lo=None, key_mask=None, scale=0.125, drop_p=0.0,
+                      seed=0):
+    """fp32 q/k/v [B*T, *] views -> O fp32 (o32) + optional bf16 hi / lo copies for the bf16
+    backward, lse fp32 [B*H*T] (ste_attention_fwd_f32: the text encoder's precise forward)."""
+    assert q.dtype == F32 and k.dtype == F32 and v.dtype == F32 and (o32 is None or o32.dtype == F32)
+    a = AttnArgs()
+    a.B, a.T, a.H = B, T, H
+    a.q, a.ldq = ptr(q), _ld(q)
+    a.k, a.ldk = ptr(k), _ld(k)
+    a.v, a.ldv = ptr(v), _ld(v)
+    if o is not None:
+        a.o, a.ldo = ptr(o), _ld(o)
+    if o_lo is not None:
+        a.o_lo, a.ldolo = ptr(o_lo), _ld(o_lo)
+    a.lse = ptr(lse)
+    a.key_mask = ptr(key_mask)
+    a.scale, a.drop_p, a.seed = float(scale), float(drop_p), int(seed) & (2**64 - 1)
+    call("ste_attention_fwd_f32", C.byref(a), ptr(o32), 0 if o32 is None else _ld(o32), _s())
+
+
+def split_bf16(x, nblk, lo_mask, out=None):
+    """fp32 [rows, K] -> bf16 [rows, nblk·K]: copy i = bf16(x), or its low half bf16(x - bf16(x)) where
+    bit i of lo_mask is set (ste_split_bf16)."""
+    rows, K = x.shape
+    if out is None:
+        out = torch.empty((rows, nblk * K), device=x.device, dtype=BF16)
+    assert out.shape == (rows, nblk * K) and out.is_contiguous() and out.dtype == BF16
+    call("ste_split_bf16", ptr(x), _ld(x), rows, K, ptr(out), int(nblk), int(lo_mask), _s())
+    return out
+
+
+def linear_x2(x, w2, bias=None, **kw):
+    """y = x·w_bf16ᵀ (+bias) with x fp32 [M, K] kept to ~16 mantissa bits, on the bf16 MFMA: one
+    GEMM over K' = 2K of [x_hi | x_lo]·[w | w]ᵀ (w2 = ParamStore.w2, the bf16 weight twice)."""
+    return gemm(split_bf16(x, 2, 2), w2, a_kc=True, b_kc=True, bias=bias, **kw)
+
+
 def attention_bwd(q, k, v, o, lse, dout, dq, dk, dv, *, B, T, H, delta, key_mask=None, rel_E=None, rel_left=64,
                   rel_right=8, scale=0.125, drop_p=0.0, seed=0, dE=None, gwork=None, o_lo=None):
     a = AttnArgs()
@@ -344,6 +396,24 @@ def attn_pool_fwd(t, w2, b2, h, mask, B, L, weights, pooled, pooled_bf16=None):
          ptr(weights), ptr(pooled), ptr(pooled_bf16), _s())
 
 
+def attn_pool_fwd_f32(t, w2, b2, h, mask, B, L, weights, pooled, pooled_bf16=None):
+    """attn_pool_fwd on fp32 scorer activations t and fp32 states h (the text side)."""
+    assert t.dtype == F32 and h.dtype == F32
+    call("ste_attn_pool_fwd_f32", ptr(t), ptr(w2), ptr(b2), ptr(h), ptr(mask), B, L, t.shape[-1], h.shape[-1],
+         ptr(weights), ptr(pooled), ptr(pooled_bf16), _s())
+
+
+def attn_pool_bwd_f32(t, w2, h, weights, dpooled, B, L, dh, dz, dw2=None, db2=None, db1=None, mask=None):
+    """attn_pool_bwd on fp32 t / h with an fp32 dz (no low half needed)."""
+    assert t.dtype == F32 and h.dtype == F32 and dz.dtype == F32
+    nwork = fn("ste_attn_pool_bwd_work_floats")(B, L, t.shape[-1])
+    if nwork < 0:
+        raise _lib.SteError(f"ste_attn_pool_bwd_work_floats failed with status {nwork}")
+    work = torch.empty(nwork, device=t.device, dtype=F32)
+    call("ste_attn_pool_bwd_f32", ptr(t), ptr(w2), ptr(h), ptr(weights), ptr(dpooled), ptr(mask), B, L, t.shape[-1],
+         h.shape[-1], ptr(dh), ptr(dz), ptr(dw2), ptr(db2), ptr(db1), ptr(work), _s())
+
+
 def attn_pool_bwd(t, w2, h, weights, dpooled, B, L, dh, dz, dw2=None, db2=None, db1=None, dz_lo=None, mask=None):
     """AttentivePooling backward: dh += ..., dz (bf16, + optional low half dz_lo), dw2/db2 and the
     first Linear's bias gradient db1 (fp32 column sums of dz) accumulated.  mask: the forward's
@@ -357,6 +427,10 @@ def attn_pool_bwd(t, w2, h, weights, dpooled, B, L, dh, dz, dw2=None, db2=None, 
 
 
 def mean_pool_fwd(h, mask, B, L, cls, weights, pooled, pooled_bf16=None):
+    if h.dtype == F32:
+        call("ste_mean_pool_fwd_f32", ptr(h), ptr(mask), B, L, h.shape[-1], int(bool(cls)), ptr(weights), ptr(pooled),
+             ptr(pooled_bf16), _s())
+        return
     call("ste_mean_pool_fwd", ptr(h), ptr(mask), B, L, h.shape[-1], int(bool(cls)), ptr(weights), ptr(pooled),
          ptr(pooled_bf16), _s())
 

@@ -124,6 +124,7 @@ class ParamStore:
         self._versions = {}
         self._wt = {}          # (name, count) -> (Wᵀ bf16, param versions, opt_epoch) (see wt())
         self._wq = {}          # (name, count) -> ((W e4m3, E8M0 scales), versions, opt_epoch) (see wq())
+        self._w2 = {}          # (name, count) -> ([W | W] bf16 [out, 2·in], versions, opt_epoch) (see w2())
         self.opt_epoch = 0     # fused optimizer steps so far (each refreshes the shadow of every trained weight)
         self._prebuilt = None  # (event, stream, streams that waited): Wᵀ rebuilt by refresh_transposes
         self.sync_shadow(force=True)
@@ -182,6 +183,26 @@ class ParamStore:
         self._wq[key] = (q, versions, self.opt_epoch)
         return q
 
+    def w2(self, name: str, count: int = 1):
+        """W as [W_bf16 | W_bf16] [out, 2·in] (the B operand of ops.linear_x2: the text encoder's
+        precise forward, activations split hi | lo against the bf16 weight twice).  Built from the
+        fp32 master; cached with wt()'s invalidation rules; refresh_transposes rebuilds the trained
+        ones after an optimizer step."""
+        key = (name, count)
+        versions, trained = self._group_versions(name, count)
+        ent = self._w2.get(key)
+        if ent is not None and ent[1] == versions and (not trained or ent[2] == self.opt_epoch):
+            self._wait_prebuilt()
+            return ent[0]
+        s = self.slots[name]
+        src = self.master[s.offset:s.offset + s.numel * count].view(s.shape[0] * count, -1)
+        dst = ent[0] if ent is not None else None
+        if dst is not None:
+            self._wait_prebuilt()
+        dst = ops.split_bf16(src, 2, 0, dst)
+        self._w2[key] = (dst, versions, self.opt_epoch)
+        return dst
+
     def wt(self, name: str, count: int = 1):
         """Wᵀ as a contiguous bf16 [in, out] matrix (the KC operand of dX = dY·W; `count` > 1:
         the adjacent fused group starting at `name`, e.g. Q|K|V -> [in, 3·out]).  Built from the
@@ -202,6 +223,10 @@ class ParamStore:
             return ent[0]
         src = self.fused(name, count, "w") if count > 1 else self.w(name)
         dst = ent[0] if ent is not None else None
+        if dst is not None:
+            # the side stream's refresh_transposes may still be writing this buffer: rebuilding
+            # it on this stream without the wait would race with that write
+            self._wait_prebuilt()
         dst = ops.transpose16(src, dst)
         self._wt[key] = (dst, versions, self.opt_epoch)
         return dst
@@ -215,13 +240,18 @@ class ParamStore:
             return
         stale = [k for k, ent in self._wt.items()
                  if ent[2] != self.opt_epoch and self.slots[k[0]].segment in ("enc", "head")]
-        if not stale:
+        stale2 = [k for k, ent in self._w2.items()
+                  if ent[2] != self.opt_epoch and self.slots[k[0]].segment in ("enc", "head")]
+        if not stale and not stale2:
             return
         cur = torch.cuda.current_stream(self.device)
         stream.wait_stream(cur)               # the optimizer's shadow writes
+        self._prebuilt = None                 # the rebuilds below must not wait on the previous event
         with torch.cuda.stream(stream):
             for name, count in stale:
                 self.wt(name, count)
+            for name, count in stale2:
+                self.w2(name, count)
             ev = torch.cuda.Event()
             ev.record(stream)
         self._prebuilt = (ev, stream, set())

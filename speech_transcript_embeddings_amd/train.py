@@ -199,6 +199,13 @@ class GradSync:
     all-reduce would give, from ~2*b*L rows instead of 192 M values.  When the lists would not be
     smaller than the table (world x capacity >= vocab / 2, e.g. long accumulation windows), the
     table goes through the dense all-reduce instead.
+    The list capacity, and with it the sparse-vs-dense choice, must be identical on every rank
+    (one rank in all_gather while another is in all_reduce hangs the job), but ranks may hold
+    different token counts (a short last batch, length-bucketed padding).  plan_words(n_ids),
+    called when a step's final micro-batch starts, all-reduces (MAX) the count asynchronously
+    and copies the result to pinned host memory on a side stream; the text stage reads it
+    after waiting only for that copy (issued a whole forward + backward earlier), never for
+    the step's own kernels.
     `finish()` waits for every collective (on the current stream) before clip + AdamW.
     """
 
@@ -215,6 +222,8 @@ class GradSync:
         self.pad_id = pad_id
         self.works = []
         self.sparse = None
+        self._plan = None
+        self._plan_stream = None
         grad_slots = [sl for sl in store.slots.values() if sl.segment in ("enc", "head")]
 
         ordered = sorted(grad_slots, key=lambda x: x.offset)
@@ -278,14 +287,52 @@ class GradSync:
                     t.mul_(1.0 / ws)
                 self.works.append(dist.all_reduce(t, op=op, async_op=True))
 
-    def _sparse_words(self, ids):
+    def plan_words(self, n_ids: int):
+        """Start agreeing on the word-table exchange capacity (MAX of every rank's token count
+        this step, async); stage_done("text") reads it."""
+        self._plan = None
+        if not self.active() or self.words is None:
+            return
+        dev = self.store.device
+        if dist.get_backend() == "nccl" and dev.type == "cuda":
+            t = torch.tensor([int(n_ids)], dtype=torch.int64, device=dev)
+            work = dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=True)
+            if self._plan_stream is None:
+                self._plan_stream = torch.cuda.Stream(device=dev)
+            host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+            with torch.cuda.stream(self._plan_stream):
+                work.wait()                       # this side stream (not the step's) waits for it
+                host.copy_(t, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            self._plan = (ev, host, t)
+        else:                                     # gloo: host tensors, the wait is the collective's
+            t = torch.tensor([int(n_ids)], dtype=torch.int64)
+            self._plan = (dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=True), t, t)
+
+    def agreed_ids(self, n_ids: int) -> int:
+        """The rank-agreed token count of this step (plan_words), or n_ids without a plan."""
+        if self._plan is None:
+            return int(n_ids)
+        waiter, host, _keep = self._plan
+        if isinstance(waiter, torch.cuda.Event):
+            waiter.synchronize()
+        else:
+            waiter.wait()
+        self._plan = None
+        n = int(host[0])
+        if n < n_ids:
+            raise RuntimeError(f"word-table capacity {n} < this rank's {n_ids} token ids: plan_words saw another count")
+        return n
+
+    def _sparse_words(self, ids, cap_ids):
         st, sl = self.store, self.words
         D = sl.shape[1]
         g2 = st.grad[sl.offset:sl.offset + sl.numel].view(sl.shape)
         dev = st.device
         if self._flags is None:
             self._flags = torch.zeros(sl.shape[0], device=dev, dtype=torch.int32)
-        cap = min(ids.numel(), sl.shape[0])
+        cap = min(cap_ids, sl.shape[0])
         out_ids = torch.empty(cap, device=dev, dtype=torch.int32)
         rows = torch.empty(cap, D, device=dev, dtype=F32)
         count = torch.empty(1, device=dev, dtype=torch.int32)
@@ -309,8 +356,9 @@ class GradSync:
             return
         self._reduce(self.ranges[stage])
         if stage == "text" and self.words is not None:
-            if ids is not None and self.sparse_pays(ids.numel()):
-                self._sparse_words(ids)
+            n = self.agreed_ids(ids.numel() if ids is not None else 0)
+            if ids is not None and self.sparse_pays(n):   # n, hence the choice, equal on every rank
+                self._sparse_words(ids, n)
             else:
                 self._reduce([(self.words.offset, self.words.offset + self.words.numel)])
 
@@ -407,7 +455,10 @@ class EmbeddingExchange:
             ops.axpby(dtp, dT)
 
     def finish(self, loss):
-        """Global similarity matrix + on-device metric accumulation (after the backward)."""
+        """Global similarity matrix + on-device metric accumulation (after the backward).  No
+        collective here: the similarity metrics come from the gathered embeddings (identical on
+        every rank), and acc[5] sums only this rank's B·loss; epoch_metrics() all-reduces it once
+        per epoch."""
         if self._pending is None:
             return
         A_g, T_g, B, ws, rank = self._wait()
@@ -416,21 +467,29 @@ class EmbeddingExchange:
         dev = A_g.device
         if self.acc is None:
             self.acc = torch.zeros(6, device=dev, dtype=torch.float64)
-        losses = loss
-        if ws > 1:
-            losses = torch.empty(ws, device=dev, dtype=F32)
-            dist.all_gather_into_tensor(losses, loss)
         S = torch.empty(NB, 2 * NB, device=dev, dtype=F32)
         ops.similarity(A_g, T_g, S)
-        ops.pair_metrics(S, NB, self.tau, self.acc, losses=losses, loss_w=float(B))
+        ops.pair_metrics(S, NB, self.tau, self.acc, losses=loss, loss_w=float(B))
         self.last_S = S
         self.steps += 1
 
     def epoch_metrics(self, reset: bool = True):
         """The reference's train_epoch return keys (ref :1156-1162) over the global batch, plus
         pair_accuracy (s_pos > s_neg) and in_batch_top1 (retrieval among the clean transcripts).
-        One device->host transfer."""
-        if self.acc is None or self.acc[4].item() == 0:
+        One device->host transfer; with several ranks also one all-reduce of the loss sum, so
+        every rank must call it (at the same epoch boundary)."""
+        ws, _ = self.world()
+        if self.acc is None:
+            if ws > 1:   # keep the collective matched with ranks that did accumulate
+                raise RuntimeError("epoch_metrics() before any finish() on this rank")
+            return {}
+        if ws > 1:
+            lsum = self.acc[5:6].clone()
+            if dist.get_backend() == "gloo" and lsum.is_cuda:
+                lsum = lsum.cpu()
+            dist.all_reduce(lsum, op=dist.ReduceOp.SUM)
+            self.acc[5:6].copy_(lsum.to(self.acc.device))
+        if self.acc[4].item() == 0:
             return {}
         a = self.acc.cpu().tolist()
         n = a[4]
@@ -510,6 +569,10 @@ class TrainStep:
         st = m.store
         st.sync_shadow()
         eng = m.engine
+        if self._micro + 1 == self.acc:   # the window's last micro-batch: agree on the word-table
+            # exchange capacity now (async), a forward + backward before stage "text" needs it
+            n_ids = batch["input_ids_pos"].numel() + batch["input_ids_neg"].numel()
+            self.gradsync.plan_words(n_ids + sum(int(t.numel()) for t in (self._ids if self._micro else [])))
         tf_p, tf_n, af, align, ctx = eng.forward(batch, True)
         B, P = af.shape
         # L2 normalise, similarity matrix S = A·[Tp;Tn]^T (fp32 MFMA), loss on its diagonals
@@ -579,6 +642,7 @@ class TrainStep:
         if self._micro == 0:
             return False
         ids_all = torch.cat(self._ids)
+        self.gradsync.plan_words(ids_all.numel())
         for stg in GradSync.STAGES:
             self.gradsync.stage_done(stg, ids_all)
         self._optimizer_step()

@@ -61,8 +61,30 @@ def rows_accumulate_ref(g2, ids, rows, scale):
             g2[i] += rows[s] * scale
 
 
+class _Recorder:
+    """Wraps torch.distributed's collectives while active and records (name, async_op) per call."""
+    NAMES = ("all_reduce", "all_gather_into_tensor", "all_gather", "broadcast", "reduce_scatter_tensor", "barrier")
+
+    def __enter__(self):
+        self.calls, self._orig = [], {}
+        for n in self.NAMES:
+            f = self._orig[n] = getattr(dist, n)
+
+            def wrap(*a, _f=f, _n=n, **k):
+                self.calls.append((_n, bool(k.get("async_op", False))))
+                return _f(*a, **k)
+            setattr(dist, n, wrap)
+        return self
+
+    def __exit__(self, *exc):
+        for n, f in self._orig.items():
+            setattr(dist, n, f)
+
+
 def _sync_case(rank, world):
-    """Dense blocks + sparse word table; returns (max err vs the all-rank average, untouched tail ok)."""
+    """Dense blocks + sparse word table; returns (max err vs the all-rank average, untouched tail ok,
+    every collective async).  The ranks hold DIFFERENT token counts (the sparse
+    capacity and the sparse-vs-dense choice must still agree), agreed by plan_words."""
     from speech_transcript_embeddings_amd import ops
     from speech_transcript_embeddings_amd.train import GradSync
     ops.rows_extract, ops.rows_accumulate = rows_extract_ref, rows_accumulate_ref
@@ -79,7 +101,7 @@ def _sync_case(rank, world):
         gen = torch.Generator().manual_seed(100 + r)
         for a, b in ((200, 237), (240, 341), (344, 357), (360, 405)):  # dense slots (gaps = alignment padding)
             g[a:b] = torch.randn(b - a, generator=gen)
-        ids = torch.randint(2, V, (12,), generator=gen)
+        ids = torch.randint(2, V, (10 + 2 * r,), generator=gen)
         ids[3] = 1  # padding_idx: never a gradient row
         for i in ids.tolist():
             if i != 1:
@@ -92,11 +114,15 @@ def _sync_case(rank, world):
     gs = GradSync(_Store(g, slots))
     assert all(gs.ranges[k] for k in GradSync.STAGES), gs.ranges   # every stage has a non-empty block
     gs.bucket = 29  # several buckets + ragged ones
-    for stage in GradSync.STAGES:
-        gs.stage_done(stage, ids)
+    with _Recorder() as rec:
+        gs.plan_words(ids.numel())
+        for stage in GradSync.STAGES:
+            gs.stage_done(stage, ids)
+    assert gs.sparse is not None and gs.sparse[3] == 10 + 2 * (world - 1)   # sparse, at the agreed MAX capacity
     gs.finish()
     n = gs.store.n_grad
-    return (g[:n] - expect[:n]).abs().max().item(), bool(torch.all(g[408:] == 7.0 + rank))
+    all_async = bool(rec.calls) and all(a for _, a in rec.calls)
+    return (g[:n] - expect[:n]).abs().max().item(), bool(torch.all(g[408:] == 7.0 + rank)), all_async
 
 
 def _exchange_stand_ins():
@@ -150,6 +176,12 @@ def _exchange_case(rank, world):
     a, tp, tn = emb(rank)
     tn_all = torch.cat([tp, tn]).contiguous()
     loss = torch.tensor([0.25 + rank])
+    # in_batch_weight == 0 (the reference's loss): start + finish issue only async collectives
+    ex0 = EmbeddingExchange(tau)
+    with _Recorder() as rec:
+        ex0.start(a, tn_all)
+        ex0.finish(torch.tensor([0.25 + rank]))
+    out_async = bool(rec.calls) and all(x for _, x in rec.calls)
     ex = EmbeddingExchange(tau, in_batch_weight=lam)
     ex.start(a, tn_all)
     # in-batch term (its own loss accumulator and cotangents, zero-initialised)
@@ -157,7 +189,7 @@ def _exchange_case(rank, world):
     dan, dtp = torch.zeros(B, P), torch.zeros(B, P)
     ex.in_batch(a, None, lterm, dan, dtp)
     ex.finish(loss)
-    out = {}
+    out = {"exchange_async": out_async}
     S = ex.last_S
     NB = world * B
     i = torch.arange(NB)
@@ -201,7 +233,7 @@ def _worker(rank, world, port, q):
         from oracle import det_init, ref_model as R
         out = {}
         # 1. overlapped dense all-reduce + row-sparse word table == plain average
-        out["sync_err"], out["tail_ok"] = _sync_case(rank, world)
+        out["sync_err"], out["tail_ok"], out["sync_async"] = _sync_case(rank, world)
         # 2. DP gradient == global-batch gradient (oracle autograd, golden mini model with alignment head)
         meta = json.loads((GOLDEN / "model_golden_align.json").read_text())
         z = np.load(GOLDEN / "model_golden_align.npz")
@@ -270,6 +302,7 @@ def test_data_parallel_gloo_world2():
         assert p.exitcode == 0
     for r, out in res.items():
         assert out["sync_err"] < 1e-6 and out["tail_ok"], (r, out["sync_err"])
+        assert out["sync_async"] and out["exchange_async"], (r, out)   # no synchronous collective in a step
         assert out["dp_rel"] < 1e-5, (r, out["dp_rel"])
         assert out["diag_ok"] and out["metrics_ok"], (r, out)
         assert out["inbatch_loss_err"] < 1e-5 and out["inbatch_grad_err"] < 1e-5, (r, out)

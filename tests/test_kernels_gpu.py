@@ -209,6 +209,180 @@ def test_gemm_epilogues(ops):
     assert rel_err(c, v + r + c0) < 1e-5
 
 
+# ------------------------------------------------ fp32 GEMM of the heads (ste_gemm_f32)
+def _rel64(a, ref):
+    a, ref = a.double(), ref.double()
+    return ((a - ref).norm() / (ref.norm() + 1e-30)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 1536, 768), (128, 768, 1536), (8192, 384, 768), (37, 68, 52), (3, 8, 4)])
+def test_gemm_f32_layouts(ops, M, N, K):
+    """fp32 operands on the f32 matrix core (exact fmaf chains): forward, dX and dW layouts at
+    the heads' shapes (projection / fusion at batch rows, the text pooling scorer at 2·b·L rows)
+    and ragged ones, against float64."""
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV)
+    b = torch.randn(N, device=DEV)
+    assert _rel64(ops.linear(x, w, b), x.double() @ w.double().t() + b.double()) < 2e-6
+    dy = torch.randn(M, N, device=DEV)
+    assert _rel64(ops.linear_dx(dy, w), dy.double() @ w.double()) < 2e-6
+    g = torch.randn(N, K, device=DEV)
+    ref = g.double() + dy.double().t() @ x.double()
+    ws = torch.empty(8 << 20, device=DEV)
+    ops.linear_dw(dy, x, out=g, beta=1.0, ws=ws)    # K = M rows: split into slabs when M >= 1024
+    assert _rel64(g, ref) < 2e-6
+    # bit-for-bit repeatable (slabs summed in order, no atomics)
+    g2 = torch.zeros(N, K, device=DEV)
+    g3 = torch.zeros(N, K, device=DEV)
+    ops.linear_dw(dy, x, out=g2, beta=1.0, ws=ws)
+    ops.linear_dw(dy, x, out=g3, beta=1.0, ws=ws)
+    assert torch.equal(g2, g3)
+
+
+def test_gemm_f32_epilogues_and_views(ops):
+    """Every epilogue option of the fp32 GEMM (bias, activation + fp32 pre-activation, activation
+    backward with fp32 Z, dropout, row scale, column sums, residual, beta, bf16 copy) and strided
+    operand / output views (the fusion input [proj | att] and its halves)."""
+    from speech_transcript_embeddings_amd import _lib
+    torch.manual_seed(2)
+    M, N, K = 130, 256, 192
+    x = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV) * 0.1
+    b = torch.randn(N, device=DEV)
+    ref = x.double() @ w.double().t() + b.double()
+    for act, fn in [(_lib.ACT_SWISH, F.silu), (_lib.ACT_GELU, F.gelu), (_lib.ACT_TANH, torch.tanh),
+                    (_lib.ACT_RELU, F.relu)]:
+        pre = torch.empty(M, N, device=DEV)
+        c3 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        out = ops.linear(x, w, b, act=act, pre_out=pre, out_bf16_copy=c3)
+        assert _rel64(out, fn(ref)) < 1e-5
+        assert _rel64(pre, ref) < 2e-6
+        assert torch.equal(c3, out.bfloat16())
+    z = torch.randn(M, N, device=DEV)
+    rs = (torch.rand(M, device=DEV) > 0.3).float()
+    r = torch.randn(M, N, device=DEV)
+    cs = torch.zeros(N, device=DEV)
+    c = torch.randn(M, N, device=DEV)
+    c0 = c.clone()
+    seed, p = 99, 0.25
+    ops.linear(x, w, None, act=_lib.ACT_GELU_BWD, z=z, drop_p=p, seed=seed, row_scale=rs, colsum=cs, residual=r,
+               beta=1.0, out=c, alpha=0.5)
+    idx = (np.arange(M)[:, None] * N + np.arange(N)[None, :]).astype(np.uint64)
+    dmask = torch.from_numpy(drop_scale(seed, idx, p)).to(DEV).double()
+    zf = z.double()
+    gd = torch.special.ndtr(zf) + zf * torch.exp(-0.5 * zf * zf) / math.sqrt(2 * math.pi)
+    v = 0.5 * (x.double() @ w.double().t()) * gd * dmask * rs.double()[:, None]
+    assert _rel64(cs, v.sum(0)) < 1e-5
+    assert _rel64(c, v + r.double() + c0.double()) < 1e-5
+    # strided views: A = the right half of a [M, 2K] buffer, C = the right half of [M, 2N]
+    big = torch.randn(M, 2 * K, device=DEV)
+    cat = torch.zeros(M, 2 * N, device=DEV)
+    ops.linear(big[:, K:], w, b, out=cat[:, N:])
+    assert _rel64(cat[:, N:], big[:, K:].double() @ w.double().t() + b.double()) < 2e-6
+    assert cat[:, :N].abs().max().item() == 0.0
+    dyv = torch.randn(M, 2 * N, device=DEV)[:, N:]
+    gw = torch.zeros(N, K, device=DEV)
+    ops.linear_dw(dyv, x, out=gw, beta=1.0)
+    assert _rel64(gw, dyv.double().t() @ x.double()) < 2e-6
+
+
+# ------------------------- split-bf16 ("bf16x3") GEMM and fp32 attention: the precise text forward
+def test_split_bf16_and_linear_x2(ops):
+    """ste_split_bf16 writes [hi | lo] (and [hi | lo | hi]) images exactly, and one bf16 MFMA GEMM over
+    the 2K concatenated columns of [x_hi | x_lo]·[w | w]ᵀ equals the product of the fp32 activations
+    with the bf16-rounded weight to ~2^-16 (plain bf16 operands: ~2^-9), under every epilogue the
+    text layer uses (bias + GELU + pre-activation + bf16 copy + dropout; residual)."""
+    from speech_transcript_embeddings_amd import _lib
+    torch.manual_seed(11)
+    M, N, K = 8192, 3072, 768
+    x = torch.randn(M, K, device=DEV) + 2.0          # a common component, as LayerNorm outputs have
+    w = torch.randn(N, K, device=DEV) * 0.05
+    b = torch.randn(N, device=DEV)
+    hi = x.bfloat16()
+    lo = (x - hi.float()).bfloat16()
+    a3 = ops.split_bf16(x, 3, 2)
+    assert torch.equal(a3[:, :K], hi) and torch.equal(a3[:, K:2 * K], lo) and torch.equal(a3[:, 2 * K:], hi)
+    a2 = ops.split_bf16(x, 2, 2)
+    assert torch.equal(a2[:, :K], hi) and torch.equal(a2[:, K:], lo)
+    w2 = ops.split_bf16(w, 2, 0)
+    wb = w.bfloat16()
+    assert torch.equal(w2[:, :K], wb) and torch.equal(w2[:, K:], wb)
+    ref = x.double() @ wb.double().t() + b.double()
+    y = ops.linear_x2(x, w2, b)
+    e2 = _rel64(y, ref)
+    e1 = _rel64(ops.linear(hi, wb, b), ref)
+    assert e2 < 2e-5 and e2 < e1 / 50, (e2, e1)
+    zt = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    hb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    h = ops.linear_x2(x, w2, b, act=_lib.ACT_GELU, pre_out=zt, out_bf16_copy=hb, drop_p=0.1, seed=5)
+    idx = (np.arange(M)[:, None] * N + np.arange(N)[None, :]).astype(np.uint64)
+    dmask = torch.from_numpy(drop_scale(5, idx, 0.1)).to(DEV).double()
+    assert _rel64(h, F.gelu(ref) * dmask) < 2e-5
+    assert torch.equal(hb, h.bfloat16()) and _rel64(zt, ref) < 4e-3
+    r = torch.randn(M, N, device=DEV)
+    y2 = ops.linear_x2(x, w2, b, residual=r)
+    assert _rel64(y2, ref + r.double()) < 2e-5
+    # producers writing the split image themselves: GEMM bf16 output + low-half copy (copy_lo),
+    # LayerNorm yb + ylo, both into the two halves of one [rows, 2·cols] buffer
+    hs = torch.empty(M, 2 * N, device=DEV, dtype=torch.bfloat16)
+    ops.linear_x2(x, w2, b, act=_lib.ACT_GELU, drop_p=0.1, seed=5, out=hs[:, :N], out_bf16_copy=hs[:, N:], copy_lo=True)
+    assert torch.equal(hs[:, :N], h.bfloat16()) and torch.equal(hs[:, N:], (h - h.bfloat16().float()).bfloat16())
+    g, be = torch.randn(K, device=DEV), torch.randn(K, device=DEV)
+    yl = torch.empty(M, K, device=DEV)
+    xs = torch.empty(M, 2 * K, device=DEV, dtype=torch.bfloat16)
+    ops.layernorm_fwd(x, g, be, 1e-5, y=yl, yb=xs[:, :K], ylo=xs[:, K:])
+    assert torch.equal(xs, ops.split_bf16(yl, 2, 2))
+
+
+@pytest.mark.parametrize("B,T,H,drop_p,masked", [(3, 64, 12, 0.0, True), (2, 100, 4, 0.1, True), (128, 64, 12, 0.1, False),
+                                                 (3, 16, 2, 0.0, "all")])
+def test_attention_f32_fwd(ops, B, T, H, drop_p, masked):
+    """The fp32 text attention forward against float64 (masked, ragged T past one 64-key chunk,
+    dropout, an all-masked sample); its saved bf16 copies + LSE drive the bf16 backward kernel to
+    the same gradients as from the bf16 forward."""
+    torch.manual_seed(T + H)
+    D, W = 64, H * 64
+    qkv = torch.randn(B * T, 3 * W, device=DEV) * 0.7
+    q, k, v = qkv[:, :W], qkv[:, W:2 * W], qkv[:, 2 * W:]
+    mask = None
+    if masked:
+        m = torch.ones(B, T, dtype=torch.int32, device=DEV)
+        m[0, T - T // 3:] = 0
+        m[1, :5] = 0
+        if masked == "all":
+            m[2, :] = 0
+        mask = m.reshape(-1).contiguous()
+    o32 = torch.empty(B * T, W, device=DEV)
+    o = torch.empty(B * T, W, device=DEV, dtype=torch.bfloat16)
+    olo = torch.empty_like(o)
+    lse = torch.empty(B * H * T, device=DEV)
+    ops.attention_fwd_f32(q, k, v, B=B, T=T, H=H, o32=o32, lse=lse, o=o, o_lo=olo, key_mask=mask, drop_p=drop_p,
+                          seed=3)
+    qd, kd, vd = (t.double().view(B, T, H, D) for t in (q, k, v))
+    ref = attention_ref(qd, kd, vd, mask.view(B, T) if masked else None, drop_p=drop_p, seed=3)
+    assert _rel64(o32.view(B, T, H, D), ref) < 1e-5
+    assert torch.equal(o, o32.bfloat16()) and torch.equal(olo, (o32 - o.float()).bfloat16())
+    sc = (qd.permute(0, 2, 1, 3) @ kd.permute(0, 2, 1, 3).transpose(-1, -2)) / 8.0
+    if masked:
+        sc = sc + (1.0 - mask.view(B, T)[:, None, None, :].double()) * torch.finfo(torch.float32).min
+    lse_ref = torch.logsumexp(sc, -1).reshape(-1)
+    fin = lse_ref.abs() < 1e30
+    assert _rel64(lse[fin], lse_ref[fin]) < 1e-6
+    # the bf16 backward on the saved copies: same gradients as the torch reference
+    qb, kb, vb = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    do = torch.randn(B * T, W, device=DEV).bfloat16()
+    dq, dk, dv = (torch.empty(B * T, W, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    delta = torch.empty(B * H * T, device=DEV)
+    ops.attention_bwd(qb, kb, vb, o, lse, do, dq, dk, dv, B=B, T=T, H=H, delta=delta, key_mask=mask, drop_p=drop_p,
+                      seed=3, o_lo=olo)
+    qf, kf, vf = (t.float().view(B, T, H, D).clone().requires_grad_() for t in (qb, kb, vb))
+    rf = attention_ref(qf, kf, vf, mask.view(B, T) if masked else None, drop_p=drop_p, seed=3)
+    rf.backward(do.float().view(B, T, H, D))
+    for got, want in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+        assert rel_err(got.view(B, T, H, D), want) < 1e-2
+
+
 # -------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("cols", [160, 768, 1024])
 def test_layernorm_fwd_bwd(ops, cols):
@@ -541,6 +715,41 @@ def test_attn_pool(ops, B, L, H, Hh):
     assert abs(db2.item() - b2r.grad.item()) < 1e-4
 
 
+@pytest.mark.parametrize("B,L,H,Hh", [(3, 64, 768, 384), (128, 64, 768, 384)])
+def test_attn_pool_f32(ops, B, L, H, Hh):
+    """The text side's fp32 pooling (fp32 scorer activations and states, fp32 dz) against
+    float64, including ragged and all-masked samples."""
+    torch.manual_seed(7)
+    h = torch.randn(B * L, H, device=DEV) + 3.0        # a large common component, as encoder states have
+    t = torch.tanh(torch.randn(B * L, Hh, device=DEV))
+    w2 = torch.randn(Hh, device=DEV) * 0.3
+    b2 = torch.randn(1, device=DEV)
+    lens = torch.randint(1, L + 1, (B,), generator=torch.Generator().manual_seed(L))
+    lens[1] = 0
+    mask = (torch.arange(L)[None, :] < lens[:, None]).to(torch.int32).reshape(-1).to(DEV)
+    weights = torch.empty(B * L, device=DEV)
+    pooled = torch.empty(B, H, device=DEV)
+    ops.attn_pool_fwd_f32(t, w2, b2, h, mask, B, L, weights, pooled)
+    tr = t.double().clone().requires_grad_()
+    hr = h.double().clone().requires_grad_()
+    w2r = w2.double().clone().requires_grad_()
+    s = (tr @ w2r + b2.double()).view(B, L).masked_fill(mask.view(B, L) == 0, -1e9)
+    pref = torch.bmm(torch.softmax(s, 1).unsqueeze(1), hr.view(B, L, H)).squeeze(1)
+    assert _rel64(pooled, pref) < 1e-6
+    dp = torch.randn(B, H, device=DEV)
+    pref.backward(dp.double())
+    dh = torch.zeros(B * L, H, device=DEV)
+    dz = torch.empty(B * L, Hh, device=DEV)
+    dw2 = torch.zeros(Hh, device=DEV)
+    db1 = torch.zeros(Hh, device=DEV)
+    ops.attn_pool_bwd_f32(t, w2, h, weights, dp, B, L, dh, dz, dw2, None, db1=db1, mask=mask)
+    dz_ref = tr.grad * (1 - t.double() ** 2)
+    assert _rel64(dh, hr.grad) < 1e-6
+    assert _rel64(dz, dz_ref) < 1e-5
+    assert _rel64(db1, dz_ref.sum(0)) < 1e-4
+    assert _rel64(dw2, w2r.grad) < 1e-4
+
+
 @pytest.mark.parametrize("cls", [False, True])
 def test_mean_pool(ops, cls):
     """use_attentive_pooling=False: text CLS row (ref:578-580), audio masked mean with
@@ -565,6 +774,12 @@ def test_mean_pool(ops, cls):
     assert (pooledb.float() - pooled).abs().max().item() <= pooled.abs().max().item() * 2 ** -8
     if not cls:
         assert pooled[2].abs().max().item() == 0.0
+    pooled32 = torch.empty(B, H, device=DEV)
+    h32 = torch.randn(B * L, H, device=DEV)
+    ops.mean_pool_fwd(h32, mask, B, L, cls, torch.empty(B * L, device=DEV), pooled32)   # fp32 states (text side)
+    h32r = h32.double().view(B, L, H)
+    p32 = h32r[:, 0, :] if cls else (h32r * mask.view(B, L, 1)).sum(1) / torch.clamp(mask.view(B, L, 1).sum(1), min=1e-9)
+    assert _rel64(pooled32, p32) < 1e-6
     dp = torch.randn(B, H, device=DEV)
     pref.backward(dp)
     dh = torch.ones(B * L, H, device=DEV)  # += semantics
