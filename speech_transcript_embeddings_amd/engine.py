@@ -180,10 +180,11 @@ class Engine:
             x, xb, sv, pre1 = self._conformer_fwd(i, x, b, T, maskf, mask32, train, _site_seed(base_seed, 100 + i),
                                                   last, save, pre1=pre1, nxt=nxt)
             layers[i] = sv if save else None
-        if xb is None:  # the last layer was dropped (only the last layer writes the bf16 copy)
-            xb = ops.cast_bf16(x, self._e(M, D, dtype=BF16))
+        if xb is None:  # the last layer was dropped (only the last layer writes the split image)
+            xb = ops.split_bf16(x, 2, 2)
         ctx["a_layers"] = layers
-        return x, xb
+        ctx["a_hs"] = xb    # [hi | lo] split image of the encoder output (audio pooling scorer)
+        return x, xb[:, :D]
 
     def _conformer_fwd(self, i, x, b, T, maskf, mask32, train, seed, want_bf16, save=True, pre1=None, nxt=None):
         """One Conformer layer.  pre1 = (a1, a1in, stats): this layer's FFN1 LN, already computed
@@ -277,10 +278,14 @@ class Engine:
         x4 = lin(h2in, pre + "ffn2.output_dense.weight", s.p(pre + "ffn2.output_dense.bias"), alpha=0.5,
                  residual=x3)
         x5 = self._e(M, D)
-        x5b = self._e(M, D, dtype=BF16) if want_bf16 else None
+        # the encoder output's bf16 copy as the [hi | lo] split image [M, 2D] (the audio pooling
+        # scorer reads it to ~fp32 accuracy; the hi half is the heads' bf16 operand)
+        x5s = self._e(M, 2 * D, dtype=BF16) if want_bf16 else None
+        x5b = x5s[:, :D] if want_bf16 else None
+        x5lo = x5s[:, D:] if want_bf16 else None
         pre_next = None
         if nxt is None:
-            sv["st6"] = self._ln(x4, pre + "final_layer_norm", eps, y=x5, yb=x5b)
+            sv["st6"] = self._ln(x4, pre + "final_layer_norm", eps, y=x5, yb=x5b, ylo=x5lo)
         else:
             # this final LN fused with layer nxt's FFN1 LN (x5 stays in registers for the second)
             prej = f"audio_encoder.encoder.layers.{nxt}.ffn1_layer_norm"
@@ -288,12 +293,12 @@ class Engine:
             second, a1j, a1inj = ln_in_out(prej, trj, gamma=s.p(prej + ".weight"), beta=s.p(prej + ".bias"), eps=eps)
             sv["st6"], st1j = ops.layernorm_fwd_pair(
                 dict(x=x4, gamma=s.p(pre + "final_layer_norm.weight"), beta=s.p(pre + "final_layer_norm.bias"), eps=eps,
-                     y=x5, yb=x5b), second)
+                     y=x5, yb=x5b, ylo=x5lo), second)
             pre_next = (a1j, a1inj, st1j)
         sv.update(x=x, z1=z1, x1=x1, qkv=qkv, o=o, o_lo=o_lo, lse=lse, x2=x2, pw1=pw1, cv=cv, x3=x3, z2=z2, x4=x4, p_conv=p_conv)
         if tr:
             sv.update(a1=a1, h1=h1, a2=a2, a3=a3, sw=sw, a5=a5, h2=h2)
-        return x5, x5b, sv, pre_next
+        return x5, x5s, sv, pre_next
 
     def _ln_bwd_kw(self, x, stats, name, **kw):
         """layernorm_bwd keyword set of the named LN (the pair kernels' argument form)."""
@@ -689,9 +694,12 @@ class Engine:
         ops.linear_dx(dz, self._w32(name + ".projection.0.weight"), out=dx_out, beta=1.0)
         self._dw32(dz, sv["x"], name + ".projection.0.weight")
 
-    def _pool_fwd(self, name, h, hb, mask32, nb, L, sv):
-        """AttentivePooling ref:171-211 -> pooled fp32 [nb, H]: text on the fp32 states (scorer on
-        ste_gemm_f32), audio on the bf16 copy (hb; hb=None: fp32 as well).  With
+    def _pool_fwd(self, name, h, hb, mask32, nb, L, sv, hs=None):
+        """AttentivePooling ref:171-211 -> pooled fp32 [nb, H] on the fp32 states h: the text
+        scorer on ste_gemm_f32; the audio scorer (31,936 rows at c2) on the bf16 MFMA over the
+        encoder output's [hi | lo] split image hs against [W | W] (~fp32 activations: its gradient
+        Σ_l dz_l ⊗ h_l cancels over frames sharing a large common component).  Without hs (the
+        wav2vec2 front end) the audio side runs on the bf16 copy hb.  With
         use_attentive_pooling=False: text CLS row (ref:578-580) / audio masked mean (ref:621-636)
         of the fp32 states."""
         s = self.s
@@ -702,11 +710,16 @@ class Engine:
             ops.mean_pool_fwd(h, mask32, nb, L, name == "text_pooling", w, pooled)
             sv.update(w=w)
             return pooled
-        f32 = name == "text_pooling" or hb is None
+        f32 = name == "text_pooling" or hb is None or hs is not None
         w2, b2 = s.p(name + ".attention.2.weight").view(-1), s.p(name + ".attention.2.bias")
         if f32:
-            t = ops.linear(h, self._w32(name + ".attention.0.weight"), s.p(name + ".attention.0.bias"), act=ACT_TANH)
+            if hs is not None:
+                t = ops.linear(hs, s.w2(name + ".attention.0.weight"), s.p(name + ".attention.0.bias"), act=ACT_TANH)
+            else:
+                t = ops.linear(h, self._w32(name + ".attention.0.weight"), s.p(name + ".attention.0.bias"),
+                               act=ACT_TANH)
             ops.attn_pool_fwd_f32(t, w2, b2, h, mask32, nb, L, w, pooled)
+            sv.update(hs=hs)
         else:
             t = ops.linear(hb, s.w(name + ".attention.0.weight"), s.p(name + ".attention.0.bias"), act=ACT_TANH,
                            out_bf16=True)
@@ -728,8 +741,20 @@ class Engine:
             dz = self._e(*t.shape)
             ops.attn_pool_bwd_f32(t, w2, sv["h"], sv["w"], dpooled, nb, L, dh, dz, dw2, s.g(name + ".attention.2.bias"),
                                   db1=s.g(name + ".attention.0.bias"), mask=sv["mask"])
-            ops.linear_dx(dz, self._w32(name + ".attention.0.weight"), out=dh, beta=1.0)
-            self._dw32(dz, sv["h"], name + ".attention.0.weight")
+            hs = sv.get("hs")
+            if hs is None:
+                ops.linear_dx(dz, self._w32(name + ".attention.0.weight"), out=dh, beta=1.0)
+                self._dw32(dz, sv["h"], name + ".attention.0.weight")
+                return
+            # audio: dX on the bf16 dz (no cancellation per row); dW = Σ_l dz_l ⊗ h_l to ~fp32 from
+            # the split halves: dz_hi·h_hi + dz_lo·h_hi + dz_hi·h_lo (three bf16 MFMA passes)
+            Hh, D = t.shape[1], hs.shape[1] // 2
+            dzs = ops.split_bf16(dz, 2, 2)
+            ops.linear_dx(dzs[:, :Hh], s.w(name + ".attention.0.weight"), out=dh, beta=1.0)
+            if gw1 is not None:
+                self._dw(dzs[:, :Hh], hs[:, :D], name + ".attention.0.weight")
+                self._dw(dzs[:, Hh:], hs[:, :D], name + ".attention.0.weight")
+                self._dw(dzs[:, :Hh], hs[:, D:], name + ".attention.0.weight")
             return
         dz = self._e(*t.shape, dtype=BF16)
         dz_lo = self._e(*t.shape, dtype=BF16) if gw1 is not None else None
@@ -761,7 +786,8 @@ class Engine:
 
     def _xq_bwd(self, name, xs, dcat, d_qin, dkvb):
         """Backward of _xq_fwd from d cat: d_qin (fp32) +=; dkvb (bf16 [B*S, 2P]) written, the
-        key/value bias gradient summed in fp32 by the kernel (over both query sets)."""
+        key/value bias gradient summed in fp32 by the kernel (over both query sets); or dkvb fp32
+        (zero-filled by the caller): accumulated, bias gradient left to the caller."""
         s = self.s
         P = d_qin.shape[1]
         datt = dcat[:, P:]
@@ -772,16 +798,32 @@ class Engine:
         dq = self._e(*xs["q"].shape)
         kv = xs["kv"]
         ops.xattn_bwd(xs["q"], kv[:, :P], kv[:, P:], xs["probs"], dq_in, xs["B"], xs["S"], self.m.xattn_heads, dq,
-                      dkvb[:, :P], dkvb[:, P:], xs["seeds"], drop_p=xs["p"], colsum=s.fused(name + ".key.bias", 2, "g"),
-                      mask=xs["mask"])
+                      dkvb[:, :P], dkvb[:, P:], xs["seeds"], drop_p=xs["p"],
+                      colsum=s.fused(name + ".key.bias", 2, "g") if dkvb.dtype == BF16 else None, mask=xs["mask"])
         ops.linear_dx(dq, self._w32(name + ".query.weight"), out=d_qin, beta=1.0)
         self._dw32(dq, xs["qin"], name + ".query.weight")
         self._db32(dq, name + ".query.bias")
 
     def _kv_src_bwd(self, name, src, dkvb, seqb, xb, dx):
         """K/V = Linear_kv(Linear_src(x)) backward (bf16, the shared side): dkvb [rows, 2P] ->
-        dx (fp32 +=); the src bias gradient summed in the K/V input-gradient GEMM's epilogue."""
+        dx (fp32 +=); the src bias gradient summed in the K/V input-gradient GEMM's epilogue.
+        dkvb fp32 (the per-call public API, whose positive and corrupted calls backpropagate
+        separately into the same audio states: their contributions cancel in dx and in these
+        weights' gradients, so each is carried to ~fp32): every product on split-bf16 operands."""
         s = self.s
+        if dkvb.dtype == F32:
+            P2 = dkvb.shape[1]
+            dkvs = ops.split_bf16(dkvb, 2, 2)
+            self._db(dkvb, name + ".key.bias", fused=2)
+            self._dw(dkvs[:, :P2], seqb, name + ".key.weight", fused=2)
+            self._dw(dkvs[:, P2:], seqb, name + ".key.weight", fused=2)
+            dseq = ops.linear(dkvs, s.wt2(name + ".key.weight", 2), colsum=s.g(src + ".bias"))
+            P = dseq.shape[1]
+            dseqs = ops.split_bf16(dseq, 2, 2)
+            self._dw(dseqs[:, :P], xb, src + ".weight")
+            self._dw(dseqs[:, P:], xb, src + ".weight")
+            ops.linear(dseqs, s.wt2(src + ".weight"), out=dx, beta=1.0)
+            return
         dseqb = self._dx(dkvb, name + ".key.weight", 2, out_bf16=True, colsum=s.g(src + ".bias"))
         self._dw(dkvb, seqb, name + ".key.weight", fused=2)
         self._dx(dseqb, src + ".weight", out=dx, beta=1.0)
@@ -817,7 +859,7 @@ class Engine:
         hs = {}
         tpool_sv, apool_sv, tproj_sv, aproj_sv = {}, {}, {}, {}
         tpooled = self._pool_fwd("text_pooling", th, thb, ctx["t_mask32"], nb, L, tpool_sv)
-        apooled = self._pool_fwd("audio_pooling", ah, ahb, ctx["a_mask32"], ab, T, apool_sv)
+        apooled = self._pool_fwd("audio_pooling", ah, ahb, ctx["a_mask32"], ab, T, apool_sv, hs=ctx.get("a_hs"))
         tproj = self._proj_fwd("text_projection", tpooled, nb, train, _site_seed(base_seed, 201), tproj_sv)
         aproj = self._proj_fwd("audio_projection", apooled, ab, train, _site_seed(base_seed, 202), aproj_sv)
         hs.update(tpool=tpool_sv, apool=apool_sv, tproj=tproj_sv, aproj=aproj_sv)
@@ -926,12 +968,14 @@ class Engine:
         dth, dah = self._z(b * L, Ht), self._z(b * T, Ha)
         dtcat = self._fuse_bwd("text_fusion", d_tf.float().contiguous(), sv["tf"])
         dacat = self._fuse_bwd("audio_fusion", d_af.float().contiguous(), sv["af"])
-        dkvb = self._e(b * T, 2 * P, dtype=BF16)
-        self._xq_bwd("text_to_audio_attention", sv["tx"], dtcat, d_tproj, dkvb)
-        self._kv_src_bwd("text_to_audio_attention", "audio_seq_to_projection", dkvb, sv["aseqb"], sv["ahb"], dah)
-        dkvtb = self._e(b * L, 2 * P, dtype=BF16)
-        self._xq_bwd("audio_to_text_attention", sv["ax"], dacat, d_aproj, dkvtb)
-        self._kv_src_bwd("audio_to_text_attention", "text_seq_to_projection", dkvtb, sv["tseqb"], sv["thb"], dth)
+        # per call, fp32 dK/dV and split-bf16 K/V products: the positive and corrupted calls'
+        # contributions to the shared audio side cancel once the caller's autograd sums them
+        dkv = self._z(b * T, 2 * P)
+        self._xq_bwd("text_to_audio_attention", sv["tx"], dtcat, d_tproj, dkv)
+        self._kv_src_bwd("text_to_audio_attention", "audio_seq_to_projection", dkv, sv["aseqb"], sv["ahb"], dah)
+        dkvt = self._z(b * L, 2 * P)
+        self._xq_bwd("audio_to_text_attention", sv["ax"], dacat, d_aproj, dkvt)
+        self._kv_src_bwd("audio_to_text_attention", "text_seq_to_projection", dkvt, sv["tseqb"], sv["thb"], dth)
         return d_tproj, dth, d_aproj, dah
 
     # ------------------------------------------------------- word alignment

@@ -270,7 +270,7 @@ class EnhancedAudioTextModel(nn.Module):
             h, hb = e.audio_forward(x, mask, self.training, _call_seed(self.training), ctx, save=False)
             B, L = ctx["a_b"], ctx["a_T"]
             m32, pool, proj = ctx["a_mask32"], "audio_pooling", "audio_projection"
-        pooled = e._pool_fwd(pool, h, hb, m32, B, L, {})
+        pooled = e._pool_fwd(pool, h, hb, m32, B, L, {}, hs=ctx.get("a_hs"))
         out = e._proj_fwd(proj, pooled, B, self.training, _call_seed(self.training), {})
         return out, h.view(B, L, -1)
 
@@ -300,7 +300,7 @@ class _EncodeFn(torch.autograd.Function):
             B, L = ctx["a_b"], ctx["a_T"]
             m32, pool, proj = ctx["a_mask32"], "audio_pooling", "audio_projection"
         sv_pool, sv_proj = {}, {}
-        pooled = e._pool_fwd(pool, h, hb, m32, B, L, sv_pool)
+        pooled = e._pool_fwd(pool, h, hb, m32, B, L, sv_pool, hs=ctx.get("a_hs"))
         out = e._proj_fwd(proj, pooled, B, train, _site(seed), sv_proj)
         fctx.model, fctx.kind, fctx.ctx = model, kind, ctx
         fctx.saved = (sv_pool, sv_proj, B, L, h.shape[-1], pool, proj)

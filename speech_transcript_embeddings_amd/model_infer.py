@@ -98,7 +98,7 @@ class EnhancedAudioTextModel(nn.Module):
         if attention_mask is None:
             attention_mask = torch.ones(B, T, dtype=torch.int64, device=input_features.device)
         h, hb = e.audio_forward(input_features.contiguous(), attention_mask.contiguous(), False, 0, ctx, save=False)
-        pooled = e._pool_fwd("audio_pooling", h, hb, ctx["a_mask32"], B, T, {})
+        pooled = e._pool_fwd("audio_pooling", h, hb, ctx["a_mask32"], B, T, {}, hs=ctx.get("a_hs"))
         return e._proj_fwd("audio_projection", pooled, B, False, 0, {}), h, hb, ctx["a_mask32"]
 
     def _attend(self, name, q_proj, kv_hb, mask32, B, S):

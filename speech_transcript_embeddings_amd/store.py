@@ -125,6 +125,8 @@ class ParamStore:
         self._wt = {}          # (name, count) -> (Wᵀ bf16, param versions, opt_epoch) (see wt())
         self._wq = {}          # (name, count) -> ((W e4m3, E8M0 scales), versions, opt_epoch) (see wq())
         self._w2 = {}          # (name, count) -> ([W | W] bf16 [out, 2·in], versions, opt_epoch) (see w2())
+        self._wt2 = {}         # (name, count) -> ([Wᵀ | Wᵀ], the wt() tensor, its rebuild stamp) (see wt2())
+        self._wt_stamp = {}    # (name, count) -> number of wt() rebuilds (wt2 follows them)
         self.opt_epoch = 0     # fused optimizer steps so far (each refreshes the shadow of every trained weight)
         self._prebuilt = None  # (event, stream, streams that waited): Wᵀ rebuilt by refresh_transposes
         self.sync_shadow(force=True)
@@ -203,6 +205,20 @@ class ParamStore:
         self._w2[key] = (dst, versions, self.opt_epoch)
         return dst
 
+    def wt2(self, name: str, count: int = 1):
+        """[Wᵀ | Wᵀ] bf16 [in, 2·out]: the KC operand of a dX GEMM over a [dy_hi | dy_lo] split image
+        (dy to ~fp32 against the bf16 weight).  Rebuilt from wt() whenever that is."""
+        wt = self.wt(name, count)
+        ent = self._wt2.get((name, count))
+        if ent is not None and ent[1] is wt and ent[2] == self._wt_stamp.get((name, count)):
+            return ent[0]
+        n, k = wt.shape
+        dst = ent[0] if ent is not None else torch.empty((n, 2 * k), device=wt.device, dtype=wt.dtype)
+        ops.copy2d(dst[:, :k], wt)
+        ops.copy2d(dst[:, k:], wt)
+        self._wt2[(name, count)] = (dst, wt, self._wt_stamp.get((name, count)))
+        return dst
+
     def wt(self, name: str, count: int = 1):
         """Wᵀ as a contiguous bf16 [in, out] matrix (the KC operand of dX = dY·W; `count` > 1:
         the adjacent fused group starting at `name`, e.g. Q|K|V -> [in, 3·out]).  Built from the
@@ -229,6 +245,7 @@ class ParamStore:
             self._wait_prebuilt()
         dst = ops.transpose16(src, dst)
         self._wt[key] = (dst, versions, self.opt_epoch)
+        self._wt_stamp[key] = self._wt_stamp.get(key, 0) + 1
         return dst
 
     def refresh_transposes(self, stream):

@@ -20,8 +20,10 @@ operands.  Random-init encoders produce activations that are nearly identical ac
 (a large common component), so every softmax backward dS = P(dP - delta) is a small
 difference of large terms: delta is formed from the ~fp32 attention output (ste_attn_args.o_lo,
 the forward's PV product on P = hi + lo), which took the q/k projections of the deepest
-trainable layer from 3.3 % to 1.7 %.  The worst tensors left are the audio attentive-pooling
-scorer (2.3 %): its tanh activations are stored bf16 and share the same common component.
+trainable layer from 3.3 % to 1.7 %.  The audio attentive-pooling scorer runs on the encoder
+output's [hi | lo] split image with fp32 tanh activations (r3: 2.3 % -> 1.75 %); what is left
+there is the bf16 audio encoder's forward rounding of that common component (the scorer's
+gradient Σ_l dz_l ⊗ h_l cancels across frames), the same limit as the deepest layers' q/k.
 """
 import pytest
 import torch
@@ -146,5 +148,8 @@ def test_full_size_vs_oracle(cname):
         # backward): measured median 12 %, worst 26 % (bf16 c5: 0.7 % / 2.1 %)
         assert median < 2e-1 and errs[0][0] < 4e-1, (median, errs[:5])
     else:
+        # measured (r3): median 0.6 %, worst 1.75 % (c2 / c4) and 2.0 % (c1), the audio pooling
+        # scorer and the deepest trainable layers' q/k: the audio encoder's bf16 forward rounding of
+        # frames that share a large common component (see the module docstring)
         assert median < 1e-2, median
-        assert errs[0][0] < 3e-2, errs[:5]
+        assert errs[0][0] < 2.5e-2, errs[:5]

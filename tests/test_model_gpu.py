@@ -1,6 +1,8 @@
 """End-to-end parity of the HIP model (through libste.so) against the CPU oracle and the
 reference's golden fixtures, at the golden mini dimensions (head_dim 64 like the real
-encoders).  bf16 MFMA path: tolerance 1e-2-class relative (north_star: 1e-2 bf16)."""
+encoders).  bf16 MFMA path: north_star's bf16 bound, 1e-2 relative on embeddings, loss and
+per-tensor gradient norms; elementwise gradients checked against the oracle with the bounds
+written in each test."""
 import json
 
 import numpy as np
@@ -163,22 +165,19 @@ def test_backward_random_cotangents(tag):
 @pytest.mark.parametrize("tag", ["noalign", "align", "nopool"])
 def test_forward_backward_matches_golden_and_oracle(tag):
     """The drop-in autograd path (compute_pos_neg_embeddings -> (aud*txt).sum(1) -> loss_fn ->
-    loss.backward(), ref :1068-1094) against the reference's golden outputs.
+    loss.backward(), ref :1068-1094) against the reference's golden outputs and the oracle.
 
     Forward: embeddings, s_pos, loss and alignment scores within 1e-2 of the reference's golden
-    values (north_star's bf16 bound; measured <= 0.5 %).
+    values (north_star's bf16 bound; measured <= 0.34 %).
 
-    Backward: per-tensor gradient norms against the reference's golden norms within 5e-2
-    (measured <= 4.7 %, median 0.4-0.9 %; 1e-1 without attentive pooling, measured 8.3 %).  Elementwise, the loss-derived gradients are NOT a test
-    of the backward: the positive and negative transcripts share 80 % of their tokens and
-    random-init encoders make every embedding point the same way, so each head's gradient is a
-    sum of nearly cancelling pos and neg terms (e.g. the text->audio out_proj gradient is
-    ~ds·a ⊗ (att_pos - att_neg)) and the bf16 forward's ~0.3 % rounding of near-identical pos/neg
-    activations reappears as 10-25 % elementwise differences — even when the oracle's backward
-    is seeded with the HIP path's own cotangents (measured 12 %), i.e. with no backward error at
-    all in the seed.  The backward's elementwise precision is checked where that cancellation is
-    absent: test_backward_random_cotangents (worst tensor 1.9 %, median 0.6 %) and, at full
-    size, tests/test_fullsize_gpu.py."""
+    Backward, loss-derived: every gradient's norm within 1e-2 of the golden norm (measured worst
+    0.30 / 0.40 / 0.29 % for noalign / align / nopool), and elementwise against the oracle's fp32
+    autograd on the same batch: per-tensor relative L2 error median < 1e-2 and worst < 3e-2
+    (measured median 0.6-0.8 %, worst 1.1 / 1.3 / 2.4 %), and >= 99 % of all gradient entries
+    with the reference's sign (measured 99.75-99.8 %).  These gradients are sums of nearly
+    cancelling positive- and corrupted-transcript terms (80 % shared tokens, random-init
+    encoders), which amplify forward rounding; the heads run in fp32 and the text encoder's
+    forward to ~fp32 accuracy for that reason (profiles/r3_parity.txt)."""
     meta, z = load(tag)
     model = mini_model(meta)
     model.eval()
@@ -215,9 +214,28 @@ def test_forward_backward_matches_golden_and_oracle(tag):
         worst.append((abs(g_gpu.double().norm().item() - gn) / gn, n))
     worst.sort(reverse=True)
     print(f"[{tag}] gradient-norm errors vs golden: worst {worst[:4]}, median {worst[len(worst) // 2][0]:.2e}")
-    # use_attentive_pooling=False (masked mean / CLS): the mean over near-identical frames
-    # cancels more strongly than the learned pooling (measured 8.3 %)
-    assert worst[0][0] < (1e-1 if tag == "nopool" else 5e-2), worst[:4]
+    assert worst[0][0] < 1e-2, worst[:4]
+    # elementwise against the oracle's fp32 autograd of the same loss (pinned to the golden)
+    cfg = R.mini_cfg(meta)
+    vals = det_init.state_dict_values(R.param_shapes(cfg, spec_augment=False))
+    p = {n: torch.from_numpy(v).requires_grad_(n in set(meta["trainable"])) for n, v in vals.items()}
+    bc = {k: v.cpu() for k, v in batch.items()}
+    lo, *_ = R.step_loss(p, bc, cfg)
+    lo.backward()
+    errs, agree, total = [], 0, 0
+    for n in meta["with_grad"]:
+        g_ref = p[n].grad.double().reshape(-1)
+        if g_ref.norm() < 1e-6:
+            continue
+        g_hip = params[n].grad.detach().double().cpu().reshape(-1)
+        errs.append((rel(g_hip, g_ref), n))
+        agree += int((torch.sign(g_hip) == torch.sign(g_ref)).sum())
+        total += g_ref.numel()
+    errs.sort(reverse=True)
+    print(f"[{tag}] elementwise vs oracle: worst {errs[:3]}, median {errs[len(errs) // 2][0]:.2e}, "
+          f"sign agreement {agree / total:.5f}")
+    assert errs[len(errs) // 2][0] < 1e-2 and errs[0][0] < 3e-2, errs[:3]
+    assert agree >= 0.99 * total, agree / total
 
 
 def test_fp8_gemm_matches_oracle():
@@ -311,17 +329,15 @@ def test_train_step_matches_reference_optimizer_step(tag):
     get_linear_schedule_with_warmup at scheduler step 1; ref :1084-1117, :1487-1541).
     Eval numerics (every dropout 0, no SpecAugment, no layerdrop) so both sides run the same
     function.  Checked:
-      * loss within 1e-2, clip_grad_norm_'s total norm within 2e-2 (a norm over every gradient,
-        inheriting the per-tensor norm errors of test_forward_backward_matches_golden_and_oracle);
+      * loss within 1e-2, clip_grad_norm_'s total norm within 1e-2 (measured 4e-5 / 4e-4);
       * both groups' learning rates exactly (lr/50 and lr at warmup factor 1/2);
       * the updated parameters at the golden's sampled entries.  AdamW's first step from zero
         moments moves each entry by lr·g/(|g| + eps) ≈ ±lr, so the new value depends only on
         the SIGN of its clipped gradient.  (a) Given the HIP gradient the fused clip + AdamW +
         schedule is exact (1e-6); (b) against the reference's updated values every entry differs
         by exactly lr·|u_hip - u_ref|, u = g/(|g| + eps) of each side's clipped gradient — only
-        through the gradients — and the update directions agree (|Δu| < 1e-3) on >= 90 % of the
-        sampled entries: the loss-derived gradients carry the pos/neg cancellation error
-        described in test_forward_backward_matches_golden_and_oracle, so small entries can flip."""
+        through the gradients — and the update directions (the gradient signs) agree on >= 99 %
+        of the sampled entries (measured 99.6 %)."""
     from speech_transcript_embeddings_amd.train import TrainStep
     meta, z = load(tag)
     model = mini_model(meta, spec_augment=False)
@@ -341,7 +357,7 @@ def test_train_step_matches_reference_optimizer_step(tag):
     tn = step.opt.total_norm()
     print(f"[{tag}] loss {loss.item():.6f} vs {float(z['loss']):.6f}; clip total norm {tn:.6f} vs "
           f"{float(z['clip_total_norm']):.6f}")
-    assert rel(tn, float(z["clip_total_norm"])) < 2e-2
+    assert rel(tn, float(z["clip_total_norm"])) < 1e-2
     f = step.opt.last_factor
     lr_enc, lr_head = step.opt.groups[0]["lr"] * f, step.opt.groups[1]["lr"] * f
     assert abs(lr_enc - float(z["lr_enc"])) <= 1e-12 and abs(lr_head - float(z["lr_head"])) <= 1e-12
@@ -366,8 +382,14 @@ def test_train_step_matches_reference_optimizer_step(tag):
         g_ref = z[f"gsamp::{n}"].astype(np.float64) * coef_ref
         u_h, u_r = g / (np.abs(g) + 1e-8), g_ref / (np.abs(g_ref) + 1e-8)
         assert np.all(np.abs(new - ref) <= lr * np.abs(u_h - u_r) + 2e-6), n
-        agree += int((np.abs(u_h - u_r) < 1e-3).sum())
-        total += u_r.size
-    print(f"[{tag}] sampled entries whose gradient sign (hence update) agrees with the reference: "
+        # signs are compared where the reference gradient is not fp32 round-off: the key biases,
+        # the pooling scorer's output bias and the key slice of in_proj_bias have analytically zero
+        # gradients (softmax shift invariance) whose ±1e-10 values carry random signs — the oracle
+        # and the reference agree on only 98 % of the sampled entries because of them
+        gn = float(z[f"gnorm::{n}"])
+        live = np.abs(g_ref) > 1e-6 * max(gn, 1e-30) if gn >= 1e-6 else np.zeros(g_ref.shape, bool)
+        agree += int((np.sign(g) == np.sign(g_ref))[live].sum())
+        total += int(live.sum())
+    print(f"[{tag}] sampled entries whose gradient sign (hence update direction) agrees with the reference: "
           f"{agree}/{total} = {agree / total:.4f}")
-    assert agree >= 0.9 * total
+    assert agree >= 0.99 * total
