@@ -113,15 +113,41 @@ def _cpu_model():
     return "unknown"
 
 
+def _cgroup_cpus():
+    """CPUs the job may use under its cgroup CPU quota (cpu.max 'quota period'), or None."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                return max(1, int(int(q) // int(per)))
+        except (OSError, ValueError):
+            pass
+    try:   # cgroup v1
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_baseline(args):
     """the oracle (CPU fp32 restatement of the step, pinned to the reference by
     the golden fixtures) at c1 and c2 shapes with B=4, every host core this job may use, 2 warm-up
     steps then the median of >= 3 timed steps; the CPU model is reported."""
     import torch
     from oracle import fbank_ref, ref_model as R
+    # BASELINE.md §3: every host core, torch.set_num_threads(len(os.sched_getaffinity(0))).  On the
+    # GPU pool the affinity mask shows the whole machine (256 cores) while the job runs under a CPU
+    # quota (cgroup cpu.max; OMP_NUM_THREADS is set to it): 256 torch threads on a 16-CPU quota did
+    # not finish one warm-up step in 180 s (r3).  "Every host core" is therefore read as every core
+    # the job may use: min(affinity, cgroup quota, OMP_NUM_THREADS — which the pool sets to the
+    # quota); the affinity count is reported beside it.
     cores = len(os.sched_getaffinity(0))
     omp = os.environ.get("OMP_NUM_THREADS")
-    threads = min(cores, int(omp)) if omp and omp.isdigit() else cores
+    threads = min(cores, _cgroup_cpus() or cores, int(omp) if omp and omp.isdigit() else cores)
+    share = threads
     torch.set_num_threads(threads)
     cfg = R.ModelCfg(use_word_alignment=args.align, text_layers_to_unfreeze=args.unfreeze,
                      audio_layers_to_unfreeze=args.unfreeze)
@@ -171,7 +197,10 @@ def cpu_baseline(args):
     def timed(B, seconds, L):
         N = int(seconds * 16000)
         for w in range(2):
+            t0 = time.perf_counter()
             one_step(1 + w, B, N, L)
+            print(f"[cpu_baseline] {seconds:g} s x {L} tok, B={B}: warm-up {w} {time.perf_counter() - t0:.2f} s",
+                  file=sys.stderr, flush=True)
         dts = []
         for s in range(max(3, args.cpu_steps)):
             t0 = time.perf_counter()
@@ -184,6 +213,11 @@ def cpu_baseline(args):
     B = args.cpu_batch
     dt_c2 = timed(B, args.seconds, args.tokens)
     dt_c1 = timed(B, 2.0, 16) if not args.eval else None
+    dt_share = None
+    if share != threads:
+        torch.set_num_threads(share)
+        dt_share = timed(B, args.seconds, args.tokens)
+        torch.set_num_threads(threads)
     what = "forward-only evaluation step (numpy fbank + forward + loss, no_grad)" if args.eval else \
         "full train step incl. numpy fbank + clip + two-group AdamW"
     out = {"value": round(B / dt_c2, 4), "unit": "audio-text pairs/s", "cores": threads, "kind": "port",
@@ -191,7 +225,12 @@ def cpu_baseline(args):
            "sample": f"oracle/ (CPU fp32 torch restatement, pinned to the reference by tests/golden) {what}; "
                      f"{args.seconds:g} s clips + {args.tokens}-token transcripts, {args.unfreeze} unfrozen layers, "
                      f"batch {B}; 2 warm-up steps, median of {max(3, args.cpu_steps)} timed steps = {dt_c2:.2f} s/step; "
-                     f"threads = the job's CPU share (min(affinity, OMP_NUM_THREADS))"}
+                     f"threads = every host core this job may use: min(len(os.sched_getaffinity(0)) = {cores}, the "
+                     f"cgroup CPU quota, OMP_NUM_THREADS) = {threads} (BASELINE.md §3)"}
+    if dt_share is not None:
+        out["job_share"] = {"value": round(B / dt_share, 4), "unit": "audio-text pairs/s", "cores": share,
+                            "sample": f"the same c2 step at the job's CPU share (min(affinity, OMP_NUM_THREADS) = "
+                                      f"{share} threads), {dt_share:.2f} s/step (median)"}
     if dt_c1 is not None:
         out["c1"] = {"value": round(B / dt_c1, 4), "unit": "audio-text pairs/s",
                      "sample": f"c1 shapes: 2 s clips + 16-token transcripts, batch {B}, {dt_c1:.2f} s/step (median)"}

@@ -244,8 +244,9 @@ int ste_glu_dwconv_bwd(const void* pre, const float* w, const void* dout, void* 
  * (tf:models/seamless_m4t/feature_extraction_seamless_m4t.py:112-138,140-301,
  * tf:audio_utils.py:809-1017) fused with ref:training/trainer_unfreeze.py:880-921
  * (custom_collate_fn padding).  wav fp32 [B, ld_wav]; lengths int32 [B].
- * feats fp32 [B, Tmax, 160]; mask int64 [B, Tmax]; work fp32 >= 2048 + B*Fmax*80 + B*160
- * with Fmax = 2*Tmax (constant tables + log-mel + per-clip CMVN statistics).  mask_mode 0: collate semantics (1 for t < T_b);
+ * feats fp32 [B, Tmax, 160]; mask int64 [B, Tmax]; work fp32 >= B*Fmax*80 + B*160 with
+ * Fmax = 2*Tmax (log-mel + per-clip CMVN statistics; the constant tables are compile-time data,
+ * so the call keeps no device state and is re-entrant and graph-capturable).  mask_mode 0: collate semantics (1 for t < T_b);
  * mask_mode 1: extractor semantics (0 for a padded odd frame).
  */
 int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* lengths, int B, int Tmax, float pad_value,

@@ -26,63 +26,16 @@ namespace {
 constexpr int FRAME = 400, HOP = 160, NFFT = 512, NBIN = 257, NMEL = 80;
 constexpr int MAXNZ = 640;  // non-zero filter taps (501 for these parameters)
 
-__device__ double hz_to_mel(double f) { return 1127.0 * log(1.0 + f / 700.0); }
-
-// Constant tables (built once per call by one block, read by every frame block):
+// Constant tables, compile-time data (fbank_tables.h, made by gen_fbank_tables.py from the
+// extractor's float64 formulas, rounded to float32 once), read by every frame block:
 //   [0, 512)   twiddles e^{-2πik/512} (float2 x 256)     [512, 912)  povey window
 //   [912, 992) mel start bin  [992, 1072) mel length  [1072, 1152) mel offset (ints)
-//   [1152, 1152+MAXNZ) mel weights (kaldi scale, triangles in mel space, fp64 -> fp32)
+//   [1152, 1152+MAXNZ) mel weights (kaldi scale, triangles in mel space)
+// No device state is built at run time: ste_fbank is re-entrant and graph-capturable.
 constexpr int T_TW = 0, T_WIN = 512, T_MSTART = 912, T_MLEN = 992, T_MOFF = 1072, T_MW = 1152;
-constexpr int TABLE_FLOATS = 2048;
-
-__global__ __launch_bounds__(256) void fbank_tables_kernel(float* __restrict__ tab) {
-  __shared__ double fk[NBIN];
-  __shared__ int slen[NMEL], soff[NMEL];
-  const int tid = threadIdx.x;
-  for (int k = tid; k < NFFT / 2; k += 256) {
-    double s, c;
-    sincos(-2.0 * M_PI * (double)k / (double)NFFT, &s, &c);
-    tab[T_TW + 2 * k] = (float)c;
-    tab[T_TW + 2 * k + 1] = (float)s;
-  }
-  for (int n = tid; n < FRAME; n += 256) {
-    const double hann = 0.5 - 0.5 * cos(2.0 * M_PI * (double)n / (double)(FRAME - 1));
-    tab[T_WIN + n] = (float)pow(hann, 0.85);
-  }
-  for (int k = tid; k < NBIN; k += 256) fk[k] = hz_to_mel(31.25 * k);
-  __syncthreads();
-  const double mel_lo = hz_to_mel(20.0), mel_hi = hz_to_mel(8000.0);
-  int start = 0, len = 0;
-  double f0 = 0, f1 = 0, f2 = 0;
-  if (tid < NMEL) {
-    f0 = mel_lo + (mel_hi - mel_lo) * tid / (NMEL + 1);
-    f1 = mel_lo + (mel_hi - mel_lo) * (tid + 1) / (NMEL + 1);
-    f2 = mel_lo + (mel_hi - mel_lo) * (tid + 2) / (NMEL + 1);
-    start = -1;
-    for (int k = 0; k < NBIN; ++k) {
-      const double wv = fmax(0.0, fmin((fk[k] - f0) / (f1 - f0), (f2 - fk[k]) / (f2 - f1)));
-      if (wv > 0.0) { if (start < 0) start = k; ++len; }
-    }
-    if (start < 0) start = 0;
-    slen[tid] = len;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int off = 0;
-    for (int m = 0; m < NMEL; ++m) { soff[m] = off; off += slen[m]; }
-  }
-  __syncthreads();
-  if (tid < NMEL) {
-    int* ti = reinterpret_cast<int*>(tab);
-    ti[T_MSTART + tid] = start;
-    ti[T_MLEN + tid] = len;
-    ti[T_MOFF + tid] = soff[tid];
-    for (int i = 0; i < len && soff[tid] + i < MAXNZ; ++i) {
-      const int k = start + i;
-      tab[T_MW + soff[tid] + i] = (float)fmax(0.0, fmin((fk[k] - f0) / (f1 - f0), (f2 - fk[k]) / (f2 - f1)));
-    }
-  }
-}
+}  // namespace
+#include "fbank_tables.h"
+namespace {
 
 constexpr int FRAMES_PER_WAVE = 4;
 constexpr int XPAD = NFFT + NFFT / 8;   // exchange buffer: one float2 of padding per 8
@@ -121,7 +74,8 @@ STE_DEV void dft8(float2 (&v)[8]) {
 // per frame and half of the kernel's time.)
 __global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restrict__ wav, int64_t ld_wav,
                                                          const int32_t* __restrict__ lengths, int Fmax,
-                                                         const float* __restrict__ tab, float* __restrict__ work) {
+                                                         float* __restrict__ work) {
+  const float* tab = reinterpret_cast<const float*>(g_fbank_tab_bits);
   __shared__ float2 sbuf[4][XPAD];
   __shared__ float2 stw[NFFT / 2];
   __shared__ float swin[FRAME];
@@ -314,25 +268,6 @@ __global__ __launch_bounds__(256) void fbank_norm_kernel(const int32_t* __restri
   }
 }
 
-// The constant tables (twiddles, window, mel filters) depend on nothing but the extractor's
-// parameters: built once per device into module memory by a single-block launch, then shared by
-// every call (the build runs serial fp64 loops: ~40 us that used to be paid per batch).
-__device__ float g_fbank_tab[TABLE_FLOATS];
-
-const float* fbank_tables(hipStream_t s) {
-  static const float* tab[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!tab[dev]) {
-    void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_fbank_tab)) != hipSuccess) return nullptr;
-    hipLaunchKernelGGL(fbank_tables_kernel, dim3(1), dim3(256), 0, s, (float*)p);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return nullptr;
-    tab[dev] = (const float*)p;
-  }
-  return tab[dev];
-}
-
 }  // namespace
 
 extern "C" int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* lengths, int B, int Tmax, float pad_value,
@@ -340,14 +275,12 @@ extern "C" int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* length
   if (B <= 0 || Tmax <= 0 || !wav || !lengths || !feats || !mask || !work) return STE_ERR_ARG;
   const int Fmax = 2 * Tmax;
   hipStream_t s = (hipStream_t)stream;
-  const float* tab = fbank_tables(s);
-  if (!tab) return STE_ERR_ARG;
-  float* logmel = work + TABLE_FLOATS;
+  float* logmel = work;
   const int fpb = 4 * FRAMES_PER_WAVE;
   hipLaunchKernelGGL(fbank_logmel_kernel, dim3((Fmax + fpb - 1) / fpb, B), dim3(256), 0, s, wav, ld_wav, lengths,
-                     Fmax, tab, logmel);
+                     Fmax, logmel);
   STE_CHECK_LAUNCH();
-  float* stats = work + TABLE_FLOATS + (int64_t)B * Fmax * NMEL;
+  float* stats = work + (int64_t)B * Fmax * NMEL;
   hipLaunchKernelGGL(fbank_stats_kernel, dim3(B), dim3(STATS_NT), 0, s, lengths, Fmax, logmel, stats);
   STE_CHECK_LAUNCH();
   hipLaunchKernelGGL(fbank_norm_kernel, dim3((Tmax + NORM_ROWS - 1) / NORM_ROWS, B), dim3(256), 0, s, lengths, Fmax,

@@ -382,7 +382,7 @@ def fbank(wav, lengths, Tmax, *, pad_value=1.0, mask_mode=0, feats=None, mask=No
     if mask is None:
         mask = torch.empty((B, Tmax), device=dev, dtype=torch.int64)
     if work is None:
-        work = torch.empty(2048 + B * 2 * Tmax * 80 + B * 160, device=dev, dtype=F32)
+        work = torch.empty(B * 2 * Tmax * 80 + B * 160, device=dev, dtype=F32)
     # algorithmic bytes: the waveforms once, the stacked features and the mask
     nbytes = 4 * B * wav.shape[1] + _nb(feats) + _nb(mask)
     _traced("fbank", nbytes, lambda: call("ste_fbank", ptr(wav), wav.stride(0), ptr(lengths), B, Tmax,

@@ -597,6 +597,52 @@ def test_fbank_matches_golden(ops):
 FBANK_ATOL = 5e-4   # half the SURVEY §8(d) fp32 bound (1e-3) on CMVN-normalised features; measured <= 3.8e-4
 
 
+_FBANK_THREADS = r"""
+import sys, threading, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from speech_transcript_embeddings_amd import ops
+z = np.load(sys.argv[2])
+cases = list(z["cases"])
+waves = [z[f"{c}_wave"] for c in cases]
+N = max(w.size for w in waves)
+wav = torch.zeros(len(waves), N, device="cuda")
+for i, w in enumerate(waves):
+    wav[i, : w.size] = torch.from_numpy(w)
+lens = torch.tensor([w.size for w in waves], dtype=torch.int32, device="cuda")
+Tmax = z["batch_feats"].shape[1]
+out, barrier = {}, threading.Barrier(2)
+
+def run(k):
+    s = torch.cuda.Stream()
+    barrier.wait()                      # both threads enter the library's first call together
+    with torch.cuda.stream(s):
+        f, m = ops.fbank(wav, lens, Tmax, pad_value=1.0, mask_mode=0)
+    s.synchronize()
+    out[k] = (f.cpu().numpy(), m.cpu().numpy())
+
+ts = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+[t.start() for t in ts]
+[t.join() for t in ts]
+for k in range(2):
+    np.testing.assert_array_equal(out[k][1], z["batch_mask"])
+    np.testing.assert_allclose(out[k][0], z["batch_feats"], atol=float(sys.argv[3]), rtol=0)
+assert np.array_equal(out[0][0], out[1][0])
+print("fbank-threads-ok")
+"""
+
+
+def test_fbank_first_calls_concurrent_on_two_streams():
+    """ste_fbank keeps no lazily built device state.  In a fresh process (fresh device
+    context), two threads make the library's first fbank calls at the same moment on two streams;
+    both match the reference's golden features."""
+    import subprocess
+    import sys
+    from conftest import GOLDEN, ROOT
+    r = subprocess.run([sys.executable, "-c", _FBANK_THREADS, str(ROOT), str(GOLDEN / "fbank_golden.npz"),
+                        str(FBANK_ATOL)], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "fbank-threads-ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_fbank_config_size_clips_match_reference_extractor(ops):
     """BASELINE clip lengths and edge paths against the reference extractor
     (tests/golden/fbank_golden_long.npz, made by make_golden.py --fbank-long): a c2 10 s clip, a
