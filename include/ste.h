@@ -219,6 +219,12 @@ typedef struct {
    * With near-uniform attention O ≈ mean(V) and dS = P(dP - delta) is a small difference of
    * large terms, so a delta from the bf16-rounded O alone is the dominant error of dQ/dK/dE. */
   void* o_lo; int64_t ldolo;
+  /* a query row whose every key is masked: 0 = uniform weights over the sequence (an additive
+   * finfo.min mask, the eager attention of w2v-bert, tf:…wav2vec2_bert…:306-327); 1 = zero weights,
+   * zero output and zero gradients (torch SDPA's fully-masked-row rule, which the XLM-R SDPA path
+   * of the reference's transformers takes, tf:…xlm_roberta…:186-250).  The forward saves the row's
+   * LSE as -inf (uniform) / +inf (zero) for the backward. */
+  int zero_masked_rows;
 } ste_attn_args;
 int ste_attention_fwd(const ste_attn_args* a, void* stream);
 /* fp32 forward of the text encoder's attention (the precise text forward, see ste_split_bf16):

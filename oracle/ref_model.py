@@ -156,9 +156,11 @@ def text_encoder(p, ids, mask, cfg: TextCfg, prefix="text_encoder."):
     B, L = ids.shape
     nz = (ids != cfg.pad_id).int()
     pos_ids = (torch.cumsum(nz, dim=1) * nz).long() + cfg.pad_id
-    e = (p[prefix + "embeddings.word_embeddings.weight"][ids]
+    # nn.Embedding(padding_idx=pad): the pad row receives no gradient (word ids == pad, and the
+    # position ids of pad tokens == pad, xlm:142-155)
+    e = (F.embedding(ids, p[prefix + "embeddings.word_embeddings.weight"], padding_idx=cfg.pad_id)
          + p[prefix + "embeddings.token_type_embeddings.weight"][0]
-         + p[prefix + "embeddings.position_embeddings.weight"][pos_ids])
+         + F.embedding(pos_ids, p[prefix + "embeddings.position_embeddings.weight"], padding_idx=cfg.pad_id))
     x = _ln(p, prefix + "embeddings.LayerNorm", e, cfg.eps)
     add_mask = None
     if mask is not None:
@@ -172,7 +174,13 @@ def text_encoder(p, ids, mask, cfg: TextCfg, prefix="text_encoder."):
         s = q @ k.transpose(-2, -1) / math.sqrt(d)
         if add_mask is not None:
             s = s + add_mask
-        o = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B, L, cfg.hidden)
+        pr = torch.softmax(s, -1)
+        if mask is not None:
+            # the reference's XLM-R attention is SDPA (transformers 5.15 in this container), whose
+            # boolean mask gives a query with every key masked zero weights (torch's safe softmax),
+            # not the uniform weights of an additive finfo.min mask (pinned by model_golden_masked)
+            pr = pr * (mask.sum(1) > 0).to(pr.dtype)[:, None, None, None]
+        o = (pr @ v).transpose(1, 2).reshape(B, L, cfg.hidden)
         x = _ln(p, pre + "attention.output.LayerNorm", _lin(p, pre + "attention.output.dense", o) + x, cfg.eps)
         inter = F.gelu(_lin(p, pre + "intermediate.dense", x))
         x = _ln(p, pre + "output.LayerNorm", _lin(p, pre + "output.dense", inter) + x, cfg.eps)

@@ -1,0 +1,45 @@
+"""Time one libste.so kernel configuration in isolation with HIP events (GPU, scratch probe).
+    python profiles/kernel_timer.py text_attn_f32      # the precise text forward's attention at c2
+"""
+import sys
+import os
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from speech_transcript_embeddings_amd import ops  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+def text_attn_f32():
+    B, T, H, D = 128, 64, 12, 64
+    W = H * D
+    qkv = torch.randn(B * T, 3 * W, device="cuda")
+    mask = torch.ones(B * T, dtype=torch.int32, device="cuda")
+    os_ = torch.empty(B * T, 2 * W, device="cuda", dtype=torch.bfloat16)
+    lse = torch.empty(B * H * T, device="cuda")
+    for p in (0.0, 0.1):
+        us = timeit(lambda: ops.attention_fwd_f32(qkv[:, :W], qkv[:, W:2 * W], qkv[:, 2 * W:], B=B, T=T, H=H, o32=None,
+                                                  lse=lse, o=os_[:, :W], o_lo=os_[:, W:], key_mask=mask, drop_p=p,
+                                                  seed=1))
+        qb = qkv.bfloat16()
+        o = torch.empty(B * T, W, device="cuda", dtype=torch.bfloat16)
+        us_b = timeit(lambda: ops.attention_fwd(qb[:, :W], qb[:, W:2 * W], qb[:, 2 * W:], B=B, T=T, H=H, o=o, lse=lse,
+                                                key_mask=mask, drop_p=p, seed=1, o_lo=os_[:, W:]))
+        print(f"text attention fwd B={B} T={T} H={H} drop={p}: fp32 {us:.1f} us, bf16 kernel {us_b:.1f} us")
+
+
+if __name__ == "__main__":
+    globals()[sys.argv[1]]()

@@ -24,7 +24,7 @@ def main():
     from oracle import det_init, ref_model as R
     from speech_transcript_embeddings_amd.model import AlignmentAwareInfoNCE, EnhancedAudioTextModel
     report = {}
-    for tag in ("noalign", "align", "nopool"):
+    for tag in ("noalign", "align", "nopool", "masked"):
         meta, z = load(tag)
         model = mini_model(meta)
         model.eval()

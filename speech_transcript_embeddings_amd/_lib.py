@@ -105,6 +105,7 @@ class AttnArgs(C.Structure):
         ("dE", c_void_p),
         ("gwork", c_void_p),
         ("o_lo", c_void_p), ("ldolo", c_int64),
+        ("zero_masked_rows", c_int),
     ]
 
 

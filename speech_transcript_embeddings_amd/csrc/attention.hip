@@ -282,7 +282,10 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(ste_attn_args a) {
     __syncthreads();
   }
   if (myq < T) {
-    const float inv_l = 1.0f / l;
+    // fully masked row under SDPA semantics (zero_masked_rows): zero output, LSE +inf (zero p and
+    // zero gradients in the backward)
+    const bool zrow = a.zero_masked_rows && m == NEG_MASK;
+    const float inv_l = zrow ? 0.f : 1.0f / l;
     bf16* O = (bf16*)a.o + (int64_t)(bT + myq) * a.ldo + h * HD;
     if (a.o_lo) {
       bf16* Ol = (bf16*)a.o_lo + (int64_t)(bT + myq) * a.ldolo + h * HD;
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(ste_attn_args a) {
     // an all-masked row (every score at the finfo.min fill: uniform weights) saves -inf, as the
     // relative-key kernels do; the backward then uses p = 1/T there (m + log l would round to
     // the fill itself and give p = 1)
-    if (g == 0) a.lse[(int64_t)(b * H + h) * T + myq] = m == NEG_MASK ? -INFINITY : m + logf(l);
+    if (g == 0) a.lse[(int64_t)(b * H + h) * T + myq] = m == NEG_MASK ? (zrow ? INFINITY : -INFINITY) : m + logf(l);
   }
 }
 

@@ -11,16 +11,19 @@
 // convention as attention.hip (natural log, masked keys at the finfo.min score, dropout index
 // ((b·H + h)·T + q)·T + key), so ste_attention_bwd runs on them unchanged.
 //
-// One block per (sample, head, 64-query tile), 4 waves x 16 query rows.  Keys in chunks of 64
-// staged in LDS (fp32 K at a 65-float row stride: lane j reads row j, conflict-free), one key
-// per lane; the online softmax's running max / sum are wave-uniform per row; O[row][c] lives
-// on lane c.  VALU fp32 throughout (T is short: 16-128 tokens).
+// One block per (sample, head, 64-query tile), 4 waves x 16 query rows, keys in chunks of 64.
+// Register-blocked VALU fp32 with the softmax row lane-local: lane (r, g) = (l & 15, l >> 4)
+// owns query row r and the keys 4kk + g (kk < 16) of a chunk, so a
+// row's max / sum is an in-lane reduction plus two cross-lane steps (not six); K rows are read
+// from LDS as b128 at a 68-float stride (the 4 simultaneous rows 4kk..4kk+3 hit disjoint bank
+// groups; so do the 16 query rows).  P goes to LDS row-major and lane (r, g) accumulates O[r][16g..16g+15] from
+// broadcast V reads.  1,024 + 1,024 FMAs per lane per 64-key chunk.
 #include "common.h"
 #include "../../include/ste.h"
 
 namespace {
 
-constexpr int HD = 64, QT = 64, KC = 64, NT = 256, KLD = HD + 1;
+constexpr int HD = 64, QT = 64, KC = 64, NT = 256;
 constexpr float NEG_MASK = -3.4028234663852886e38f;   // finfo(float32).min, as attention.hip
 
 STE_DEV float key_flag32(const int32_t* mask, int bT, int key, int T) {
@@ -28,93 +31,118 @@ STE_DEV float key_flag32(const int32_t* mask, int bT, int key, int T) {
   return (mask == nullptr || mask[bT + key] != 0) ? 1.f : 0.f;
 }
 
+constexpr int KLD = HD + 4;   // K / V row stride in LDS (floats)
+constexpr int PLD = KC + 1;   // P row stride
+
 template <bool DROP>
 __global__ __launch_bounds__(NT) void attn_f32_fwd_kernel(ste_attn_args a, float* o32, int64_t ldo32) {
-  __shared__ float sK[KC * KLD];
-  __shared__ float sV[KC * HD];
-  __shared__ float sQ[QT * HD];
-  __shared__ float sP[NT / 64][KC];
+  __shared__ __attribute__((aligned(16))) float sQ[QT * KLD];
+  __shared__ __attribute__((aligned(16))) float sK[KC * KLD];
+  __shared__ __attribute__((aligned(16))) float sV[KC * KLD];
+  __shared__ float sP[NT / 64][16 * PLD];
   __shared__ float sF[KC];
   const int T = a.T, H = a.H;
   const int ntile = (T + QT - 1) / QT;
   const int tile = blockIdx.x % ntile, bh = blockIdx.x / ntile, h = bh % H, b = bh / H;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int bT = b * T, q0 = tile * QT;
-  const float* Q = (const float*)a.q + h * HD;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int bT = b * T, q0 = tile * QT, q = q0 + w * 16 + r;
   const float* K = (const float*)a.k + h * HD;
   const float* V = (const float*)a.v + h * HD;
   for (int i = tid; i < QT * HD / 4; i += NT) {
-    const int r = i >> 4, c = (i & 15) * 4;
-    const f32x4 v = q0 + r < T ? *reinterpret_cast<const f32x4*>(Q + (int64_t)(bT + q0 + r) * a.ldq + c)
-                               : f32x4{0.f, 0.f, 0.f, 0.f};
-    *reinterpret_cast<f32x4*>(sQ + r * HD + c) = v;
+    const int qr = i >> 4, c = (i & 15) * 4;
+    *reinterpret_cast<f32x4*>(sQ + qr * KLD + c) =
+        q0 + qr < T ? *reinterpret_cast<const f32x4*>((const float*)a.q + h * HD + (int64_t)(bT + q0 + qr) * a.ldq + c)
+                    : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  const float* qrow = sQ + (w * 16 + r) * KLD;
   const uint32_t thresh = (uint32_t)(a.drop_p * 4294967296.0);
   const float inv_keep = DROP ? 1.0f / (1.0f - a.drop_p) : 1.0f;
-  float m[16], l[16], o[16];
+  const uint64_t drow = ((uint64_t)(b * H + h) * T + q) * (uint64_t)T;
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[4];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    m[r] = -INFINITY;
-    l[r] = 0.f;
-    o[r] = 0.f;
-  }
+  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float* sp = sP[w] + r * PLD;
   for (int k0 = 0; k0 < T; k0 += KC) {
-    __syncthreads();  // the previous chunk is consumed (first pass: sQ is staged)
+    __syncthreads();   // the previous chunk is consumed
     for (int i = tid; i < KC * HD / 4; i += NT) {
-      const int r = i >> 4, c = (i & 15) * 4, key = k0 + r;
+      const int kr = i >> 4, c = (i & 15) * 4, key = k0 + kr;
       f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
       if (key < T) {
         kv = *reinterpret_cast<const f32x4*>(K + (int64_t)(bT + key) * a.ldk + c);
         vv = *reinterpret_cast<const f32x4*>(V + (int64_t)(bT + key) * a.ldv + c);
       }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) sK[r * KLD + c + e] = kv[e];
-      *reinterpret_cast<f32x4*>(sV + r * HD + c) = vv;
+      *reinterpret_cast<f32x4*>(sK + kr * KLD + c) = kv;
+      *reinterpret_cast<f32x4*>(sV + kr * KLD + c) = vv;
     }
     if (tid < KC) sF[tid] = key_flag32(a.key_mask, bT, k0 + tid, T);
     __syncthreads();
-    const int nk = min(KC, T - k0);
-    const float f = sF[lane];
+    float s[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int q = q0 + w * 16 + r;
-      const float* qrow = sQ + (w * 16 + r) * HD;
-      float s = 0.f;
-#pragma unroll 16
-      for (int d = 0; d < HD; ++d) s = fmaf(qrow[d], sK[lane * KLD + d], s);
-      float v = s * a.scale;
+    for (int kk = 0; kk < 16; ++kk) s[kk] = 0.f;
+#pragma unroll 2
+    for (int d = 0; d < HD / 4; ++d) {
+      const f32x4 qv = *reinterpret_cast<const f32x4*>(qrow + 4 * d);   // 4 lanes per row: broadcast
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const f32x4 kv = *reinterpret_cast<const f32x4*>(sK + (4 * kk + g) * KLD + 4 * d);
+        s[kk] = fmaf(qv[0], kv[0], fmaf(qv[1], kv[1], fmaf(qv[2], kv[2], fmaf(qv[3], kv[3], s[kk]))));
+      }
+    }
+    float cm = -INFINITY;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      const float f = sF[4 * kk + g];
+      float v = s[kk] * a.scale;
       v = f > 0.5f ? v : (f < -0.5f ? -INFINITY : NEG_MASK);
-      const float mn = fmaxf(m[r], wave_max(v));
-      const float alpha = mn == -INFINITY ? 1.f : __expf(m[r] - mn);
-      float p = mn == -INFINITY ? 0.f : __expf(v - mn);
-      l[r] = l[r] * alpha + wave_sum(p);
-      m[r] = mn;
-      if (DROP) p *= drop_scale(a.seed, ((uint64_t)(b * H + h) * T + q) * (uint64_t)T + (uint64_t)(k0 + lane), thresh,
-                                inv_keep);
-      sP[w][lane] = p;
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
-      float acc = o[r] * alpha;
-      for (int j = 0; j < nk; ++j) acc = fmaf(sP[w][j], sV[j * HD + lane], acc);
-      o[r] = acc;
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
+      s[kk] = v;
+      cm = fmaxf(cm, v);
+    }
+    cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+    cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+    const float mn = fmaxf(m, cm);
+    const float alpha = mn == -INFINITY ? 1.f : __expf(m - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float p = mn == -INFINITY ? 0.f : __expf(s[kk] - mn);
+      ps += p;
+      if (DROP) p *= drop_scale(a.seed, drow + (uint64_t)(k0 + 4 * kk + g), thresh, inv_keep);
+      sp[4 * kk + g] = p;
+    }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] *= alpha;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const int nk = min(KC, T - k0);
+    for (int j = 0; j < nk; ++j) {
+      const float p = sp[j];
+      const float* vr = sV + j * KLD + 16 * g;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] += p * *reinterpret_cast<const f32x4*>(vr + 4 * i);
     }
   }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int q = q0 + w * 16 + r;
-    if (q >= T) continue;
-    const float ov = o[r] / l[r];
+  if (q < T) {
+    const bool zrow = a.zero_masked_rows && m == NEG_MASK;   // SDPA: a fully masked row -> 0
+    const float inv_l = zrow ? 0.f : 1.0f / l;
     const int64_t row = bT + q;
-    if (o32) o32[row * ldo32 + h * HD + lane] = ov;
-    if (a.o) {
-      const bf16 hi = (bf16)ov;
-      ((bf16*)a.o)[row * a.ldo + h * HD + lane] = hi;
-      if (a.o_lo) ((bf16*)a.o_lo)[row * a.ldolo + h * HD + lane] = (bf16)(ov - (float)hi);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 ov = o[i] * inv_l;
+      const int col = h * HD + 16 * g + 4 * i;
+      if (o32) *reinterpret_cast<f32x4*>(o32 + row * ldo32 + col) = ov;
+      if (a.o) {
+        if (a.o_lo) store_bf16x4_split((bf16*)a.o + row * a.ldo + col, (bf16*)a.o_lo + row * a.ldolo + col, ov);
+        else store_bf16x4((bf16*)a.o + row * a.ldo + col, ov);
+      }
     }
-    // all keys masked (uniform weights): -inf, the convention the backward kernels read as p = 1/T
-    if (lane == 0) a.lse[(int64_t)(b * H + h) * T + q] = m[r] == NEG_MASK ? -INFINITY : m[r] + logf(l[r]);
+    // all keys masked: -inf (uniform weights, the backward reads p = 1/T) or, under SDPA
+    // semantics, +inf (zero weights: p = exp(v - inf) = 0 in the backward)
+    if (g == 0) a.lse[(int64_t)(b * H + h) * T + q] = m == NEG_MASK ? (zrow ? INFINITY : -INFINITY) : m + logf(l);
   }
 }
 
@@ -125,7 +153,7 @@ extern "C" int ste_attention_fwd_f32(const ste_attn_args* args, float* o32, int6
   const ste_attn_args& a = *args;
   if (!a.q || !a.k || !a.v || !a.lse || a.rel_E) return STE_ERR_ARG;
   if (a.B <= 0 || a.T <= 0 || a.H <= 0) return STE_ERR_SHAPE;
-  if ((a.ldq & 3) || (a.ldk & 3) || (a.ldv & 3) || (o32 && ldo32 < (int64_t)a.H * 64) ||
+  if ((a.ldq & 3) || (a.ldk & 3) || (a.ldv & 3) || (o32 && (ldo32 < (int64_t)a.H * 64 || (ldo32 & 3))) ||
       (((uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v) & 15))
     return STE_ERR_SHAPE;
   const int ntile = (a.T + QT - 1) / QT;

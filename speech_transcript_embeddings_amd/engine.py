@@ -501,7 +501,8 @@ class Engine:
         """One post-LN transformer layer: XLM-R (tf:…xlm_roberta…:186-398) and wav2vec2
         (tf:models/wav2vec2/modeling_wav2vec2.py:466-608) share the math
         LN(x + drop(O(attn(QKV x)))) -> LN(x1 + drop(W2·drop_act(gelu(W1 x1)))); `nm` maps the
-        parameter names (XLMR_NAMES / W2V2_NAMES)."""
+        parameter names (XLMR_NAMES / W2V2_NAMES).  Both run on SDPA in the reference's
+        transformers, so a query whose keys are all masked gets zero attention (zero_masked_rows)."""
         s = self.s
         pre = nm["layer"].format(i=i)
         M, D, F_ = x.shape[0], c.hidden_size, c.intermediate_size
@@ -516,7 +517,7 @@ class Engine:
         lse = self._e(nb * H * L)
         ops.attention_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B=nb, T=L, H=H, o=o, lse=lse,
                           key_mask=mask32, scale=1.0 / math.sqrt(D // H), drop_p=ap, seed=_site_seed(seed, 1),
-                          o_lo=o_lo)
+                          o_lo=o_lo, zero_masked_rows=True)
         y1 = ops.linear(o, s.w(pre + nm["o"] + ".weight"), s.p(pre + nm["o"] + ".bias"),
                         residual=x, drop_p=hp, seed=_site_seed(seed, 2))
         x1 = self._e(M, D)
@@ -559,7 +560,7 @@ class Engine:
         lse = self._e(nb * H * L)
         ops.attention_fwd_f32(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B=nb, T=L, H=H, o32=None, lse=lse,
                               o=os_[:, :D], o_lo=os_[:, D:], key_mask=mask32, scale=1.0 / math.sqrt(D // H),
-                              drop_p=ap, seed=_site_seed(seed, 1))
+                              drop_p=ap, seed=_site_seed(seed, 1), zero_masked_rows=True)
         del qkv
         y1 = ops.linear(os_, s.w2(pre + nm["o"] + ".weight"), s.p(pre + nm["o"] + ".bias"), residual=x, drop_p=hp,
                         seed=_site_seed(seed, 2))

@@ -281,7 +281,7 @@ def layernorm_bwd_pair(first: dict, second: dict):
 
 # -------------------------------------------------------------- attention
 def attention_fwd(q, k, v, *, B, T, H, o, lse, key_mask=None, rel_E=None, rel_left=64, rel_right=8,
-                  scale=0.125, drop_p=0.0, seed=0, o_lo=None):
+                  scale=0.125, drop_p=0.0, seed=0, o_lo=None, zero_masked_rows=False):
     """q/k/v/o: bf16 [B*T, *] views (row-major, head h at columns h*64..), lse fp32 [B*H*T].
     o_lo (optional, bf16 like o): receives bf16(O - bf16(O)) for the backward's delta."""
     a = AttnArgs()
@@ -296,12 +296,13 @@ def attention_fwd(q, k, v, *, B, T, H, o, lse, key_mask=None, rel_E=None, rel_le
     a.scale, a.drop_p, a.seed = float(scale), float(drop_p), int(seed) & (2**64 - 1)
     if o_lo is not None:
         a.o_lo, a.ldolo = ptr(o_lo), _ld(o_lo)
+    a.zero_masked_rows = int(bool(zero_masked_rows))
     call("ste_attention_fwd", C.byref(a), _s())
     return a
 
 
 def attention_fwd_f32(q, k, v, *, B, T, H, o32, lse, o=None, o_lo=None, key_mask=None, scale=0.125, drop_p=0.0,
-                      seed=0):
+                      seed=0, zero_masked_rows=False):
     """fp32 q/k/v [B*T, *] views -> O fp32 (o32) + optional bf16 hi / lo copies for the bf16
     backward, lse fp32 [B*H*T] (ste_attention_fwd_f32: the text encoder's precise forward)."""
     assert q.dtype == F32 and k.dtype == F32 and v.dtype == F32 and (o32 is None or o32.dtype == F32)
@@ -317,6 +318,7 @@ def attention_fwd_f32(q, k, v, *, B, T, H, o32, lse, o=None, o_lo=None, key_mask
     a.lse = ptr(lse)
     a.key_mask = ptr(key_mask)
     a.scale, a.drop_p, a.seed = float(scale), float(drop_p), int(seed) & (2**64 - 1)
+    a.zero_masked_rows = int(bool(zero_masked_rows))
     call("ste_attention_fwd_f32", C.byref(a), ptr(o32), 0 if o32 is None else _ld(o32), _s())
 
 

@@ -134,11 +134,11 @@ def fbank_long_fixture(T):
     print("fbank_golden_long.npz", {k: v.shape for k, v in out.items()})
 
 
-def synth_batch(T, B=2, L=12, vocab=1000):
+def synth_batch(T, B=2, L=12, vocab=1000, masked=False):
     from transformers import SeamlessM4TFeatureExtractor
     fe = SeamlessM4TFeatureExtractor(feature_size=80, num_mel_bins=80, padding_value=1.0, sampling_rate=16000,
                                      stride=2)
-    lens = [16000, 12800][:B]
+    lens = [16000, 12800, 9600][:B]
     rng = np.random.default_rng(77)
     items = []
     for i in range(B):
@@ -157,10 +157,15 @@ def synth_batch(T, B=2, L=12, vocab=1000):
             "input_ids_pos": torch.from_numpy(ids), "attention_mask_pos": torch.from_numpy(mask),
             "input_ids_neg": torch.from_numpy(neg), "attention_mask_neg": torch.from_numpy(mask.copy()),
             "input_values": r["input_features"][0], "attention_mask_audio": r["attention_mask"][0]})
-    return T.custom_collate_fn(items)
+    batch = T.custom_collate_fn(items)
+    if masked:   # edge cases of the masks: sample 1's transcripts and sample 2's audio fully masked
+        batch["attention_mask_pos"][1] = 0
+        batch["attention_mask_neg"][1] = 0
+        batch["attention_mask_audio"][2] = 0
+    return batch
 
 
-def model_fixture(T, use_align: bool, attentive: bool = True):
+def model_fixture(T, use_align: bool, attentive: bool = True, masked: bool = False):
     T.AutoModel = make_automodel_shim(MINI)
     torch.manual_seed(0)
     model = T.EnhancedAudioTextModel(
@@ -173,7 +178,7 @@ def model_fixture(T, use_align: bool, attentive: bool = True):
     vals = det_init.state_dict_values([(n, t.shape) for n, t in sd.items() if t.is_floating_point()])
     model.load_state_dict({n: torch.from_numpy(v) for n, v in vals.items()}, strict=False)
     model.eval()
-    batch = synth_batch(T)
+    batch = synth_batch(T, B=3, masked=True) if masked else synth_batch(T)
     tpn, tnn, an = T.EnhancedAudioTextModel.compute_pos_neg_embeddings(model, batch)
     s_pos = (an * tpn).sum(1)
     s_neg = (an * tnn).sum(1)
@@ -223,7 +228,7 @@ def model_fixture(T, use_align: bool, attentive: bool = True):
            "with_grad": with_grad, "lr": lr, "warmup": 2, "total_steps": 10, "sched_step": 1,
            "param_count": sum(p.numel() for p in model.parameters()),
            "trainable_count": sum(p.numel() for p in model.parameters() if p.requires_grad)}
-    tag = ("align" if use_align else "noalign") if attentive else "nopool"
+    tag = "masked" if masked else ("align" if use_align else "noalign") if attentive else "nopool"
     np.savez_compressed(HERE / f"model_golden_{tag}.npz", **out)
     (HERE / f"model_golden_{tag}.json").write_text(json.dumps(cfg, indent=1))
     print(f"model_golden_{tag}.npz loss={loss.item():.6f} trainable={cfg['trainable_count']}")
@@ -258,10 +263,14 @@ if __name__ == "__main__":
     if "--fbank-long" in sys.argv:  # only the config-size fbank fixture
         fbank_long_fixture(T)
         sys.exit(0)
+    if "--masked" in sys.argv:      # only the all-masked-sample model fixture
+        model_fixture(T, use_align=False, masked=True)
+        sys.exit(0)
     fbank_fixture(T)
     fbank_long_fixture(T)
     model_fixture(T, use_align=False)
     model_fixture(T, use_align=True)
     model_fixture(T, use_align=False, attentive=False)  # CLS text / masked-mean audio (ref:578-580,621-636)
+    model_fixture(T, use_align=False, masked=True)      # fully masked transcripts / audio of one sample
     if "--counts" in sys.argv:
         param_count_fixture(T)

@@ -80,7 +80,7 @@ def _grad_errors(model, meta, batch_cpu):
     return sorted(out, reverse=True), lo.item()
 
 
-@pytest.mark.parametrize("tag", ["noalign", "align", "nopool"])
+@pytest.mark.parametrize("tag", ["noalign", "align", "nopool", "masked"])
 def test_backward_random_cotangents(tag):
     """Backward of the whole model for random output cotangents vs the oracle's autograd.
 
@@ -162,7 +162,7 @@ def test_backward_random_cotangents(tag):
     assert errs[len(errs) // 2][0] < 1e-2
 
 
-@pytest.mark.parametrize("tag", ["noalign", "align", "nopool"])
+@pytest.mark.parametrize("tag", ["noalign", "align", "nopool", "masked"])
 def test_forward_backward_matches_golden_and_oracle(tag):
     """The drop-in autograd path (compute_pos_neg_embeddings -> (aud*txt).sum(1) -> loss_fn ->
     loss.backward(), ref :1068-1094) against the reference's golden outputs and the oracle.

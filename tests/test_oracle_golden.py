@@ -73,7 +73,7 @@ def golden_batch(z):
     return {k: torch.from_numpy(z[k]) for k in keys}
 
 
-@pytest.mark.parametrize("tag", ["noalign", "align", "nopool"])
+@pytest.mark.parametrize("tag", ["noalign", "align", "nopool", "masked"])
 def test_param_tree_matches_reference(tag):
     meta, _ = _load(tag)
     cfg = R.mini_cfg(meta)
@@ -99,7 +99,7 @@ def test_full_size_param_counts_match_reference_logs():
         assert sorted(tr) == sorted(ref["trainable_names"])
 
 
-@pytest.mark.parametrize("tag", ["noalign", "align", "nopool"])
+@pytest.mark.parametrize("tag", ["noalign", "align", "nopool", "masked"])
 def test_model_oracle_matches_reference(tag):
     meta, z = _load(tag)
     cfg = R.mini_cfg(meta)
@@ -126,7 +126,7 @@ def test_model_oracle_matches_reference(tag):
         np.testing.assert_allclose(g[idx], z[f"gsamp::{n}"], atol=1e-6, rtol=1e-4, err_msg=n)
 
 
-@pytest.mark.parametrize("tag", ["noalign", "align", "nopool"])
+@pytest.mark.parametrize("tag", ["noalign", "align", "nopool", "masked"])
 def test_optimizer_oracle_matches_reference(tag):
     """clip_grad_norm_(1.0) + two-group AdamW at scheduler step 1 (ref:1108-1113, 1487-1541)."""
     meta, z = _load(tag)
