@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--heads", type=int, default=16)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-bwd", action="store_true")
+    ap.add_argument("--no-split", action="store_true", help="forward without the O_lo (hi + lo P) product")
     a = ap.parse_args()
     from speech_transcript_embeddings_amd import ops
     B, T, H = a.batch, a.frames, a.heads
@@ -49,7 +50,8 @@ def main():
     gwork = torch.empty(B * H * T * 80, device="cuda")
 
     def fwd():
-        ops.attention_fwd(q, k, v, B=B, T=T, H=H, o=o, lse=lse, key_mask=mask, rel_E=E, scale=0.125, o_lo=o_lo)
+        ops.attention_fwd(q, k, v, B=B, T=T, H=H, o=o, lse=lse, key_mask=mask, rel_E=E, scale=0.125,
+                          o_lo=None if a.no_split else o_lo)
 
     def bwd():
         ops.attention_bwd(q, k, v, o, lse, do, dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], B=B, T=T, H=H,

@@ -11,7 +11,7 @@ committed summaries under profiles/.
 
 gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half the bytes of wide
 coalesced reads -> x2; WRITE_SIZE is exact for 16-B stores; both counters are in KiB.  For traffic
-only the dispatches of the last step are used (from the last fbank_tables_kernel launch, the
+only the dispatches of the last step are used (from the last fbank_logmel_kernel launch, the
 first kernel of every step, to the end).
 """
 import csv
@@ -54,7 +54,7 @@ def counter(db, name):
         a[0] = k
         a[1] += float(v)
     out = sorted(agg.items())
-    start = max(i for i, (_, (k, _)) in enumerate(out) if "fbank_tables_kernel" in k)
+    start = max(i for i, (_, (k, _)) in enumerate(out) if "fbank_logmel_kernel" in k)
     return [(k, v) for _, (k, v) in out[start:]]
 
 

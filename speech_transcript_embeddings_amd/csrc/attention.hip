@@ -1119,6 +1119,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
   };
   float m[2] = {-INFINITY, -INFINITY};
   f32x4 o[2][4], lsum[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  float lp[2] = {0.f, 0.f};   // SPLIT: per-lane fp32 partial row sums of the exact p (reduced at the end)
   bf16x8 ones;
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
@@ -1158,7 +1159,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
       const int q0g = qw + 16 * gq, myq = q0g + li;
       const bool all_lo = (kb + TK - 1) - q0g <= -left;
       const bool all_hi = kb - (q0g + 15) >= right;
-      if (all_lo || all_hi) {
+      if (all_lo || all_hi || (STE_ABLATE & 512)) {
         const float bc = all_lo ? blo[gq] : bhi[gq];
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -1200,7 +1201,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
       if (__builtin_amdgcn_ballot_w64(tmax > m[gq] + THRESH) != 0ull) {
         const float mnew = fmaxf(m[gq], tmax);
         const float alpha = __builtin_amdgcn_exp2f(m[gq] - mnew);
-        lsum[gq] *= alpha;
+        if (SPLIT) lp[gq] *= alpha;
+        else lsum[gq] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
         m[gq] = mnew;
@@ -1209,7 +1211,11 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_amdgcn_exp2f(s[gq][t][r] - mg);
+        for (int r = 0; r < 4; ++r) s[gq][t][r] = (STE_ABLATE & 128) ? s[gq][t][r] - mg : __builtin_amdgcn_exp2f(s[gq][t][r] - mg);
+      if (SPLIT) {   // the row sum of p itself (hi + lo P sums to p within 2^-16): fp32 adds, not 2 MFMAs per u
+        f32x4 t01 = (s[gq][0] + s[gq][1]) + (s[gq][2] + s[gq][3]);
+        lp[gq] += (t01[0] + t01[1]) + (t01[2] + t01[3]);
+      }
       if (gq == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1217,18 +1223,18 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
         const bf16x8 pb = pack_acc(s[gq][2 * u], s[gq][2 * u + 1]);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pb, o[gq][dt]);
-        lsum[gq] = mfma16(ones, pb, lsum[gq]);   // row sum of the same (rounded) P, on the MFMA
         if (SPLIT) {
           const bf16x8 pl = pack_acc_lo(s[gq][2 * u], s[gq][2 * u + 1], pb);
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pl, o[gq][dt]);
-          lsum[gq] = mfma16(ones, pl, lsum[gq]);
+        } else {
+          lsum[gq] = mfma16(ones, pb, lsum[gq]);   // row sum of the same (rounded) P, on the MFMA
         }
       }
     }
     if (kt + 1 < nkt) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (this wave's pieces)
-      __builtin_amdgcn_s_barrier();                     // ... every wave's, and tile kt fully read
+      if (!(STE_ABLATE & 32)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (this wave's pieces)
+      if (!(STE_ABLATE & 256)) __builtin_amdgcn_s_barrier();                     // ... every wave's, and tile kt fully read
       if (kt + 2 < nkt) issue(kt + 2);
     }
   };
@@ -1238,7 +1244,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
   }
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq) {
-    const float lt = lsum[gq][0];   // every accumulator row holds the full row sum
+    // every accumulator row holds the full row sum (MFMA form) / the 4 lanes of a row hold partials
+    const float lt = SPLIT ? rowsum4(lp[gq]) : lsum[gq][0];
     const int myq = qw + 16 * gq + li;
     if (myq < T) {
       const float inv_l = 1.0f / lt;

@@ -8,6 +8,7 @@ from the library and surfaces as SteError.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -102,6 +103,14 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
         def launch():
             call("ste_gemm", C.byref(args), _s())
         name = None
+    if GEMM_CENSUS is not None and name is None:
+        key = "%s act=%d M=%d N=%d K=%d batch=%d %s" % (
+            gemm_kernel_name(args), act, M, N, K, batch,
+            "".join(f for f, v in (("B", bias), ("C2", pre_out), ("Z", z), ("R", residual), ("CS", colsum),
+                                   ("RS", row_scale), ("C3", out_bf16_copy)) if v is not None)
+            + ("D" if drop_p > 0 else "") + ("beta" if beta != 0 else "") + ("bf16" if out_bf16 or (
+                out is not None and out is not False and out.dtype == BF16) else ""))
+        GEMM_CENSUS[key] = GEMM_CENSUS.get(key, 0) + 1
     if GEMM_TRACE is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -116,6 +125,15 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
 
 
 GEMM_TRACE = None  # list while bench.py measures per-launch GEMM durations with HIP events
+# STE_GEMM_CENSUS=<file>: count bf16 GEMM launches per (kernel, epilogue features, shape) and
+# write the table at exit (profiles/ tooling: which launches miss a compiled epilogue)
+GEMM_CENSUS = {} if os.environ.get("STE_GEMM_CENSUS") else None
+if GEMM_CENSUS is not None:
+    import atexit
+    import json
+
+    atexit.register(lambda: open(os.environ["STE_GEMM_CENSUS"], "w").write(
+        json.dumps(dict(sorted(GEMM_CENSUS.items())), indent=1)))
 # list while bench.py measures the HBM-bound kernels (fbank, LayerNorm): (name, algorithmic
 # bytes, ev0, ev1) per launch, timed with HIP events on the launching (current) stream
 HBM_TRACE = None
