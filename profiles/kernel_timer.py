@@ -41,5 +41,33 @@ def text_attn_f32():
         print(f"text attention fwd B={B} T={T} H={H} drop={p}: fp32 {us:.1f} us, bf16 kernel {us_b:.1f} us")
 
 
+
+
+def layernorm():
+    """c2 Conformer LayerNorms (rows 31,936 x 1,024): forward to bf16, the chained pair, backward
+    with the residual gradient (dx fp32 + dxb bf16); GB/s of algorithmic bytes."""
+    R, D = 64 * 499, 1024
+    x = torch.randn(R, D, device="cuda")
+    g, b = torch.rand(D, device="cuda") + 0.5, torch.randn(D, device="cuda") * 0.1
+    yb = torch.empty(R, D, device="cuda", dtype=torch.bfloat16)
+    y = torch.empty(R, D, device="cuda")
+    yb2 = torch.empty_like(yb)
+    st = ops.layernorm_fwd(x, g, b, 1e-5, yb=yb)
+    us = timeit(lambda: ops.layernorm_fwd(x, g, b, 1e-5, yb=yb, mean=st[0], rstd=st[1]))
+    print(f"ln fwd -> bf16: {us:.1f} us, {R * D * 6 / us / 1e3:.0f} GB/s", flush=True)
+    us = timeit(lambda: ops.layernorm_fwd_pair(dict(x=x, gamma=g, beta=b, eps=1e-5, y=y, yb=yb),
+                                               dict(gamma=g, beta=b, eps=1e-5, yb=yb2)))
+    print(f"ln fwd pair (y fp32 + bf16, then bf16): {us:.1f} us, {R * D * 12 / us / 1e3:.0f} GB/s", flush=True)
+    dy = torch.randn(R, D, device="cuda").bfloat16()
+    dres = torch.randn(R, D, device="cuda")
+    dx = torch.empty(R, D, device="cuda")
+    dxb = torch.empty(R, D, device="cuda", dtype=torch.bfloat16)
+    us = timeit(lambda: ops.layernorm_bwd(dy, x, st[0], st[1], g, beta=b, dres=dres, dx=dx, dxb=dxb))
+    print(f"ln bwd (dy bf16, x, dres -> dx, dxb): {us:.1f} us, {R * D * 16 / us / 1e3:.0f} GB/s", flush=True)
+    us = timeit(lambda: ops.layernorm_bwd(dy, x, st[0], st[1], g, beta=b, dres=dres, dx=dx, dxb=dxb,
+                                          dgamma=torch.zeros(D, device="cuda"), dbeta=torch.zeros(D, device="cuda")))
+    print(f"ln bwd + dgamma/dbeta: {us:.1f} us, {R * D * 16 / us / 1e3:.0f} GB/s", flush=True)
+
+
 if __name__ == "__main__":
     globals()[sys.argv[1]]()

@@ -418,6 +418,83 @@ def test_layernorm_fwd_bwd(ops, cols):
         assert rel_err(db, br.grad) < 1e-5
 
 
+@pytest.mark.parametrize("reduce", [False, True])
+def test_layernorm_many_rows_per_wave(ops, reduce):
+    """c2-like row counts: each wave walks several rows, the forward and the column-sum-free
+    backward with the next row's operands in flight (the prefetch paths); bf16 dy as in the step."""
+    torch.manual_seed(11)
+    rows, cols = 9001, 1024
+    x = torch.randn(rows, cols, device=DEV) * 2 + 0.5
+    g, b = torch.randn(cols, device=DEV), torch.randn(cols, device=DEV)
+    yb = torch.empty(rows, cols, device=DEV, dtype=torch.bfloat16)
+    mean, rstd = ops.layernorm_fwd(x, g, b, 1e-5, yb=yb)
+    xr, gr, br = (t.clone().requires_grad_() for t in (x, g, b))
+    ref = F.layer_norm(xr, (cols,), gr, br, 1e-5)
+    assert rel_err(yb, ref) < 5e-3
+    assert torch.allclose(mean, x.mean(1), atol=1e-5)
+    dy = torch.randn(rows, cols, device=DEV).bfloat16()
+    ref.backward(dy.float())
+    dres = torch.randn_like(x)
+    dx = torch.empty_like(x)
+    dxb = torch.empty(rows, cols, device=DEV, dtype=torch.bfloat16)
+    dg = torch.zeros(cols, device=DEV) if reduce else None
+    db = torch.zeros(cols, device=DEV) if reduce else None
+    ops.layernorm_bwd(dy, x, mean, rstd, g, beta=b, dx=dx, dxb=dxb, dres=dres, dgamma=dg, dbeta=db)
+    assert rel_err(dx, xr.grad + dres) < 1e-5
+    assert rel_err(dxb, xr.grad + dres) < 5e-3
+    if reduce:
+        assert rel_err(dg, gr.grad) < 1e-5
+        assert rel_err(db, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("case", ["noreduce", "reduce", "frozen_second"])
+def test_layernorm_pair_matches_single_calls(ops, case):
+    """ste_layernorm_fwd_pair / _bwd_pair (a Conformer layer's final LN chained with the next
+    layer's FFN1 LN) against the same two LayerNorms run as single calls: forward outputs (fp32,
+    bf16, the second LN's MX-fp8 copy) bit for bit, input gradients bit for bit, column sums to
+    atomic-order rounding.  noreduce: no column sums (the residual row preloaded); reduce: both
+    LNs trainable; frozen_second: the later LN frozen (null dgamma/dbeta) under a trainable first."""
+    torch.manual_seed(12)
+    rows, cols = 5003, 1024
+    x = torch.randn(rows, cols, device=DEV) * 1.5 + 0.3
+    g1, b1 = torch.randn(cols, device=DEV), torch.randn(cols, device=DEV) * 0.1
+    g2, b2 = torch.randn(cols, device=DEV), torch.randn(cols, device=DEV) * 0.1
+    E = lambda dt=torch.float32: torch.empty(rows, cols, device=DEV, dtype=dt)  # noqa: E731
+    q8 = lambda: (E(torch.uint8), torch.empty(rows, cols // 32, device=DEV, dtype=torch.uint8))  # noqa: E731
+    # forward: pair vs singles
+    y1, y1b, y2b, q2 = E(), E(torch.bfloat16), E(torch.bfloat16), q8()
+    (ma, ra), (mb, rb) = ops.layernorm_fwd_pair(dict(x=x, gamma=g1, beta=b1, eps=1e-5, y=y1, yb=y1b),
+                                                dict(gamma=g2, beta=b2, eps=1e-5, yb=y2b, q8=q2))
+    y1s, y1bs, y2bs, q2s = E(), E(torch.bfloat16), E(torch.bfloat16), q8()
+    mas, ras = ops.layernorm_fwd(x, g1, b1, 1e-5, y=y1s, yb=y1bs)
+    mbs, rbs = ops.layernorm_fwd(y1s, g2, b2, 1e-5, yb=y2bs, q8=q2s)
+    for got, want in ((y1, y1s), (y1b, y1bs), (y2b, y2bs), (q2[0], q2s[0]), (q2[1], q2s[1]), (ma, mas), (ra, ras),
+                      (mb, mbs), (rb, rbs)):
+        assert torch.equal(got, want)
+    # backward: b (the later LN, with dy and the residual gradient) then a, fused vs chained
+    dy2 = torch.randn(rows, cols, device=DEV).bfloat16()
+    dres = torch.randn(rows, cols, device=DEV)
+    tr_a = case != "noreduce"
+    tr_b = case == "reduce"
+    Z = lambda on: torch.zeros(cols, device=DEV) if on else None  # noqa: E731
+    dga, dba, dsa, dgb, dbb = Z(tr_a), Z(tr_a), Z(tr_a), Z(tr_b), Z(tr_b)
+    dxa, dxab = E(), E(torch.bfloat16)
+    ops.layernorm_bwd_pair(
+        dict(x=x, mean=ma, rstd=ra, gamma=g1, beta=b1, dx=dxa, dxb=dxab, out_scale=0.5, dgamma=dga, dbeta=dba,
+             dsum=dsa),
+        dict(dy=dy2, x=y1, mean=mb, rstd=rb, gamma=g2, beta=b2, dres=dres, dgamma=dgb, dbeta=dbb))
+    dmid = E()
+    dgbs, dbbs, dgas, dbas, dsas = Z(tr_b), Z(tr_b), Z(tr_a), Z(tr_a), Z(tr_a)
+    ops.layernorm_bwd(dy2, y1s, mbs, rbs, g2, beta=b2, dres=dres, dx=dmid, dgamma=dgbs, dbeta=dbbs)
+    dxas, dxabs = E(), E(torch.bfloat16)
+    ops.layernorm_bwd(dmid, x, mas, ras, g1, beta=b1, dx=dxas, dxb=dxabs, out_scale=0.5, dgamma=dgas, dbeta=dbas,
+                      dsum=dsas)
+    assert torch.equal(dxa, dxas) and torch.equal(dxab, dxabs)
+    for got, want in ((dga, dgas), (dba, dbas), (dsa, dsas), (dgb, dgbs), (dbb, dbbs)):
+        if want is not None:
+            assert rel_err(got, want) < 1e-5
+
+
 # -------------------------------------------------------------- attention
 def _attn_case(ops, B, T, H, rel, masked, drop_p, seed=7, qk_scale=0.7, v_common=0.0, o_lo=False, tol=1e-2):
     """v_common > 0: every value row is a shared per-(batch, head) vector plus 0.05 noise, and
