@@ -451,8 +451,10 @@ def test_layernorm_many_rows_per_wave(ops, reduce):
 def test_layernorm_pair_matches_single_calls(ops, case):
     """ste_layernorm_fwd_pair / _bwd_pair (a Conformer layer's final LN chained with the next
     layer's FFN1 LN) against the same two LayerNorms run as single calls: forward outputs (fp32,
-    bf16, the second LN's MX-fp8 copy) bit for bit, input gradients bit for bit, column sums to
-    atomic-order rounding.  noreduce: no column sums (the residual row preloaded); reduce: both
+    bf16, the second LN's MX-fp8 copy) bit for bit; input gradients to fp32 rounding (the pair keeps
+    the intermediate gradient in registers and sums its row terms in another order than the
+    chained calls, which round it to an fp32 tensor in between), column sums to atomic-order
+    rounding.  noreduce: no column sums (the residual row preloaded); reduce: both
     LNs trainable; frozen_second: the later LN frozen (null dgamma/dbeta) under a trainable first."""
     torch.manual_seed(12)
     rows, cols = 5003, 1024
@@ -489,7 +491,9 @@ def test_layernorm_pair_matches_single_calls(ops, case):
     dxas, dxabs = E(), E(torch.bfloat16)
     ops.layernorm_bwd(dmid, x, mas, ras, g1, beta=b1, dx=dxas, dxb=dxabs, out_scale=0.5, dgamma=dgas, dbeta=dbas,
                       dsum=dsas)
-    assert torch.equal(dxa, dxas) and torch.equal(dxab, dxabs)
+    print(f"LN pair bwd [{case}]: dx {rel_err(dxa, dxas):.2e}, dxb {rel_err(dxab.float(), dxabs.float()):.2e}")
+    assert rel_err(dxa, dxas) < 1e-6
+    assert rel_err(dxab.float(), dxabs.float()) < 1e-4      # bf16 copies: the odd element one ulp apart
     for got, want in ((dga, dgas), (dba, dbas), (dsa, dsas), (dgb, dgbs), (dbb, dbbs)):
         if want is not None:
             assert rel_err(got, want) < 1e-5
