@@ -76,11 +76,15 @@ def parse(argv=None):
                     help="facebook/wav2vec2-base: the raw-waveform wav2vec2 encoder (SURVEY §8f rank 4, "
                          "not a BASELINE config: informational line, no CPU baseline)")
     ap.add_argument("--trace-steps", type=int, default=2,
-                    help="extra (untimed) steps whose launches are timed with HIP events for roofline / hbm_kernels")
+                    help="extra (untimed) steps whose launches are timed with HIP events for roofline / hbm_kernels "
+                         "(at least 1: the roofline object needs them)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=4, help="BASELINE.md §3: B=4")
     ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU steps (median), after 2 warm-ups")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.trace_steps < 1:
+        ap.error("--trace-steps must be >= 1 (the roofline object is measured on those steps)")
+    return args
 
 
 def batch_plan(args, world):
@@ -392,6 +396,8 @@ def main(argv=None):
         a[0] += 1
         a[1] += flops
         a[2] += e0.elapsed_time(e1) * 1e-3
+    if not agg:
+        raise SystemExit("bench: no GEMM launch was traced on the step's stream (--trace-steps must be >= 1)")
     dom = max(agg, key=lambda k: agg[k][2])
     n_l, fl, tm = agg[dom]
     achieved = fl / tm / 1e12

@@ -152,8 +152,11 @@ int ste_layernorm_fwd(const ste_ln_fwd_args* a, void* stream);
 
 /* Backward: g = dy (fp32 or bf16; times row_scale; through swish' if act==SWISH,
  * recomputing the pre-activation from x/mean/rstd), dx = LN'(g) (+ dres),
- * dgamma/dbeta += (fp32 atomics, optional).  Outputs: dx fp32 (optional),
- * dxb = bf16(dx * dropmask(drop_seed) * out_scale) (optional). */
+ * dgamma/dbeta/dsum += column sums (optional).  Outputs: dx fp32 (optional),
+ * dxb = bf16(dx * dropmask(drop_seed) * out_scale) (optional).
+ * Column sums: with a workspace (ws, >= ste_layernorm_bwd_ws_floats(rows, cols) floats, ws_floats
+ * its size) every block writes its partials there and a second launch adds them in a fixed
+ * order — run-to-run deterministic, no same-address atomics; ws = NULL: fp32 atomics. */
 typedef struct {
   int rows, cols;
   const void* dy; int64_t lddy; int dy_bf16;
@@ -171,8 +174,11 @@ typedef struct {
   const float* out_row_scale;                     /* multiplies the dxb copy rows (optional) */
   float* dsum;                                    /* += column sums of the dxb values (fp32, optional):
                                                      the bias gradient of the Linear feeding this residual */
+  float* ws; int64_t ws_floats;                   /* column-partial workspace (optional, see above) */
 } ste_ln_bwd_args;
 int ste_layernorm_bwd(const ste_ln_bwd_args* a, void* stream);
+/* workspace floats ste_layernorm_bwd / _bwd_pair need for deterministic column sums */
+int64_t ste_layernorm_bwd_ws_floats(int rows, int cols);
 
 /* Two chained LayerNorms in one pass over the rows (a Conformer layer's final_layer_norm and
  * the next layer's ffn1_layer_norm, tf:…wav2vec2_bert…:381-394, 359-362): forward

@@ -2,7 +2,11 @@
 epilogue the step uses, ste_gemm with a plain bf16 output, and torch.mm (hipBLASLt) on the
 same operands — the A/B harness behind DESIGN §3's GEMM numbers.
 
-    python profiles/gemm_probe.py [--rows 31936] [--iters 20] [--only NAME]
+    python profiles/gemm_probe.py [--rows 31936] [--iters 20] [--only NAME] [--mx8]
+
+--mx8: the forward GEMMs on MX-fp8 operands (ste_gemm_mx8, config 5) with the step's epilogues
+(FFN-in: pre-activation + fp8 copy of the output only, as in a frozen layer), next to the bf16
+kernel with the same epilogue (run twice, STE_MX8_8PH=0 / 1, to compare the two MX kernels).
 
 Shapes (M = b·T rows of c2 = 64 x 499): forward QKV / O / FFN-in / FFN-out, the input-gradient
 (dX = dY·W through the cached Wᵀ) and the weight-gradient (dW = dYᵀX, k-major operands,
@@ -22,6 +26,7 @@ def main():
     ap.add_argument("--rows", type=int, default=64 * 499)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--mx8", action="store_true")
     a = ap.parse_args()
     from speech_transcript_embeddings_amd import _lib, ops
     M = a.rows
@@ -55,6 +60,35 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / a.iters
 
+    if a.mx8:
+        for name, (K, N, epi) in cases.items():
+            if not epi.startswith("bias") or (a.only and not name.startswith(a.only)):
+                continue
+            A = x if K == D else (h if K == F else rnd(M, K))
+            W = rnd(N, K, sc=0.02)
+            bias = torch.randn(N, device=dev, generator=g) * 0.1
+            Aq, Wq = ops.mx8_quant(A), ops.mx8_quant(W)
+            kw = dict(bias=bias)
+            if epi == "bias_bf16":
+                kw.update(out_bf16=True)
+            elif epi == "bias_res":
+                kw.update(residual=res if N == D else rnd(M, N, dt=torch.float32))
+            else:   # FFN-in of a frozen layer: bf16 pre-activation + the fp8 copy only
+                kw.update(act=_lib.ACT_SWISH, pre_out=torch.empty(M, N, device=dev, dtype=torch.bfloat16), out=False,
+                          q_out=(torch.empty(M, N, device=dev, dtype=torch.uint8),
+                                 torch.empty(M, N // 32, device=dev, dtype=torch.uint8)))
+            t_mx = timed(lambda: ops.linear_mx8(Aq, Wq, **kw))
+            kwb = {k: v for k, v in kw.items() if k not in ("q_out", "out")}
+            if epi == "bias_swish_c2":
+                kwb.update(out_bf16=True)
+            t_bf = timed(lambda: ops.linear(A, W, **kwb))
+            fl = 2.0 * M * N * K
+            out[name] = {"M": M, "N": N, "K": K, "epilogue": epi, "mx8_us": round(t_mx, 1),
+                         "mx8_tflops": round(fl / t_mx / 1e6, 1), "bf16_us": round(t_bf, 1),
+                         "bf16_tflops": round(fl / t_bf / 1e6, 1)}
+            print(json.dumps({name: out[name]}), flush=True)
+        print(json.dumps(out), flush=True)
+        return
     for name, (K, N, epi) in cases.items():
         if a.only and not name.startswith(a.only):
             continue

@@ -9,6 +9,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from speech_transcript_embeddings_amd import ops  # noqa: E402
 
+ops.LN_ATOMIC_COLSUMS = os.environ.get("STE_LN_ATOMIC") == "1"   # A/B: LN column sums by fp32 atomics
+
 
 def timeit(fn, iters=20):
     for _ in range(3):
@@ -67,6 +69,14 @@ def layernorm():
     us = timeit(lambda: ops.layernorm_bwd(dy, x, st[0], st[1], g, beta=b, dres=dres, dx=dx, dxb=dxb,
                                           dgamma=torch.zeros(D, device="cuda"), dbeta=torch.zeros(D, device="cuda")))
     print(f"ln bwd + dgamma/dbeta: {us:.1f} us, {R * D * 16 / us / 1e3:.0f} GB/s", flush=True)
+    y1 = torch.empty_like(x)
+    (ma, ra), (mb, rb) = ops.layernorm_fwd_pair(dict(x=x, gamma=g, beta=b, eps=1e-5, y=y1),
+                                                dict(gamma=g, beta=b, eps=1e-5, yb=yb2))
+    Z = lambda: torch.zeros(D, device="cuda")  # noqa: E731
+    us = timeit(lambda: ops.layernorm_bwd_pair(
+        dict(x=x, mean=ma, rstd=ra, gamma=g, beta=b, dxb=dxb, dgamma=Z(), dbeta=Z(), dsum=Z()),
+        dict(dy=dy, x=y1, mean=mb, rstd=rb, gamma=g, beta=b, dres=dres, dgamma=Z(), dbeta=Z())))
+    print(f"ln bwd pair + column sums (both LNs): {us:.1f} us", flush=True)
 
 
 if __name__ == "__main__":

@@ -82,6 +82,7 @@ class LnBwdArgs(C.Structure):
         ("in_drop_p", c_float), ("in_seed", c_uint64),
         ("out_row_scale", c_void_p),
         ("dsum", c_void_p),
+        ("ws", c_void_p), ("ws_floats", c_int64),
     ]
 
 
@@ -122,6 +123,7 @@ _SIGS = {
     "ste_layernorm_bwd": (c_int, [C.POINTER(LnBwdArgs), c_void_p]),
     "ste_layernorm_fwd_pair": (c_int, [C.POINTER(LnFwdArgs), C.POINTER(LnFwdArgs), c_void_p]),
     "ste_layernorm_bwd_pair": (c_int, [C.POINTER(LnBwdArgs), C.POINTER(LnBwdArgs), c_void_p]),
+    "ste_layernorm_bwd_ws_floats": (c_int64, [c_int, c_int]),
     "ste_attention_fwd": (c_int, [C.POINTER(AttnArgs), c_void_p]),
     "ste_attention_bwd": (c_int, [C.POINTER(AttnArgs), c_void_p]),
     "ste_attention_fwd_f32": (c_int, [C.POINTER(AttnArgs), c_void_p, c_int64, c_void_p]),

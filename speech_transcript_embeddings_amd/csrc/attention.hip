@@ -1036,25 +1036,21 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
     glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w, lane);
     glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w + 1, lane);
   };
-  // prologue: every global read is issued up front and waited once (the first two K/V tiles by
-  // DMA, Q and E fragments and the key-mask flags into registers)
+  // prologue: K/V tile 0 and the distance table E (80 rows, clamped to nrel-1: rows >= nrel only
+  // reach table entries that are never written) by DMA — E into ring slot 1, which takes tile 1
+  // once the Q·Eᵀ table is built: one 10 KB image per block instead of 40 KB of per-wave fragment
+  // loads — then Q fragments and the key-mask flags
   issue(0);
-  if (nkt > 1) issue(1);
-  bf16x8 qf[2][2], ef[NREL / 16][2];
+  const char* sE = sm + KV;
+  for (int pc = w; pc < NREL / 8; pc += 4)
+    glds_tile_piece((const bf16*)a.rel_E, HD, 0, 0, nrel, sm + KV, pc, lane);
+  bf16x8 qf[2][2];
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int q = qw + 16 * gq + li;
       qf[gq][s] = q < T ? *reinterpret_cast<const bf16x8*>(Qb + (int64_t)(bT + q) * a.ldq + 32 * s + 8 * g) : bf16x8{};
-    }
-#pragma unroll
-  for (int jt = 0; jt < NREL / 16; ++jt)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {   // E row jt*16 + li as the A operand (rows >= nrel: zero)
-      const int j = jt * 16 + li;
-      ef[jt][s] = j < nrel ? *reinterpret_cast<const bf16x8*>((const bf16*)a.rel_E + j * HD + 32 * s + 8 * g)
-                           : bf16x8{};
     }
   // key-validity words: bit j of word kt = key 64kt+j is < T and unmasked
   uint64_t* okw = reinterpret_cast<uint64_t*>(sm + OKW_OFF);
@@ -1067,13 +1063,15 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
   // padded, pre-scaled Q·Eᵀ rows of the wave's 32 queries: entry PADL + j = bin j,
   // entries 0..PADL-1 replicate bin 0 and PADL+nrel.. replicate bin nrel-1
   float* qe = reinterpret_cast<float*>(sm + QE_OFF) + w * WQ * QS;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's tile-0 and E pieces, Q
+  __syncthreads();                                    // every wave's E pieces and validity words
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq)
 #pragma unroll
     for (int jt = 0; jt < NREL / 16; ++jt) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 2; ++s) acc = mfma16(ef[jt][s], qf[gq][s], acc);
+      for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sE, jt * 16, s, lane), qf[gq][s], acc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = jt * 16 + 4 * g + r;
@@ -1096,9 +1094,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
     blo[gq] = qe[(16 * gq + li) * QS + PADL];
     bhi[gq] = qe[(16 * gq + li) * QS + PADL + nrel - 1];
   }
-  if (nkt > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // tile 0 landed (this wave's pieces)
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();   // every wave's tile-0 pieces, validity words and table rows
+  __syncthreads();   // every wave has read E: slot 1 takes tile 1
+  if (nkt > 1) issue(1);
 
   // lane constants of the transposed V reads: frag_tr's rows 32u+4g+q (+16), column quad 4dt+p
   const int tq = li >> 2, tp = li & 3, r0 = 4 * g + tq;
@@ -1159,7 +1156,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
       const int q0g = qw + 16 * gq, myq = q0g + li;
       const bool all_lo = (kb + TK - 1) - q0g <= -left;
       const bool all_hi = kb - (q0g + 15) >= right;
-      if (all_lo || all_hi || (STE_ABLATE & 512)) {
+      const bool band = !(all_lo || all_hi || (STE_ABLATE & 512));
+      if (!band) {
         const float bc = all_lo ? blo[gq] : bhi[gq];
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -1189,14 +1187,14 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
             s[gq][t][r] = ok ? s[gq][t][r] : fill;
           }
       }
-      float tmax = max3f(s[gq][0][0], s[gq][0][1], s[gq][0][2]);
-      tmax = max3f(tmax, s[gq][0][3], s[gq][1][0]);
-      tmax = max3f(tmax, s[gq][1][1], s[gq][1][2]);
-      tmax = max3f(tmax, s[gq][1][3], s[gq][2][0]);
-      tmax = max3f(tmax, s[gq][2][1], s[gq][2][2]);
-      tmax = max3f(tmax, s[gq][2][3], s[gq][3][0]);
-      tmax = max3f(tmax, s[gq][3][1], s[gq][3][2]);
-      tmax = rowmax4(max3f(tmax, s[gq][3][3], tmax));
+      // row max as a depth-3 tree (a sequential max3 chain serialises 8 dependent VALU ops)
+      const float t0 = max3f(s[gq][0][0], s[gq][0][1], s[gq][0][2]);
+      const float t1 = max3f(s[gq][0][3], s[gq][1][0], s[gq][1][1]);
+      const float t2 = max3f(s[gq][1][2], s[gq][1][3], s[gq][2][0]);
+      const float t3 = max3f(s[gq][2][1], s[gq][2][2], s[gq][2][3]);
+      const float t4 = max3f(s[gq][3][0], s[gq][3][1], s[gq][3][2]);
+      const float u0 = max3f(t0, t1, t2), u1 = max3f(t3, t4, s[gq][3][3]);
+      const float tmax = rowmax4(max3f(u0, u1, u1));
       // deferred rescale: raise the running max only when a row grew past m + THRESH
       if (__builtin_amdgcn_ballot_w64(tmax > m[gq] + THRESH) != 0ull) {
         const float mnew = fmaxf(m[gq], tmax);
@@ -1211,7 +1209,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s[gq][t][r] = (STE_ABLATE & 128) ? s[gq][t][r] - mg : __builtin_amdgcn_exp2f(s[gq][t][r] - mg);
+        for (int r = 0; r < 4; ++r)
+          s[gq][t][r] = (STE_ABLATE & 128) ? s[gq][t][r] - mg : __builtin_amdgcn_exp2f(s[gq][t][r] - mg);
       if (SPLIT) {   // the row sum of p itself (hi + lo P sums to p within 2^-16): fp32 adds, not 2 MFMAs per u
         f32x4 t01 = (s[gq][0] + s[gq][1]) + (s[gq][2] + s[gq][3]);
         lp[gq] += (t01[0] + t01[1]) + (t01[2] + t01[3]);

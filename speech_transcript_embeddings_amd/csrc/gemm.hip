@@ -25,6 +25,7 @@
 // Both: XCD-aware bijective block remap + grouped tile order for L2 reuse, and an
 // LDS-staged epilogue with row-contiguous (16 B/lane) loads and stores.
 #include <cstdio>
+#include <utility>
 #include "common.h"
 #include "../../include/ste.h"
 
@@ -145,6 +146,15 @@ struct Q8Out {  // optional MX-fp8 copy of a GEMM output: q [M][ldq] e4m3, s [M]
   int64_t ldq;
 };
 
+// MX-fp8 operands of gemm_8ph_kernel<…, MX = true>: the E8M0 block scales (one per 32 k of a row,
+// [rows][K/32] bytes) of A and B, and the optional MX-fp8 copy of the output (generic epilogue)
+struct Mx8Args {
+  const uint8_t* sa;
+  const uint8_t* sb;
+  int64_t lsa, lsb;
+  Q8Out q8;
+};
+
 STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, int row0, int col0, int col1,
                            int batch, int lane, Csum& csum, int ld = EPI_LD, bool swz16 = false,
                            const Q8Out* q8 = nullptr) {
@@ -234,7 +244,10 @@ STE_DEV void colsum_flush(const ste_gemm_args& p, Csum csum, int col0, int col1,
 // a row behind the previous row's stores.  EF_GENERIC keeps every feature runtime.
 enum : int {
   EF_BIAS = 1, EF_C2 = 2, EF_Z = 4, EF_DROP = 8, EF_RS = 16, EF_COLSUM = 32, EF_R = 64, EF_RBF16 = 128,
-  EF_BETA = 256, EF_CBF16 = 512, EF_C3 = 1024, EF_GENERIC = -1
+  EF_BETA = 256, EF_CBF16 = 512, EF_C3 = 1024,
+  EF_Q8 = 2048,   // + MX-fp8 copy of the output (8-phase MX kernel: the FFN intermediate for the next MX GEMM)
+  EF_NOC = 4096,  // no C output (with EF_Q8: a frozen layer's FFN intermediate exists only in fp8)
+  EF_GENERIC = -1
 };
 
 int epi_flags(const ste_gemm_args& a) {
@@ -329,7 +342,8 @@ STE_DEV EpiFlags epi_flags_dev(const ste_gemm_args& p) {
 template <int EF>
 constexpr int epi_stores() {
   if (EF < 0) return 0;
-  return 16 * (((EF & EF_CBF16) ? 1 : 2) + ((EF & EF_C2) ? 1 : 0) + ((EF & EF_C3) ? 1 : 0));
+  return 16 * (((EF & EF_NOC) ? 0 : ((EF & EF_CBF16) ? 1 : 2)) + ((EF & EF_C2) ? 1 : 0) + ((EF & EF_C3) ? 1 : 0) +
+               ((EF & EF_Q8) ? 2 : 0));
 }
 struct EpiLoads {
   f32x8 z[2], r[2], c[2];
@@ -362,7 +376,7 @@ STE_DEV void epi_load16(const ste_gemm_args& p, int row0, int col0, int col1, in
 
 template <int EF, int ACT, bool FULL>
 STE_DEV void epi_store16(const ste_gemm_args& p, const float* epi, int row0, int col0, int col1, int batch,
-                         int lane, f32x8 bias, const EpiLoads& L, Csum& csum) {
+                         int lane, f32x8 bias, const EpiLoads& L, Csum& csum, const Q8Out* q8 = nullptr) {
   const EpiFlags f = epi_flags_dev<EF, ACT>(p);
   const int cg = lane & 7, cl = cg * 8;
   const int col = cl < 32 ? col0 + cl : col1 + (cl - 32);
@@ -407,7 +421,9 @@ STE_DEV void epi_store16(const ste_gemm_args& p, const float* epi, int row0, int
     }
     if (f.f_r) x += L.r[k];
     if (f.f_beta) x += L.c[k] * p.beta;
-    st8((char*)p.C + (offC + row * p.ldc + col) * (f.c_bf ? 2 : 4), f.c_bf, x, full, nval);
+    if constexpr (EF >= 0 && (EF & EF_Q8) != 0)   // 4 lanes = one 32-column block (FULL tiles: N % 128 == 0)
+      mx8_block_store(x, q8->q + row * q8->ldq + col, q8->s + row * (q8->ldq >> 5) + (col >> 5), lane);
+    if (EF < 0 || (EF & EF_NOC) == 0) st8((char*)p.C + (offC + row * p.ldc + col) * (f.c_bf ? 2 : 4), f.c_bf, x, full, nval);
     if (f.f_c3) st8((bf16*)p.C3 + offC + row * p.ldc3 + col, true, p.c3_lo ? lo8(x) : x, full, nval);
   }
 }
@@ -430,7 +446,7 @@ constexpr int DJ[4] = {0, 16, 128, 144};  // column of accumulator block j from 
 template <int EF>
 constexpr bool epi_bf16s() {
   return EF >= 0 && (EF & EF_CBF16) != 0 &&
-         (EF & (EF_R | EF_BETA | EF_C3 | EF_RS | EF_DROP | EF_C2 | EF_COLSUM | EF_Z)) == 0;
+         (EF & (EF_R | EF_BETA | EF_C3 | EF_RS | EF_DROP | EF_C2 | EF_COLSUM | EF_Z | EF_Q8 | EF_NOC)) == 0;
 }
 STE_DEV f32x4 act4(f32x4 v, int act) {
 #pragma unroll
@@ -840,7 +856,10 @@ STE_DEV int half_row(int pr, int h) {
   return (pr / G) * (2 * G) + h * G + (pr % G);
 }
 
-template <bool KC, int G>
+// O32: the source as a 32-bit byte offset from the (wave-uniform) base, which the DMA takes as
+// saddr + voffset: one VGPR per piece instead of a 64-bit pointer (operands < 4 GiB; the MX kernel,
+// whose scale staging needs the registers)
+template <bool KC, int G, bool O32 = false>
 STE_DEV void stage_half(const bf16* base, int64_t ld, int row0, int rows, int k0, int h, char* dst, int wave,
                         int lane) {
 #pragma unroll
@@ -851,7 +870,8 @@ STE_DEV void stage_half(const bf16* base, int64_t ld, int row0, int rows, int k0
       const int pr = piece * 8 + (lane >> 3);
       const int ch = (lane & 7) ^ (lane >> 3);
       const int gr = min(row0 + half_row<G>(pr, h), rows - 1);
-      src = base + (int64_t)gr * ld + k0 + ch * 8;
+      if (O32) src = (const bf16*)((const char*)base + (uint32_t)(((uint32_t)gr * (uint32_t)ld + k0 + ch * 8) * 2u));
+      else src = base + (int64_t)gr * ld + k0 + ch * 8;
     } else {   // image [64 k][128 cols], 256-B k-rows, chunk ^ km_xor(k)
       const int kk = piece * 4 + (lane >> 4);
       const int lc = (lane & 15) ^ km_chunk_xor(kk);
@@ -860,6 +880,55 @@ STE_DEV void stage_half(const bf16* base, int64_t ld, int row0, int rows, int k0
     }
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
   }
+}
+// MX (e4m3 operands, K-tile = 128 fp8 = the same 128-B LDS rows as 64 bf16): the K-tile's scales,
+// 4 bytes (k-blocks 0..3) per row, A then B, 2 KiB per stage in the epilogue-slot region (the MX
+// kernel stages its epilogue in the ring's free K-tile-1 halves instead); one 4-B LDS-DMA piece per
+// wave: waves 0-3 the A rows, 4-7 the B rows
+constexpr int SC_OFF = EPI_OFF;
+constexpr int SC_STAGE = 2048;
+STE_DEV void stage_scales(const Mx8Args& mx, int m0, int M, int n0, int N, int t, char* smem, int wave, int lane) {
+  const bool isb = wave >= 4;
+  const int r = (wave & 3) * 64 + lane;
+  const uint8_t* src = isb ? mx.sb + (uint32_t)(min(n0 + r, N - 1) * (uint32_t)mx.lsb + 4 * t)
+                           : mx.sa + (uint32_t)(min(m0 + r, M - 1) * (uint32_t)mx.lsa + 4 * t);
+  char* dst = smem + SC_OFF + (t & 1) * SC_STAGE + (isb ? 1024 : 0) + (wave & 3) * 256;
+  __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 4, 0, 0);
+}
+// the scale bytes lane l feeds the MFMAs (its row l & 15 of each 16-row group, k-block l >> 4),
+// two per register: ds_read_u8_d16 into bits 0-7, ds_read_u8_d16_hi into bits 16-23 (the MFMA's
+// scale op_sel then picks byte 0 or 2).  asm reads: the caller waits lgkmcnt before the MFMAs.
+template <int OFF>
+STE_DEV void ds_u8_lo(int& r, uint32_t addr) {
+  asm volatile("ds_read_u8_d16 %0, %1 offset:%2" : "+v"(r) : "v"(addr), "i"(OFF) : "memory");
+}
+template <int OFF>
+STE_DEV void ds_u8_hi(int& r, uint32_t addr) {
+  asm volatile("ds_read_u8_d16_hi %0, %1 offset:%2" : "+v"(r) : "v"(addr), "i"(OFF) : "memory");
+}
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4m __attribute__((ext_vector_type(4)));
+// the MX operand of row rb + (l & 15): bytes k 16g..16g+15 and 64+16g.. of its swizzled 128-B row
+// (g = l >> 4), straight into one 8-register tuple
+STE_DEV i32x8 frag_mx(const char* tile, int rb, int lane) {
+  const int r = rb + (lane & 15), g = lane >> 4;
+  const i32x4m lo = *reinterpret_cast<const i32x4m*>(tile + r * 128 + ((g ^ (r & 7)) << 4));
+  const i32x4m hi = *reinterpret_cast<const i32x4m*>(tile + r * 128 + (((g + 4) ^ (r & 7)) << 4));
+  return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+// f(integral_constant<int, I>) for I = 0..N-1 (compile-time indices for the MFMA's op_sel)
+template <typename F, int... I>
+STE_DEV void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+STE_DEV void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+// scales: byte 2*(X&1) of sx / 2*(Y&1) of sy (see ds_u8_lo / ds_u8_hi)
+template <int X, int Y>
+STE_DEV f32x4 mfma_mx(const i32x8& x, const i32x8& y, f32x4 c, int sx, int sy) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(x, y, c, 0, 0, 2 * (X & 1), sx, 2 * (Y & 1), sy);
 }
 }  // namespace ph8
 
@@ -931,7 +1000,7 @@ STE_DEV f32x8 tile_bias(const ste_gemm_args& p, int n0, int wn, int lane) {
 // 16 rows x 64 columns through the wave's own LDS slot; straight-line code per FULL value.
 template <int EF, int ACT, bool FULL>
 STE_DEV void epilogue_8ph(const ste_gemm_args& p, const f32x4 (&acc)[8][4], float* epi, int m0, int n0, int batch,
-                          int wm, int wn, int lane, f32x8 bias) {
+                          int wm, int wn, int lane, f32x8 bias, const Q8Out* q8 = nullptr) {
   Csum csum = {};
   const int c0 = n0 + wn * 32, c1 = n0 + 128 + wn * 32;
 #define STE_EPI_STAGE(PS)                                                                       \
@@ -948,13 +1017,13 @@ STE_DEV void epilogue_8ph(const ste_gemm_args& p, const f32x4 (&acc)[8][4], floa
 #define STE_EPI_ROW0(PS) (m0 + wm * 128 + (PS) * 16)
 #define STE_EPI_LOAD(PS, L) epi_load16<EF, ACT, FULL>(p, STE_EPI_ROW0(PS), c0, c1, batch, lane, L);
 #define STE_EPI_STORE(PS, L)                                                                    \
-  epi_store16<EF, ACT, FULL>(p, epi, STE_EPI_ROW0(PS), c0, c1, batch, lane, bias, L, csum);     \
+  epi_store16<EF, ACT, FULL>(p, epi, STE_EPI_ROW0(PS), c0, c1, batch, lane, bias, L, csum, q8); \
   __builtin_amdgcn_s_waitcnt(0xc07f);                                                           \
   __builtin_amdgcn_wave_barrier();
   if constexpr (EF < 0) {
 #define STE_EPI_G(PS)                                                                           \
     STE_EPI_STAGE(PS)                                                                           \
-    epilogue_tile(p, epi, 16, STE_EPI_ROW0(PS), c0, c1, batch, lane, csum, 64, true);           \
+    epilogue_tile(p, epi, 16, STE_EPI_ROW0(PS), c0, c1, batch, lane, csum, 64, true, q8);       \
     __builtin_amdgcn_s_waitcnt(0xc07f);                                                         \
     __builtin_amdgcn_wave_barrier();
     STE_EPI_G(0) STE_EPI_G(1) STE_EPI_G(2) STE_EPI_G(3) STE_EPI_G(4) STE_EPI_G(5) STE_EPI_G(6) STE_EPI_G(7)
@@ -978,10 +1047,14 @@ STE_DEV void epilogue_8ph(const ste_gemm_args& p, const f32x4 (&acc)[8][4], floa
   if (EF < 0 ? p.colsum != nullptr : (EF & EF_COLSUM) != 0) colsum_flush(p, csum, c0, c1, batch, lane);
 }
 
-template <int E>
+// steady-state operand wait: W pieces stay in flight (4 half-tiles = 8; MX adds the K-tile's scale
+// piece, issued with A-half 0, so 9), plus the previous tile's epilogue stores still draining
+// (capped at the 6-bit vmcnt field: waiting for a few more of those stores is merely early)
+template <int W, int E>
 STE_DEV void vm_wait8(int extra) {
-  if (E > 0 && extra) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + E) : "memory");
-  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  constexpr int WE = W + E < 63 ? W + E : 63;
+  if (E > 0 && extra) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WE) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W) : "memory");
 }
 
 // Operands of batch entry `batch` and its K-tile count.  Split-K slab launches (ste_gemm's
@@ -1003,12 +1076,16 @@ STE_DEV void operand_bases(const ste_gemm_args& p, int batch, const bf16*& A, co
   nk = p.K / 64;
 }
 
-template <bool A_KC, bool B_KC, int EF, int ACT>
-__global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
+// MX: e4m3 operands (A_KC = B_KC = true), the kernel arguments in bf16 units (K, lda, ldb halved:
+// two fp8 per bf16 slot), scales and the optional fp8 output copy in mx.
+template <bool A_KC, bool B_KC, int EF, int ACT, bool MX = false>
+__global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p, Mx8Args mx) {
   using namespace ph8;
   constexpr int E_ST = epi_stores<EF>();
   constexpr bool SW = epi_bf16s<EF>();  // swapped MFMA operands + bf16-staged epilogue
-  static_assert(8 + E_ST <= 63, "vmcnt immediate");
+  constexpr int VW = MX ? 9 : 8;
+  static_assert(!MX || (A_KC && B_KC), "MX operands are k-contiguous");
+  static_assert(VW <= 63, "vmcnt immediate");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1024,28 +1101,37 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
   const bf16* A;
   const bf16* B;
   operand_bases(p, batch, A, B, nk);
-#define STAGE_A(t, h) stage_half<A_KC, 64>(A, p.lda, m0, p.M, (t) * 64, h, smem + ((t) & 1) * BUF + (h) * HALF, wave, lane)
+#define STAGE_A(t, h) \
+  stage_half<A_KC, 64, MX>(A, p.lda, m0, p.M, (t) * 64, h, smem + ((t) & 1) * BUF + (h) * HALF, wave, lane)
 #define STAGE_B(t, h) \
-  stage_half<B_KC, 128>(B, p.ldb, n0, p.N, (t) * 64, h, smem + ((t) & 1) * BUF + (2 + (h)) * HALF, wave, lane)
-#define STAGE_PROLOGUE()                                        \
-  {                                                             \
-    STAGE_A(0, 0); STAGE_B(0, 0); STAGE_B(0, 1); STAGE_A(0, 1); \
-    if (nk > 1) { STAGE_A(1, 0); STAGE_B(1, 0); }               \
+  stage_half<B_KC, 128, MX>(B, p.ldb, n0, p.N, (t) * 64, h, smem + ((t) & 1) * BUF + (2 + (h)) * HALF, wave, lane)
+#define STAGE_S(t) \
+  if constexpr (MX) stage_scales(mx, m0, p.M, n0, p.N, (t), smem, wave, lane)
+#define STAGE_PROLOGUE()                                                    \
+  {                                                                         \
+    STAGE_A(0, 0); STAGE_S(0); STAGE_B(0, 0); STAGE_B(0, 1); STAGE_A(0, 1); \
+    if (nk > 1) { STAGE_A(1, 0); STAGE_S(1); STAGE_B(1, 0); }               \
   }
   // prologue of the first tile: tile 0 complete, tile 1's A0/B0 (phases (-1,*) of the steady state)
   STAGE_PROLOGUE();
   int extra = 0;  // stores of the previous tile's epilogue issued after this prologue (FULL tiles)
-  float* epi = reinterpret_cast<float*>(smem + EPI_OFF) + wave * EPI16_FLOATS;
+  // MX: the epilogue-slot region holds the scale stages; the epilogue stages through ring buffer 1's
+  // A1 / B1 halves instead, which no DMA touches between the main loop and the next tile's phase 0
+  char* const epi_base = MX ? smem + BUF + (wave < 4 ? HALF : 3 * HALF) + (wave & 3) * EPI16_FLOATS * 4
+                            : smem + EPI_OFF + wave * EPI16_FLOATS * 4;
+  float* epi = reinterpret_cast<float*>(epi_base);
   constexpr bool EPI_OVL = EF >= 0 && (EF & (EF_Z | EF_R | EF_BETA | EF_COLSUM | EF_RS)) == 0;
   f32x8 bias = f32x8{};
   f32x4 sbias[4] = {};
-  if constexpr (EF >= 0 && (EF & EF_BIAS) != 0) {
+  // the tile's bias preloaded across the main loop — except MX, whose main loop needs the registers
+  // (loaded at the epilogue instead)
+  if constexpr (EF >= 0 && (EF & EF_BIAS) != 0 && !MX) {
     if constexpr (SW) swap_bias(p, n0, wn, lane, sbias);
     else bias = tile_bias(p, n0, wn, lane);
   }
 
   for (;;) {
-    if (nk > 1) vm_wait8<E_ST>(extra);
+    if (nk > 1) vm_wait8<VW, E_ST>(extra);
     else STE_VMCNT(0);
     STE_BARRIER();
 
@@ -1056,6 +1142,7 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
+    i32x8 ma0[MX ? 4 : 1], ma1[MX ? 4 : 1], mb0[MX ? 2 : 1], mb1[MX ? 2 : 1];
     // Ping-pong: waves 4-7 run one barrier behind waves 0-3, so on every SIMD (one wave of
     // each group) one wave's MFMA cluster overlaps the other's ds_reads + staging.  Buffer
     // safety holds with the extra barrier of skew (reads stay >= 1 phase after the retiring
@@ -1068,7 +1155,35 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
       const char* buf = smem + (t & 1) * BUF;
       const bool tail = t + 2 >= nk;  // fewer stages in flight: drain fully instead of counting
       const int ex = t == 0 ? extra : 0;
+      // MX: the K-tile's 12 scale bytes of this lane in 6 registers, read with phase 0's fragments
+      // (S(t) is staged with A-half 0 of K-tile t and retired by the same waits): sca[i >> 1] holds
+      // A row group i (rows wm*128 + 16i..), scb[j >> 1] B column group j
+      int sca[4] = {0, 0, 0, 0}, scb[2] = {0, 0};
+      if constexpr (MX) {
+        typedef __attribute__((address_space(3))) char lds_char_t;
+        // the lane id regenerated (mbcnt) behind an opaque copy each K-tile: the addresses are rebuilt
+        // (a few VALU) instead of being hoisted out of the loop and spilled (a scratch reload inside
+        // the loop makes hipcc drain the counted DMA pipeline with vmcnt(0))
+        int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        asm volatile("" : "+v"(ln));
+        const uint32_t sbase = (uint32_t)(uintptr_t)(lds_char_t*)smem + SC_OFF + (t & 1) * SC_STAGE + (ln >> 4) +
+                               (ln & 15) * 4;
+        const uint32_t aa = sbase + wm * 512, ab = sbase + 1024 + wn * 128;
+        ds_u8_lo<0>(sca[0], aa);    ds_u8_hi<64>(sca[0], aa);
+        ds_u8_lo<128>(sca[1], aa);  ds_u8_hi<192>(sca[1], aa);
+        ds_u8_lo<256>(sca[2], aa);  ds_u8_hi<320>(sca[2], aa);
+        ds_u8_lo<384>(sca[3], aa);  ds_u8_hi<448>(sca[3], aa);
+        ds_u8_lo<0>(scb[0], ab);    ds_u8_hi<64>(scb[0], ab);
+        ds_u8_lo<512>(scb[1], ab);  ds_u8_hi<576>(scb[1], ab);
+      }
       // ---- phase 0
+      if constexpr (MX) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) mb0[j] = frag_mx(buf + 2 * HALF, wn * 32 + j * 16, lane);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ma0[i] = frag_mx(buf, wm * 64 + i * 16, lane);
+      } else {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -1078,65 +1193,123 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s = 0; s < 2; ++s) a0[i][s] = frag_a_8ph<A_KC>(buf, wm * 64 + i * 16, s, lane);
+      }
       if (t + 1 < nk) STAGE_B(t + 1, 1);
-      if (tail) STE_VMCNT(0); else vm_wait8<E_ST>(ex);
+      if (tail) STE_VMCNT(0); else vm_wait8<VW, E_ST>(ex);
       STE_BARRIER();
-      STE_LDS_SYNC(!A_KC || !B_KC);
+      STE_LDS_SYNC(!A_KC || !B_KC || MX);   // MX: the asm scale reads
       STE_PRIO_HI();
+      if constexpr (MX) {
+        static_for<4>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          static_for<2>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            acc[i][j] = SW ? mfma_mx<j, i>(mb0[j], ma0[i], acc[i][j], scb[0], sca[i >> 1])
+                           : mfma_mx<i, j>(ma0[i], mb0[j], acc[i][j], sca[i >> 1], scb[0]);
+          });
+        });
+      } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = SW ? mfma16(b0[j][s], a0[i][s], acc[i][j]) : mfma16(a0[i][s], b0[j][s], acc[i][j]);
+      }
       STE_PRIO_LO();
       STE_BARRIER();
       // ---- phase 1
+      if constexpr (MX) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) mb1[j] = frag_mx(buf + 3 * HALF, wn * 32 + j * 16, lane);
+      } else {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int s = 0; s < 2; ++s) b1[j][s] = frag_b_8ph<B_KC>(buf + 3 * HALF, wn * 32 + j * 16, s, lane);
+      }
       if (t + 1 < nk) STAGE_A(t + 1, 1);
-      if (tail) STE_VMCNT(0); else vm_wait8<E_ST>(ex);
+      if (tail) STE_VMCNT(0); else vm_wait8<VW, E_ST>(ex);
       STE_BARRIER();
       STE_LDS_SYNC(!B_KC);
       STE_PRIO_HI();
+      if constexpr (MX) {
+        static_for<4>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          static_for<2>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            acc[i][2 + j] = SW ? mfma_mx<j, i>(mb1[j], ma0[i], acc[i][2 + j], scb[1], sca[i >> 1])
+                               : mfma_mx<i, j>(ma0[i], mb1[j], acc[i][2 + j], sca[i >> 1], scb[1]);
+          });
+        });
+      } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][2 + j] = SW ? mfma16(b1[j][s], a0[i][s], acc[i][2 + j]) : mfma16(a0[i][s], b1[j][s], acc[i][2 + j]);
+      }
       STE_PRIO_LO();
       STE_BARRIER();
       // ---- phase 2
+      if constexpr (MX) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ma1[i] = frag_mx(buf + HALF, wm * 64 + i * 16, lane);
+      } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s = 0; s < 2; ++s) a1[i][s] = frag_a_8ph<A_KC>(buf + HALF, wm * 64 + i * 16, s, lane);
-      if (t + 2 < nk) STAGE_A(t + 2, 0);
+      }
+      if (t + 2 < nk) {
+        STAGE_A(t + 2, 0);
+        STAGE_S(t + 2);
+      }
       STE_BARRIER();
       STE_LDS_SYNC(!A_KC);
       STE_PRIO_HI();
+      if constexpr (MX) {
+        static_for<4>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          static_for<2>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            acc[4 + i][2 + j] = SW ? mfma_mx<j, i>(mb1[j], ma1[i], acc[4 + i][2 + j], scb[1], sca[2 + (i >> 1)])
+                                   : mfma_mx<i, j>(ma1[i], mb1[j], acc[4 + i][2 + j], sca[2 + (i >> 1)], scb[1]);
+          });
+        });
+      } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = SW ? mfma16(b1[j][s], a1[i][s], acc[4 + i][2 + j]) : mfma16(a1[i][s], b1[j][s], acc[4 + i][2 + j]);
+      }
       STE_PRIO_LO();
       STE_BARRIER();
       // ---- phase 3
       if (t + 2 < nk) STAGE_B(t + 2, 0);
-      if (tail) STE_VMCNT(0); else vm_wait8<E_ST>(ex);
+      if (tail) STE_VMCNT(0); else vm_wait8<VW, E_ST>(ex);
       STE_BARRIER();
       STE_PRIO_HI();
+      if constexpr (MX) {
+        static_for<4>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          static_for<2>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            acc[4 + i][j] = SW ? mfma_mx<j, i>(mb0[j], ma1[i], acc[4 + i][j], scb[0], sca[2 + (i >> 1)])
+                               : mfma_mx<i, j>(ma1[i], mb0[j], acc[4 + i][j], sca[2 + (i >> 1)], scb[0]);
+          });
+        });
+      } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[4 + i][j] = SW ? mfma16(b0[j][s], a1[i][s], acc[4 + i][j]) : mfma16(a1[i][s], b0[j][s], acc[4 + i][j]);
+      }
       STE_PRIO_LO();
       STE_BARRIER();
     }
@@ -1149,8 +1322,15 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
     const int vb_next = vb + gridDim.x;
     const bool more = vb_next < total;
     const bool full_tile = em0 + 256 <= p.M && en0 + 256 <= p.N;
-    asm volatile("" : "+v"(bias));  // bias landed long ago (the main loop drained vmcnt): no waits below
-    if constexpr (SW && (EF & EF_BIAS) != 0) {
+    if constexpr (EF >= 0 && (EF & EF_BIAS) != 0 && MX) {
+      // this tile's bias, issued before the next prologue's DMA (the compiler counts that DMA in the
+      // wait it places before the bias's first use)
+      if constexpr (SW) swap_bias(p, en0, wn, lane, sbias);
+      else bias = tile_bias(p, en0, wn, lane);
+    } else {
+      asm volatile("" : "+v"(bias));  // bias landed long ago (the main loop drained vmcnt): no waits below
+    }
+    if constexpr (SW && (EF & EF_BIAS) != 0 && !MX) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(sbias[j]));
     }
@@ -1165,24 +1345,26 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p) {
     };
     if (EPI_OVL) next_prologue();
     if constexpr (SW) {
-      char* slot = smem + EPI_OFF + wave * EPI16_FLOATS * 4;
+      char* slot = epi_base;
       if (full_tile) epilogue_bf16s<EF, ACT, true>(p, acc, slot, em0, en0, ebatch, wm, wn, lane, sbias);
       else epilogue_bf16s<EF, ACT, false>(p, acc, slot, em0, en0, ebatch, wm, wn, lane, sbias);
     } else {
-      if (full_tile) epilogue_8ph<EF, ACT, true>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias);
-      else epilogue_8ph<EF, ACT, false>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias);
+      const Q8Out* q8 = MX && mx.q8.q ? &mx.q8 : nullptr;
+      if (full_tile) epilogue_8ph<EF, ACT, true>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias, q8);
+      else epilogue_8ph<EF, ACT, false>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias, q8);
     }
     if (!EPI_OVL) next_prologue();
     if (!more) break;
     vb = vb_next;
     extra = (EPI_OVL && full_tile) ? 1 : 0;
-    if constexpr (EF >= 0 && (EF & EF_BIAS) != 0) {
+    if constexpr (EF >= 0 && (EF & EF_BIAS) != 0 && !MX) {
       if constexpr (SW) swap_bias(p, n0, wn, lane, sbias);
       else bias = tile_bias(p, n0, wn, lane);
     }
   }
 #undef STAGE_A
 #undef STAGE_B
+#undef STAGE_S
 #undef STAGE_PROLOGUE
 #undef STE_LDS_SYNC
 }
@@ -1233,14 +1415,15 @@ int launch_8ph(const ste_gemm_args& a, hipStream_t s) {
   if constexpr (AK == A_KC && BK == B_KC) {                                                           \
     if (ef == (E) && a.act == (ACT)) {                                                                \
       hipLaunchKernelGGL((gemm_8ph_kernel<A_KC, B_KC, (E), (ACT)>), dim3(grid), dim3(ph8::NT),        \
-                         ph8::LDS_BYTES, s, a);                                                       \
+                         ph8::LDS_BYTES, s, a, Mx8Args{});                                            \
       STE_CHECK_LAUNCH();                                                                             \
       return 0;                                                                                       \
     }                                                                                                 \
   }
   STE_EPI_SPECS(STE_TRY)
 #undef STE_TRY
-  hipLaunchKernelGGL((gemm_8ph_kernel<A_KC, B_KC, EF_GENERIC, 0>), dim3(grid), dim3(ph8::NT), ph8::LDS_BYTES, s, a);
+  hipLaunchKernelGGL((gemm_8ph_kernel<A_KC, B_KC, EF_GENERIC, 0>), dim3(grid), dim3(ph8::NT), ph8::LDS_BYTES, s, a,
+                     Mx8Args{});
   STE_CHECK_LAUNCH();
   return 0;
 }
@@ -1603,6 +1786,44 @@ extern "C" int ste_mx8_quant(const void* x, int64_t ldx, int rows, int K, void* 
   return 0;
 }
 
+namespace {
+// STE_MX8_8PH=0: the single-stage gemm_mx8_kernel for every shape (A/B runs)
+bool mx8_8ph_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("STE_MX8_8PH");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+// MX-fp8 on the persistent 8-phase kernel: the e4m3 operands passed as bf16 pairs (K, lda, ldb
+// halved), compile-time epilogues for the Conformer forward GEMMs without an fp8 output copy,
+// the run-time epilogue (which also writes the fp8 copy) otherwise
+int launch_mx8_8ph(const ste_gemm_args& a8, const Mx8Args& mx, hipStream_t s) {
+  ste_gemm_args a = a8;
+  a.K = a8.K / 2;
+  a.lda = a8.lda / 2;
+  a.ldb = a8.ldb / 2;
+  const int nb = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  const int grid = nb < num_cus() ? nb : num_cus();
+  const int ef = epi_flags(a) | (mx.q8.q ? EF_Q8 : 0) | (a.C ? 0 : EF_NOC);
+#define STE_MX(E, ACT)                                                                                          \
+  if (ef == (E) && a.act == (ACT)) {                                                                            \
+    hipLaunchKernelGGL((gemm_8ph_kernel<true, true, (E), (ACT), true>), dim3(grid), dim3(ph8::NT), ph8::LDS_BYTES, \
+                       s, a, mx);                                                                               \
+    STE_CHECK_LAUNCH();                                                                                         \
+    return 0;                                                                                                   \
+  }
+  STE_MX(EF_BIAS | EF_CBF16, STE_ACT_NONE)                            /* QKV */
+  STE_MX(EF_CBF16, STE_ACT_NONE)                                      /* pointwise conv 1 */
+  STE_MX(EF_BIAS | EF_R, STE_ACT_NONE)                                /* O-proj, FFN out */
+  STE_MX(EF_BIAS | EF_C2 | EF_CBF16 | EF_Q8, STE_ACT_SWISH)           /* FFN in: bf16 + fp8 copies */
+  STE_MX(EF_BIAS | EF_C2 | EF_CBF16 | EF_Q8 | EF_NOC, STE_ACT_SWISH)  /* FFN in, frozen: fp8 copy only */
+#undef STE_MX
+  return -1;   // other epilogues: the single-stage kernel
+}
+}  // namespace
+
 extern "C" int ste_gemm_mx8(const ste_gemm_args* args, const void* a_scales, const void* b_scales, void* q_out,
                             void* q_scales, void* stream) {
   if (!args || !a_scales || !b_scales || (!args->C && !q_out) || (!q_out != !q_scales)) return STE_ERR_ARG;
@@ -1623,6 +1844,11 @@ extern "C" int ste_gemm_mx8(const ste_gemm_args* args, const void* a_scales, con
     return STE_ERR_SHAPE;
   const int nb = ((a.M + 255) / 256) * ((a.N + 255) / 256);
   const Q8Out q8o = {(uint8_t*)q_out, (uint8_t*)q_scales, a.N};
+  // the 8-phase kernel's fp8 copy is written per 32-column block of FULL 256-column tiles
+  if (mx8_8ph_on() && gemm_mode() == 2 && nb >= 240 && (!q_out || (a.N % 256) == 0)) {
+    const Mx8Args mx = {(const uint8_t*)a_scales, (const uint8_t*)b_scales, a.K / 32, a.K / 32, q8o};
+    if (launch_mx8_8ph(a, mx, (hipStream_t)stream) == 0) return 0;
+  }
   hipLaunchKernelGGL(gemm_mx8_kernel, dim3(nb), dim3(mx8::NT), mx8::LDS_BYTES, (hipStream_t)stream, a,
                      (const uint8_t*)a_scales, (const uint8_t*)b_scales, q8o);
   STE_CHECK_LAUNCH();

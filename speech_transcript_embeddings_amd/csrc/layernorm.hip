@@ -4,7 +4,10 @@
 // Rows are processed grid-stride; launches put ~16 waves on every CU so enough row loads
 // are in flight to cover HBM latency.  When column sums are wanted (dgamma/dbeta/dsum of
 // a trainable layer) the partials of a block are reduced through one reused LDS array and
-// flushed with one atomic per column per block; frozen layers compile without that LDS.
+// written to the caller's workspace, one row of partials per block, which ln_colsum_kernel
+// adds in block order (run-to-run deterministic, no same-address atomics); without a
+// workspace they are flushed with one atomic per column per block.  Frozen layers compile
+// without that LDS.
 #include "common.h"
 #include "../../include/ste.h"
 
@@ -232,7 +235,8 @@ STE_DEV void ln_bwd_row(const ste_ln_bwd_args& a, int row, int lane, float (&x)[
   }
 }
 
-// the block's column sums of one backward through one reused LDS array, one atomic per column
+// the block's column sums of one backward through one reused LDS array: into the workspace
+// (ws[k][block][col], summed by ln_colsum_kernel) or, without one, one atomic per column
 template <int MAXC>
 STE_DEV void ln_flush(const ste_ln_bwd_args& a, const LnAcc<MAXC>& acc, float (*red)[MAXC * 4 * 64], int lane,
                       int wid) {
@@ -245,6 +249,7 @@ STE_DEV void ln_flush(const ste_ln_bwd_args& a, const LnAcc<MAXC>& acc, float (*
 #pragma unroll
     for (int i = 0; i < MAXC * 4; ++i) red[wid][(i >> 2) * 256 + lane * 4 + (i & 3)] = src[i];
     __syncthreads();
+    float* part = a.ws ? a.ws + ((int64_t)k * gridDim.x + blockIdx.x) * a.cols : nullptr;
     for (int j = threadIdx.x; j < MAXC * 256; j += NT) {
       const int c = j >> 8, rem = j & 255;
       const int col = (c * 64 + (rem >> 2)) * 4 + (rem & 3);
@@ -252,8 +257,41 @@ STE_DEV void ln_flush(const ste_ln_bwd_args& a, const LnAcc<MAXC>& acc, float (*
       float sum = 0.f;
 #pragma unroll
       for (int w = 0; w < NT / 64; ++w) sum += red[w][j];
-      atomicAdd(outs[k] + col, sum);
+      if (part) part[col] = sum;
+      else atomicAdd(outs[k] + col, sum);
     }
+  }
+}
+
+// out_k[col] += Σ_block ws[k][block][col] in a fixed order (16 interleaved slices of the blocks,
+// then the slices in order): grid (ceil(cols / 64), 3), 1024 threads, 8 loads in flight per thread
+__global__ __launch_bounds__(1024) void ln_colsum_kernel(const float* __restrict__ ws, int nblk, int cols,
+                                                         float* dgamma, float* dbeta, float* dsum) {
+  float* const out = blockIdx.y == 0 ? dgamma : (blockIdx.y == 1 ? dbeta : dsum);
+  if (!out) return;  // uniform
+  __shared__ float red[16][64];
+  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + c;
+  float acc = 0.f;
+  if (col < cols) {
+    const float* p = ws + (int64_t)blockIdx.y * nblk * cols + col;
+    int b = sl;
+    for (; b + 7 * 16 < nblk; b += 8 * 16) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(b + 16 * u) * cols];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; b < nblk; b += 16) acc += p[(int64_t)b * cols];
+  }
+  red[sl][c] = acc;
+  __syncthreads();
+  if (sl == 0 && col < cols) {
+    float t = red[0][c];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t += red[k][c];
+    out[col] += t;
   }
 }
 
@@ -336,6 +374,16 @@ inline int grid_for(int rows, int cap = 1024) {
   int g = (rows + 3) / 4;
   return g < cap ? g : cap;
 }
+// column-sum launches: fewer, longer blocks (one partial row or one atomic per column per block)
+inline int grid_bwd(const ste_ln_bwd_args& a, bool reduce) { return grid_for(a.rows, reduce ? 512 : 1024); }
+inline bool ws_ok(const ste_ln_bwd_args& a, int nblk) {
+  return !a.ws || a.ws_floats >= 3 * (int64_t)nblk * a.cols;
+}
+inline void colsum(const ste_ln_bwd_args& a, int nblk, hipStream_t s) {
+  if (!a.ws || !(a.dgamma || a.dbeta || a.dsum)) return;
+  hipLaunchKernelGGL(ln_colsum_kernel, dim3((unsigned)((a.cols + 63) / 64), 3), dim3(1024), 0, s, (const float*)a.ws,
+                     nblk, a.cols, a.dgamma, a.dbeta, a.dsum);
+}
 
 }  // namespace
 
@@ -375,15 +423,26 @@ extern "C" int ste_layernorm_bwd_pair(const ste_ln_bwd_args* a, const ste_ln_bwd
   if ((a->act == STE_ACT_SWISH && !a->beta) || (b->act == STE_ACT_SWISH && !b->beta)) return STE_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const bool reduce = a->dgamma || a->dbeta || a->dsum || b->dgamma || b->dbeta || b->dsum;
-  const dim3 grid(grid_for(a->rows, reduce ? 512 : 1024));
+  // one grid for both: atomics as soon as either LN has no workspace
+  const bool use_ws = (a->ws || !(a->dgamma || a->dbeta || a->dsum)) && (b->ws || !(b->dgamma || b->dbeta || b->dsum));
+  const int nblk = grid_for(a->rows, reduce ? 512 : 1024);
+  if (reduce && use_ws && (!ws_ok(*a, nblk) || !ws_ok(*b, nblk))) return STE_ERR_ARG;
+  ste_ln_bwd_args aa = *a, bb = *b;
+  if (!use_ws) aa.ws = bb.ws = nullptr;
+  const dim3 grid(nblk);
   if (a->cols <= 256) {
-    if (reduce) hipLaunchKernelGGL((ln_bwd_pair_kernel<1, true>), grid, dim3(NT), 0, s, *a, *b);
-    else hipLaunchKernelGGL((ln_bwd_pair_kernel<1, false>), grid, dim3(NT), 0, s, *a, *b);
+    if (reduce) hipLaunchKernelGGL((ln_bwd_pair_kernel<1, true>), grid, dim3(NT), 0, s, aa, bb);
+    else hipLaunchKernelGGL((ln_bwd_pair_kernel<1, false>), grid, dim3(NT), 0, s, aa, bb);
   } else {
-    if (reduce) hipLaunchKernelGGL((ln_bwd_pair_kernel<4, true>), grid, dim3(NT), 0, s, *a, *b);
-    else hipLaunchKernelGGL((ln_bwd_pair_kernel<4, false>), grid, dim3(NT), 0, s, *a, *b);
+    if (reduce) hipLaunchKernelGGL((ln_bwd_pair_kernel<4, true>), grid, dim3(NT), 0, s, aa, bb);
+    else hipLaunchKernelGGL((ln_bwd_pair_kernel<4, false>), grid, dim3(NT), 0, s, aa, bb);
   }
   STE_CHECK_LAUNCH();
+  if (reduce && use_ws) {
+    colsum(bb, nblk, s);
+    colsum(aa, nblk, s);
+    STE_CHECK_LAUNCH();
+  }
   return 0;
 }
 
@@ -392,8 +451,9 @@ extern "C" int ste_layernorm_bwd(const ste_ln_bwd_args* a, void* stream) {
   if (a->act == STE_ACT_SWISH && !a->beta) return STE_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const bool reduce = a->dgamma || a->dbeta || a->dsum;
-  // column-sum launches pay one atomic per column per block: fewer, longer blocks
-  const dim3 grid(grid_for(a->rows, reduce ? 512 : 1024));
+  const int nblk = grid_bwd(*a, reduce);
+  if (reduce && !ws_ok(*a, nblk)) return STE_ERR_ARG;
+  const dim3 grid(nblk);
   if (a->cols <= 256) {
     if (reduce) hipLaunchKernelGGL((ln_bwd_kernel<1, true>), grid, dim3(NT), 0, s, *a);
     else hipLaunchKernelGGL((ln_bwd_kernel<1, false>), grid, dim3(NT), 0, s, *a);
@@ -402,5 +462,13 @@ extern "C" int ste_layernorm_bwd(const ste_ln_bwd_args* a, void* stream) {
     else hipLaunchKernelGGL((ln_bwd_kernel<4, false>), grid, dim3(NT), 0, s, *a);
   }
   STE_CHECK_LAUNCH();
+  if (reduce) {
+    colsum(*a, nblk, s);
+    STE_CHECK_LAUNCH();
+  }
   return 0;
+}
+
+extern "C" int64_t ste_layernorm_bwd_ws_floats(int rows, int cols) {
+  return rows <= 0 || cols <= 0 ? 0 : 3 * (int64_t)grid_for(rows, 512) * cols;
 }

@@ -249,6 +249,10 @@ def layernorm_fwd_pair(first: dict, second: dict):
     return (m1, r1), (m2, r2)
 
 
+# True: LayerNorm column sums through fp32 atomics (the library's workspace-free path; A/B and tests)
+LN_ATOMIC_COLSUMS = False
+
+
 def _ln_bwd_struct(dy, x, mean, rstd, gamma, beta=None, dx=None, dxb=None, dres=None, dgamma=None, dbeta=None,
                    row_scale=None, act=_lib.ACT_NONE, drop_p=0.0, seed=0, out_scale=1.0, in_drop_p=0.0, in_seed=0,
                    out_row_scale=None, dsum=None):
@@ -272,18 +276,25 @@ def _ln_bwd_struct(dy, x, mean, rstd, gamma, beta=None, dx=None, dxb=None, dres=
     a.drop_p, a.seed, a.out_scale = float(drop_p), int(seed) & (2**64 - 1), float(out_scale)
     a.in_drop_p, a.in_seed = float(in_drop_p), int(in_seed) & (2**64 - 1)
     a.out_row_scale, a.dsum = ptr(out_row_scale), ptr(dsum)
+    ws = None
+    if (dgamma is not None or dbeta is not None or dsum is not None) and not LN_ATOMIC_COLSUMS:
+        # per-block column partials, summed in a fixed order by the library (deterministic; the
+        # caching allocator reuses the block stream-ordered, so it may be dropped after the launch)
+        n = 3 * min((rows + 3) // 4, 512) * cols   # == ste_layernorm_bwd_ws_floats(rows, cols)
+        ws = torch.empty(n, device=x.device, dtype=F32)
+        a.ws, a.ws_floats = ptr(ws), n
     # algorithmic bytes: read dy, x (and dres), write dx / dxb, 8 B/row of statistics
     nbytes = rows * cols * ((dy.element_size() if dy is not None else 0) + x.element_size() +
                             (4 if dres is not None else 0) + (4 if dx is not None else 0) +
                             (2 if dxb is not None else 0)) + 8 * rows + 16 * cols
-    return a, nbytes
+    return a, nbytes, ws
 
 
 def layernorm_bwd(dy, x, mean, rstd, gamma, *, beta=None, dx=None, dxb=None, dres=None, dgamma=None, dbeta=None,
                   row_scale=None, act=_lib.ACT_NONE, drop_p=0.0, seed=0, out_scale=1.0, in_drop_p=0.0, in_seed=0,
                   out_row_scale=None, dsum=None):
-    a, nbytes = _ln_bwd_struct(dy, x, mean, rstd, gamma, beta, dx, dxb, dres, dgamma, dbeta, row_scale, act, drop_p,
-                               seed, out_scale, in_drop_p, in_seed, out_row_scale, dsum)
+    a, nbytes, _ws = _ln_bwd_struct(dy, x, mean, rstd, gamma, beta, dx, dxb, dres, dgamma, dbeta, row_scale, act,
+                                    drop_p, seed, out_scale, in_drop_p, in_seed, out_row_scale, dsum)
     _traced("layernorm_bwd", nbytes, lambda: call("ste_layernorm_bwd", C.byref(a), _s()))
     return dx, dxb
 
@@ -292,8 +303,8 @@ def layernorm_bwd_pair(first: dict, second: dict):
     """Backward of layernorm_fwd_pair in one pass (ste_layernorm_bwd_pair): `second` (the later
     LN, with its dy) runs first and its input gradient feeds `first` in registers (`first` has
     no dy; second's dx output is optional).  Keyword sets as layernorm_bwd."""
-    a, nb1 = _ln_bwd_struct(None, **first)
-    b, nb2 = _ln_bwd_struct(**second)
+    a, nb1, _wa = _ln_bwd_struct(None, **first)
+    b, nb2, _wb = _ln_bwd_struct(**second)
     _traced("layernorm_bwd", nb1 + nb2, lambda: call("ste_layernorm_bwd_pair", C.byref(a), C.byref(b), _s()))
 
 

@@ -114,7 +114,9 @@ def _mx8_dequant(q, sc):
     return v * torch.pow(2.0, e.double())
 
 
-@pytest.mark.parametrize("M,N,K", [(1000, 768, 1024), (4000, 3072, 1024), (2000, 1024, 4096), (300, 2048, 128)])
+# the last three have >= 240 256x256 tiles: the persistent 8-phase MX kernel (ragged M, N = 4096)
+@pytest.mark.parametrize("M,N,K", [(1000, 768, 1024), (4000, 3072, 1024), (2000, 1024, 4096), (300, 2048, 128),
+                                   (8000, 2048, 1024), (6000, 3072, 2048), (4100, 4096, 1024)])
 def test_gemm_mx8(ops, M, N, K):
     """MX-fp8 GEMM (config 5): exact on the dequantised operands (fp32 accumulation), quantiser
     bit-exact against torch's e4m3 cast with the same block scale, and a few % from bf16."""
@@ -445,6 +447,48 @@ def test_layernorm_many_rows_per_wave(ops, reduce):
     if reduce:
         assert rel_err(dg, gr.grad) < 1e-5
         assert rel_err(db, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("pair", [False, True])
+def test_layernorm_colsums_deterministic(ops, pair):
+    """Column sums (dgamma, dbeta, dsum) through the per-block workspace are run-to-run identical
+    (fixed-order block sum) and add into the outputs like the atomic path (+=), which they match to
+    fp32 rounding; single and chained-pair backward, c2-sized rows."""
+    torch.manual_seed(5)
+    rows, cols = 31936 // 4, 1024
+    x = torch.randn(rows, cols, device=DEV) * 1.5 + 0.3
+    g1, b1, g2, b2 = (torch.randn(cols, device=DEV) for _ in range(4))
+    y1 = torch.empty(rows, cols, device=DEV)
+    (ma, ra), (mb, rb) = ops.layernorm_fwd_pair(dict(x=x, gamma=g1, beta=b1, eps=1e-5, y=y1),
+                                                dict(gamma=g2, beta=b2, eps=1e-5,
+                                                     yb=torch.empty(rows, cols, device=DEV, dtype=torch.bfloat16)))
+    dy = torch.randn(rows, cols, device=DEV).bfloat16()
+    dres = torch.randn(rows, cols, device=DEV)
+
+    def run():
+        sums = [torch.full((cols,), 0.25, device=DEV) for _ in range(5)]   # += onto a non-zero start
+        dxb = torch.empty(rows, cols, device=DEV, dtype=torch.bfloat16)
+        if pair:
+            ops.layernorm_bwd_pair(dict(x=x, mean=ma, rstd=ra, gamma=g1, beta=b1, dxb=dxb, dgamma=sums[0],
+                                        dbeta=sums[1], dsum=sums[2]),
+                                   dict(dy=dy, x=y1, mean=mb, rstd=rb, gamma=g2, beta=b2, dres=dres, dgamma=sums[3],
+                                        dbeta=sums[4]))
+        else:
+            ops.layernorm_bwd(dy, y1, mb, rb, g2, beta=b2, dres=dres, dxb=dxb, dgamma=sums[3], dbeta=sums[4],
+                              dsum=sums[2])
+            sums = sums[2:]
+        return sums
+
+    first, second = run(), run()
+    for a_, b_ in zip(first, second):
+        assert torch.equal(a_, b_)
+    ops.LN_ATOMIC_COLSUMS = True
+    try:
+        atomic = run()
+    finally:
+        ops.LN_ATOMIC_COLSUMS = False
+    for a_, b_ in zip(first, atomic):
+        assert rel_err(a_, b_) < 1e-5
 
 
 @pytest.mark.parametrize("case", ["noreduce", "reduce", "frozen_second"])
