@@ -703,6 +703,24 @@ STE_DEV void glds_tile_piece(const bf16* base, int64_t ld, int bT, int r0, int T
   __builtin_amdgcn_global_load_lds((const void*)(base + (int64_t)(bT + src_row) * ld + ch * 8),
                                    (lds_void*)(tile + piece * 1024), 16, 0, 0);
 }
+// the dK/dV kernel's form: the source as a 32-bit byte offset from the wave-uniform base (saddr +
+// voffset DMA: one VGPR per piece instead of a 64-bit pointer) and the lane id regenerated by mbcnt
+// — that kernel sits at 256 VGPRs, and a hoisted lane-derived address spilled there is reloaded from
+// scratch right after the tile's DMA is issued, where hipcc then waits vmcnt(0) for that DMA (the
+// forward and dQ kernels keep the 64-bit form: measured 3-5 % faster there)
+STE_DEV int lane_now() {
+  int l = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  asm volatile("" : "+v"(l));
+  return l;
+}
+STE_DEV void glds_tile_piece32(const bf16* base, int64_t ld, int bT, int r0, int T, char* tile, int piece) {
+  const int lane = lane_now();
+  const int row = piece * 8 + (lane >> 3);
+  const int src_row = min(r0 + row, T - 1);
+  const int ch = (lane & 7) ^ (row & 7);
+  const uint32_t off = ((uint32_t)(bT + src_row) * (uint32_t)ld + (uint32_t)(ch * 8)) * 2u;
+  __builtin_amdgcn_global_load_lds((const void*)((const char*)base + off), (lds_void*)(tile + piece * 1024), 16, 0, 0);
+}
 STE_DEV void glds_mask(const int32_t* mask, int bT, int r0, int T, char* dst, int lane) {
   __builtin_amdgcn_global_load_lds((const void*)(mask + bT + min(r0 + lane, T - 1)), (lds_void*)dst, 4, 0, 0);
 }
@@ -1868,9 +1886,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel2_kernel(ste_attn_args 
     glds_tile_piece(Qb, a.ldq, bT, qb, T, buf, 2 * w + 1, lane);
     glds_tile_piece(dOb, a.lddo, bT, qb, T, buf + TILE, 2 * w, lane);
     glds_tile_piece(dOb, a.lddo, bT, qb, T, buf + TILE, 2 * w + 1, lane);
-    if (w < 2) {
-      const float* src = (w == 0 ? a.lse : a.delta) + rowbase + min(qb + lane, T - 1);
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(buf + 2 * TILE + w * 256), 4, 0, 0);
+    if (w < 2) {   // wave-uniform base + 32-bit lane offset (saddr DMA; no 64-bit address to keep live)
+      const char* base = (const char*)(w == 0 ? a.lse : a.delta);
+      const uint32_t off = (uint32_t)(rowbase + min(qb + lane_now(), T - 1)) * 4u;
+      __builtin_amdgcn_global_load_lds((const void*)(base + off), (lds_void*)(buf + 2 * TILE + w * 256), 4, 0, 0);
     }
   };
   issue(0);
@@ -2066,13 +2085,14 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
   auto issue = [&](int qt) {
     char* buf = sm + (qt & 1) * QD;
     const int qb = qt * TQ;
-    glds_tile_piece(Qb, a.ldq, bT, qb, T, buf, 2 * w, lane);
-    glds_tile_piece(Qb, a.ldq, bT, qb, T, buf, 2 * w + 1, lane);
-    glds_tile_piece(dOb, a.lddo, bT, qb, T, buf + TILE, 2 * w, lane);
-    glds_tile_piece(dOb, a.lddo, bT, qb, T, buf + TILE, 2 * w + 1, lane);
-    if (w < 2) {
-      const float* src = (w == 0 ? a.lse : a.delta) + rowbase + min(qb + lane, T - 1);
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(buf + 2 * TILE + w * 256), 4, 0, 0);
+    glds_tile_piece32(Qb, a.ldq, bT, qb, T, buf, 2 * w);
+    glds_tile_piece32(Qb, a.ldq, bT, qb, T, buf, 2 * w + 1);
+    glds_tile_piece32(dOb, a.lddo, bT, qb, T, buf + TILE, 2 * w);
+    glds_tile_piece32(dOb, a.lddo, bT, qb, T, buf + TILE, 2 * w + 1);
+    if (w < 2) {   // wave-uniform base + 32-bit lane offset (saddr DMA; no 64-bit address to keep live)
+      const char* base = (const char*)(w == 0 ? a.lse : a.delta);
+      const uint32_t off = (uint32_t)(rowbase + min(qb + lane_now(), T - 1)) * 4u;
+      __builtin_amdgcn_global_load_lds((const void*)(base + off), (lds_void*)(buf + 2 * TILE + w * 256), 4, 0, 0);
     }
   };
   issue(0);
@@ -2118,20 +2138,13 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
         for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sE, jt * 16, s, lane), qfr[s], acc);
         *reinterpret_cast<f32x4*>(qrow + jt * 16 + 4 * g) = acc;
       }
-      if (g == 0) {
-        elo[16 * w + li] = qrow[0] * c2;
-        ehi[16 * w + li] = qrow[nrel - 1] * c2;
+      if (g == 0) {   // (addresses from a regenerated lane id: see lane_now)
+        const int l16 = lane_now() & 15;
+        elo[16 * w + l16] = qrow[0] * c2;
+        ehi[16 * w + l16] = qrow[nrel - 1] * c2;
       }
     }
     __syncthreads();
-    // per-lane query vectors (queries 16n + 4g + r): -lse*log2e, delta, edge biases
-    f32x4 nl2[4], dlt[4], lsev[4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      lsev[n] = *reinterpret_cast<const f32x4*>(sL + 16 * n + 4 * g);
-      dlt[n] = *reinterpret_cast<const f32x4*>(sL + 64 + 16 * n + 4 * g);
-      nl2[n] = lsev[n] * -LOG2E;
-    }
     // Two 32-query halves u; per half: S and dP of both key groups from Q/dO fragments read once,
     // P and dS, then dV/dK from transposed Q/dO fragments read once for both key groups
 #pragma unroll
@@ -2154,6 +2167,22 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
           dp[gk][nn] = mfma16(da[1], vf[gk][1], dp[gk][nn]);
         }
       }
+      // the half's transposed Q/dO fragments for dV/dK, issued now: their latency hides under the
+      // S/dP MFMAs and the softmax (v3 read them per dt right before use: 8 exposed LDS round trips
+      // per tile); the per-query vectors are read per half instead of per tile to make room
+      bf16x8 trd[4], trq[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        trd[dt] = frag_tr_asm(tD, dt * 16, u, lane);
+        trq[dt] = frag_tr_asm(tQ, dt * 16, u, lane);
+      }
+      // per-lane query vectors (queries 16n + 4g + r): lse, delta
+      f32x4 lsev[2], dlt[2];
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) {
+        lsev[nn] = *reinterpret_cast<const f32x4*>(sL + 16 * (2 * u + nn) + 4 * g);
+        dlt[nn] = *reinterpret_cast<const f32x4*>(sL + 64 + 16 * (2 * u + nn) + 4 * g);
+      }
       bf16x8 pv[2], pk[2];
 #pragma unroll
       for (int gk = 0; gk < 2; ++gk) {
@@ -2163,43 +2192,42 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
 #pragma unroll
         for (int nn = 0; nn < 2; ++nn) {
           const int n = 2 * u + nn;
+          const f32x4 nl2 = lsev[nn] * -LOG2E;
           if (all_lo || all_hi) {
             const f32x4 eb = *reinterpret_cast<const f32x4*>((all_lo ? elo : ehi) + 16 * n + 4 * g);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r], c2, eb[r] + nl2[n][r]));
+            for (int r = 0; r < 4; ++r) sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r], c2, eb[r] + nl2[r]));
           } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int ql = 16 * n + 4 * g + r;
               int d = mykey - (qb + ql);
               d = med3i(d, -left, right);
-              sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r] + qet3[ql * QE3 + d + left], c2, nl2[n][r]));
+              sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r] + qet3[ql * QE3 + d + left], c2, nl2[r]));
             }
           }
           if (any_masked && kmask[gk]) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) sc[gk][nn][r] = lsev[n][r] == -INFINITY ? 1.0f / T : 0.f;
+            for (int r = 0; r < 4; ++r) sc[gk][nn][r] = lsev[nn][r] == -INFINITY ? 1.0f / T : 0.f;
           }
           if (qb + TQ > T) {  // last query tile: rows past T (copies of row T-1) add nothing
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (qb + 16 * n + 4 * g + r >= T) sc[gk][nn][r] = 0.f;
           }
-          dp[gk][nn] = sc[gk][nn] * (dp[gk][nn] - dlt[n]) * a.scale;   // dS * scale (for dK)
+          dp[gk][nn] = sc[gk][nn] * (dp[gk][nn] - dlt[nn]) * a.scale;   // dS * scale (for dK)
         }
         pv[gk] = pack_acc(sc[gk][0], sc[gk][1]);
         pk[gk] = pack_acc(dp[gk][0], dp[gk][1]);
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the asm transposed reads
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const bf16x8 trd = frag_tr_asm(tD, dt * 16, u, lane);
-        const bf16x8 trq = frag_tr_asm(tQ, dt * 16, u, lane);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int gk = 0; gk < 2; ++gk) {
-          dv[gk][dt] = mfma16(trd, pv[gk], dv[gk][dt]);
-          dk[gk][dt] = mfma16(trq, pk[gk], dk[gk][dt]);
+          dv[gk][dt] = mfma16(trd[dt], pv[gk], dv[gk][dt]);
+          dk[gk][dt] = mfma16(trq[dt], pk[gk], dk[gk][dt]);
         }
       }
     }

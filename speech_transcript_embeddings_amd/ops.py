@@ -249,8 +249,9 @@ def layernorm_fwd_pair(first: dict, second: dict):
     return (m1, r1), (m2, r2)
 
 
-# True: LayerNorm column sums through fp32 atomics (the library's workspace-free path; A/B and tests)
-LN_ATOMIC_COLSUMS = False
+# True: LayerNorm column sums through fp32 atomics (the library's workspace-free path; A/B and tests;
+# STE_LN_ATOMIC=1 sets it for a whole run)
+LN_ATOMIC_COLSUMS = os.environ.get("STE_LN_ATOMIC") == "1"
 
 
 def _ln_bwd_struct(dy, x, mean, rstd, gamma, beta=None, dx=None, dxb=None, dres=None, dgamma=None, dbeta=None,
