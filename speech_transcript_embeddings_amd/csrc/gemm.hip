@@ -1392,6 +1392,8 @@ int num_cus() {
   X(true, true, EF_BIAS | EF_R | EF_DROP, STE_ACT_NONE)      /* post-LN O-proj / FFN out + dropout */ \
   X(true, true, EF_BIAS | EF_C2 | EF_DROP | EF_CBF16, STE_ACT_GELU) /* wav2vec2 FFN in + act dropout */ \
   X(true, true, EF_BIAS | EF_CBF16, STE_ACT_GELU)                                     \
+  X(true, true, EF_BIAS | EF_C3, STE_ACT_NONE)               /* precise text QKV: fp32 + bf16 copy */ \
+  X(true, true, EF_BIAS | EF_C2 | EF_C3 | EF_CBF16, STE_ACT_GELU) /* precise text FFN in: h, h_lo, z */ \
   X(true, true, EF_BIAS | EF_R, STE_ACT_NONE)                /* FFN out, O-proj    */ \
   X(true, true, EF_BIAS | EF_CBF16, STE_ACT_NONE)            /* QKV                */ \
   X(true, true, EF_CBF16, STE_ACT_NONE)                      /* pointwise conv 1   */ \

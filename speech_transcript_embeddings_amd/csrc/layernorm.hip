@@ -109,15 +109,12 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(ste_ln_fwd_args a) {
   const int nwaves = gridDim.x * (NT / 64);
   LnParams<MAXC> pa;
   pa.load(a.gamma, a.beta, a.cols, lane);
-  // the next row's loads are issued before this row's reductions and stores (two rows in flight
-  // per wave: the kernel is latency-bound at one)
-  float v[MAXC * 4], nx[MAXC * 4];
-  if (wave < a.rows) load_row<MAXC>(a.x, a.x_bf16, a.ldx, wave, a.cols, lane, v);
+  // one row in flight per wave (the next-row prefetch the pair kernel uses measured 34.2 -> 34.8 us
+  // here at c2 rows: the single kernel already keeps ~16 waves per CU loading)
   for (int row = wave; row < a.rows; row += nwaves) {
-    if (row + nwaves < a.rows) load_row<MAXC>(a.x, a.x_bf16, a.ldx, row + nwaves, a.cols, lane, nx);
+    float v[MAXC * 4];
+    load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, v);
     ln_fwd_row<MAXC>(a, pa, row, lane, v);
-#pragma unroll
-    for (int i = 0; i < MAXC * 4; ++i) v[i] = nx[i];
   }
 }
 
@@ -303,40 +300,19 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
   const int nwaves = gridDim.x * (NT / 64);
   LnAcc<MAXC> acc;
   acc.zero();
-  if constexpr (REDUCE) {
-    LnParams<MAXC> pa;
-    pa.load(a.gamma, a.act == STE_ACT_SWISH ? a.beta : nullptr, a.cols, lane);
-    for (int row = wave; row < a.rows; row += nwaves) {
-      float x[MAXC * 4], g[MAXC * 4], dr[MAXC * 4];
-      load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, x);
-      load_row<MAXC>(a.dy, a.dy_bf16, a.lddy, row, a.cols, lane, g);
-      if (a.dres) load_row<MAXC>(a.dres, false, a.lddres, row, a.cols, lane, dr);
-      ln_bwd_row<MAXC, true>(a, row, lane, x, g, dr, &pa, acc);
-    }
-    ln_flush<MAXC>(a, acc, red, lane, wid);
-  } else {   // no column sums: registers for the next row's operands, issued one row ahead
-    float x[MAXC * 4], g[MAXC * 4], dr[MAXC * 4], nx[MAXC * 4], ng[MAXC * 4], nd[MAXC * 4];
-    if (wave < a.rows) {
-      load_row<MAXC>(a.x, a.x_bf16, a.ldx, wave, a.cols, lane, x);
-      load_row<MAXC>(a.dy, a.dy_bf16, a.lddy, wave, a.cols, lane, g);
-      if (a.dres) load_row<MAXC>(a.dres, false, a.lddres, wave, a.cols, lane, dr);
-    }
-    for (int row = wave; row < a.rows; row += nwaves) {
-      const int nrow = row + nwaves;
-      if (nrow < a.rows) {
-        load_row<MAXC>(a.x, a.x_bf16, a.ldx, nrow, a.cols, lane, nx);
-        load_row<MAXC>(a.dy, a.dy_bf16, a.lddy, nrow, a.cols, lane, ng);
-        if (a.dres) load_row<MAXC>(a.dres, false, a.lddres, nrow, a.cols, lane, nd);
-      }
-      ln_bwd_row<MAXC, false, true>(a, row, lane, x, g, dr, nullptr, acc);   // gamma re-read (L1): registers
-#pragma unroll
-      for (int i = 0; i < MAXC * 4; ++i) {
-        x[i] = nx[i];
-        g[i] = ng[i];
-        dr[i] = nd[i];
-      }
-    }
+  // gamma (beta) preloaded, one row in flight per wave, for both variants: issuing the next row's
+  // x / dy / dres a row ahead (round 3, a6ffbd2) raised the column-sum-free kernel to 154 VGPRs and
+  // 3 waves per SIMD and made it slower, 94.5 -> 126.2 us at c2 rows (2.3 % of the c2 step)
+  LnParams<MAXC> pa;
+  pa.load(a.gamma, a.act == STE_ACT_SWISH ? a.beta : nullptr, a.cols, lane);
+  for (int row = wave; row < a.rows; row += nwaves) {
+    float x[MAXC * 4], g[MAXC * 4], dr[MAXC * 4];
+    load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, x);
+    load_row<MAXC>(a.dy, a.dy_bf16, a.lddy, row, a.cols, lane, g);
+    if (a.dres) load_row<MAXC>(a.dres, false, a.lddres, row, a.cols, lane, dr);
+    ln_bwd_row<MAXC, true>(a, row, lane, x, g, dr, &pa, acc);
   }
+  if constexpr (REDUCE) ln_flush<MAXC>(a, acc, red, lane, wid);
 }
 
 // Backward of the forward pair, in reverse: LN_b's backward (a.dy ignored: its dy is b.dy)
