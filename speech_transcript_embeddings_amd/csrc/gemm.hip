@@ -1406,6 +1406,7 @@ int num_cus() {
   X(true, true, EF_Z | EF_CBF16, STE_ACT_SWISH_BWD)          /* frozen layer: no db */ \
   X(true, true, EF_Z | EF_CBF16, STE_ACT_GELU_BWD)                                    \
   X(true, true, EF_Z | EF_COLSUM | EF_DROP | EF_CBF16, STE_ACT_GELU_BWD) /* wav2vec2 act dropout */ \
+  X(true, true, EF_Z | EF_DROP | EF_CBF16, STE_ACT_GELU_BWD) /* frozen wav2vec2 layer, act dropout */ \
   X(false, false, 0, STE_ACT_NONE)                           /* dW split-K slabs   */
 
 template <bool A_KC, bool B_KC>
