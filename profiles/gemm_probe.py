@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None)
     ap.add_argument("--mx8", action="store_true")
+    ap.add_argument("--text", action="store_true")
     a = ap.parse_args()
     from speech_transcript_embeddings_amd import _lib, ops
     M = a.rows
@@ -60,6 +61,8 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / a.iters
 
+    if a.text:
+        return text_shapes(a, ops, timed, rnd, ws)
     if a.mx8:
         for name, (K, N, epi) in cases.items():
             if not epi.startswith("bias") or (a.only and not name.startswith(a.only)):
@@ -134,6 +137,42 @@ def main():
         out[name] = {"M": N, "N": K, "K": M, "kernel": ops.gemm_kernel_name(_dw_args(ops, dy, X, dw, ws)),
                      "ste_us": round(t_ste, 1), "ste_tflops": round(fl / t_ste / 1e6, 1),
                      "hipblaslt_us": round(t_blas, 1), "hipblaslt_tflops": round(fl / t_blas / 1e6, 1)}
+        print(json.dumps({name: out[name]}), flush=True)
+    print(json.dumps(out), flush=True)
+
+
+def text_shapes(a, ops, timed, rnd, ws):
+    """--text: the text encoder's N = 768 outputs at M = 8,192 rows (c2: 64 pairs x 2 x 64
+    tokens), 96 tiles of 256 x 256: the forward O-proj / FFN-out of the split-bf16 (precise)
+    forward (K doubled: [hi | lo]) and the QKV / FFN-in input gradients, each with the step's
+    epilogue, timed with and without the workspace (the few-tile split-K plan needs it).  Run
+    under STE_GEMM_MIN_TILES / STE_GEMM_FEW_SPLIT to compare the kernel choices."""
+    M, D = 8192, 768
+    dev = "cuda"
+    out = {"rows": M, "min_tiles": os.environ.get("STE_GEMM_MIN_TILES", "240"),
+           "few_split": os.environ.get("STE_GEMM_FEW_SPLIT", "1")}
+    res = rnd(M, D, dt=torch.float32)
+    bias = torch.randn(D, device=dev) * 0.1
+    for name, (K, epi) in {"o_fwd_precise": (2 * D, "BRD"), "ffn_out_fwd_precise": (8 * D, "BRD"),
+                           "dx_qkv": (3 * D, "R"), "dx_ffn_in": (4 * D, "R"), "dx_o": (D, "bf16")}.items():
+        A = rnd(M, K)
+        W = rnd(D, K, sc=0.02)
+        if epi == "BRD":
+            kw = dict(bias=bias, residual=res, drop_p=0.1, seed=7)
+            o = torch.empty(M, D, device=dev)
+        elif epi == "R":
+            kw = dict(residual=res)
+            o = torch.empty(M, D, device=dev)
+        else:
+            kw = {}
+            o = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+        ref = ops.linear(A, W, out=torch.empty_like(o), **kw).float()
+        t0 = timed(lambda: ops.linear(A, W, out=o, **kw))
+        t1 = timed(lambda: ops.linear(A, W, out=o, ws=ws, **kw))
+        err = ((o.float() - ref).abs().max() / ref.abs().max()).item()
+        fl = 2.0 * M * D * K
+        out[name] = {"K": K, "epilogue": epi, "no_ws_us": round(t0, 1), "no_ws_tflops": round(fl / t0 / 1e6, 1),
+                     "ws_us": round(t1, 1), "ws_tflops": round(fl / t1 / 1e6, 1), "ws_vs_no_ws_rel": err}
         print(json.dumps({name: out[name]}), flush=True)
     print(json.dumps(out), flush=True)
 

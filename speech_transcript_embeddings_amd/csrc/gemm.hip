@@ -155,6 +155,47 @@ struct Mx8Args {
   Q8Out q8;
 };
 
+// The generic epilogue of one lane's 8 columns of one row (run-time feature switches): used by
+// the fp32-staged tile epilogue and by the split-K reduction below.
+STE_DEV void epi_apply8(const ste_gemm_args& p, f32x8 v, int row, int col, bool full, int nval, f32x8 bias,
+                        uint32_t thresh, float inv_keep, int64_t offC, int64_t offR, Csum& csum, const Q8Out* q8,
+                        int lane) {
+  v = (v + bias) * p.alpha;
+  if (p.act >= STE_ACT_SWISH && p.act <= STE_ACT_RELU) {
+    if (p.C2) st8((bf16*)p.C2 + offC + (int64_t)row * p.ldc2 + col, true, v, full, nval);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act);
+  } else if (p.act >= STE_ACT_SWISH_BWD) {
+    const f32x8 z = ld8((const bf16*)p.Z + offC + (int64_t)row * p.ldz + col, true, full, nval);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= act_grad(z[e], p.act);
+  }
+  if (p.drop_p > 0.f) {
+    const uint64_t base = (uint64_t)row * (uint64_t)p.drop_ld + (uint64_t)col;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= drop_scale(p.seed, base + e, thresh, inv_keep);
+  }
+  if (p.row_scale) v = v * p.row_scale[row];
+  if (!full) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) if (e >= nval) v[e] = 0.f;
+  }
+  if (p.colsum) {
+    csum.lo += f32x4{v[0], v[1], v[2], v[3]};
+    csum.hi += f32x4{v[4], v[5], v[6], v[7]};
+  }
+  if (p.R) {
+    const char* rp = (const char*)p.R + (offR + (int64_t)row * p.ldr + col) * (p.r_bf16 ? 2 : 4);
+    v += ld8(rp, p.r_bf16, full, nval);
+  }
+  char* cp = (char*)p.C + (offC + (int64_t)row * p.ldc + col) * (p.c_bf16 ? 2 : 4);
+  if (p.beta != 0.f) v += ld8(cp, p.c_bf16, full, nval) * p.beta;
+  if (q8) mx8_block_store(v, q8->q + (int64_t)row * q8->ldq + col, q8->s + (int64_t)row * (q8->ldq >> 5) + (col >> 5),
+                          lane);
+  if (p.C) st8(cp, p.c_bf16, v, full, nval);
+  if (p.C3) st8((bf16*)p.C3 + offC + (int64_t)row * p.ldc3 + col, true, p.c3_lo ? lo8(v) : v, full, nval);
+}
+
 STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, int row0, int col0, int col1,
                            int batch, int lane, Csum& csum, int ld = EPI_LD, bool swz16 = false,
                            const Q8Out* q8 = nullptr) {
@@ -178,41 +219,8 @@ STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, 
       s0 = s1;
       s1 = t;
     }
-    f32x8 v = f32x8{s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-    v = (v + bias) * p.alpha;
-    if (p.act >= STE_ACT_SWISH && p.act <= STE_ACT_RELU) {
-      if (p.C2) st8((bf16*)p.C2 + offC + (int64_t)row * p.ldc2 + col, true, v, full, nval);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act);
-    } else if (p.act >= STE_ACT_SWISH_BWD) {
-      const f32x8 z = ld8((const bf16*)p.Z + offC + (int64_t)row * p.ldz + col, true, full, nval);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= act_grad(z[e], p.act);
-    }
-    if (p.drop_p > 0.f) {
-      const uint64_t base = (uint64_t)row * (uint64_t)p.drop_ld + (uint64_t)col;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= drop_scale(p.seed, base + e, thresh, inv_keep);
-    }
-    if (p.row_scale) v = v * p.row_scale[row];
-    if (!full) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) if (e >= nval) v[e] = 0.f;
-    }
-    if (p.colsum) {
-      csum.lo += f32x4{v[0], v[1], v[2], v[3]};
-      csum.hi += f32x4{v[4], v[5], v[6], v[7]};
-    }
-    if (p.R) {
-      const char* rp = (const char*)p.R + (offR + (int64_t)row * p.ldr + col) * (p.r_bf16 ? 2 : 4);
-      v += ld8(rp, p.r_bf16, full, nval);
-    }
-    char* cp = (char*)p.C + (offC + (int64_t)row * p.ldc + col) * (p.c_bf16 ? 2 : 4);
-    if (p.beta != 0.f) v += ld8(cp, p.c_bf16, full, nval) * p.beta;
-    if (q8) mx8_block_store(v, q8->q + (int64_t)row * q8->ldq + col, q8->s + (int64_t)row * (q8->ldq >> 5) + (col >> 5),
-                            lane);
-    if (p.C) st8(cp, p.c_bf16, v, full, nval);
-    if (p.C3) st8((bf16*)p.C3 + offC + (int64_t)row * p.ldc3 + col, true, p.c3_lo ? lo8(v) : v, full, nval);
+    epi_apply8(p, f32x8{s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]}, row, col, full, nval, bias, thresh,
+               inv_keep, offC, offR, csum, q8, lane);
   }
 }
 
@@ -1058,16 +1066,17 @@ STE_DEV void vm_wait8(int extra) {
 }
 
 // Operands of batch entry `batch` and its K-tile count.  Split-K slab launches (ste_gemm's
-// weight-gradient plan: A_KC = B_KC = false, batch = slab) mark themselves with ws_bytes =
+// weight-gradient plan, A_KC = B_KC = false, and the few-tile epilogue plan, k-contiguous; batch = slab) mark themselves with ws_bytes =
 // -(rem + 1), a field the kernel never reads otherwise: the K/64 - S·Kc K-tiles that do not
 // divide over the S slabs go one each to slabs 0..rem-1 (slab s starts at K-tile
 // s·Kc + min(s, rem)), so no remainder launch is needed.
+template <bool A_KC, bool B_KC>
 STE_DEV void operand_bases(const ste_gemm_args& p, int batch, const bf16*& A, const bf16*& B, int& nk) {
   if (p.ws_bytes < 0) {
     const int kc = p.K / 64, rem = (int)(-p.ws_bytes - 1);
     const int64_t k0 = ((int64_t)batch * kc + (batch < rem ? batch : rem)) * 64;
-    A = (const bf16*)p.A + k0 * p.lda;
-    B = (const bf16*)p.B + k0 * p.ldb;
+    A = (const bf16*)p.A + k0 * (A_KC ? 1 : p.lda);
+    B = (const bf16*)p.B + k0 * (B_KC ? 1 : p.ldb);
     nk = kc + (batch < rem ? 1 : 0);
     return;
   }
@@ -1100,7 +1109,7 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p, M
   int m0 = tm * 256, n0 = tn * 256;
   const bf16* A;
   const bf16* B;
-  operand_bases(p, batch, A, B, nk);
+  operand_bases<A_KC, B_KC>(p, batch, A, B, nk);
 #define STAGE_A(t, h) \
   stage_half<A_KC, 64, MX>(A, p.lda, m0, p.M, (t) * 64, h, smem + ((t) & 1) * BUF + (h) * HALF, wave, lane)
 #define STAGE_B(t, h) \
@@ -1339,7 +1348,7 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p, M
         map_tile_bid(xcd_remap(vb_next, total), num_m, num_n, batch, tm, tn);
         m0 = tm * 256;
         n0 = tn * 256;
-        operand_bases(p, batch, A, B, nk);
+        operand_bases<A_KC, B_KC>(p, batch, A, B, nk);
         STAGE_PROLOGUE();
       }
     };
@@ -1407,6 +1416,7 @@ int num_cus() {
   X(true, true, EF_Z | EF_CBF16, STE_ACT_GELU_BWD)                                    \
   X(true, true, EF_Z | EF_COLSUM | EF_DROP | EF_CBF16, STE_ACT_GELU_BWD) /* wav2vec2 act dropout */ \
   X(true, true, EF_Z | EF_DROP | EF_CBF16, STE_ACT_GELU_BWD) /* frozen wav2vec2 layer, act dropout */ \
+  X(true, true, 0, STE_ACT_NONE)                             /* few-tile split-K slabs */ \
   X(false, false, 0, STE_ACT_NONE)                           /* dW split-K slabs   */
 
 template <bool A_KC, bool B_KC>
@@ -1460,6 +1470,49 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ 
   }
 }
 
+// Few-tile split-K: C = epilogue(sum_s ws[s]) for the forward / input-gradient GEMMs whose
+// output is too narrow to fill the CUs with 256x256 tiles (the text encoder's N = 768 outputs
+// at M = 8,192: 96 tiles).  The slabs are summed in slab order (run-to-run identical) and the
+// generic epilogue (bias, activation, Z, dropout, row scale, residual, beta, C2 / C3) applied
+// per 8 columns, exactly as the tile epilogue would.  No column sums (plan excludes them).
+__global__ __launch_bounds__(256) void splitk_epi_kernel(ste_gemm_args p, const float* __restrict__ ws, int S) {
+  const int n8 = p.N >> 3;
+  const int64_t total = (int64_t)p.M * n8;
+  const int64_t slab = (int64_t)p.M * p.N;
+  const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
+  const float inv_keep = p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f;
+  Csum csum;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / n8), col = (int)(i - (int64_t)row * n8) * 8;
+    const float* w = ws + (int64_t)row * p.N + col;
+    f32x4 lo = *reinterpret_cast<const f32x4*>(w), hi = *reinterpret_cast<const f32x4*>(w + 4);
+    for (int k = 1; k < S; ++k) {
+      lo += *reinterpret_cast<const f32x4*>(w + k * slab);
+      hi += *reinterpret_cast<const f32x4*>(w + k * slab + 4);
+    }
+    const f32x8 bias = p.bias ? ld8(p.bias + col, false, true, 8) : f32x8{};
+    epi_apply8(p, f32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}, row, col, true, 8, bias, thresh,
+               inv_keep, 0, 0, csum, nullptr, 0);
+  }
+}
+
+// Few-tile plan: k-contiguous operands, one output image, no column sums, N % 8 == 0, K a
+// multiple of 64 with >= 16 K-tiles per slab pair, fewer 256x256 tiles than CUs / 2: S = 2
+// slabs (2 x tiles workgroups).  STE_GEMM_FEW_SPLIT=0 disables it (A/B).
+int few_split(const ste_gemm_args& a) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("STE_GEMM_FEW_SPLIT");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!on || !a.a_kc || !a.b_kc || !a.ws || a.batch != 1 || a.colsum) return 0;
+  if ((a.N & 7) || (a.K & 63) || a.K / 64 < 32 || a.M < 2048) return 0;
+  const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  if (tiles * 2 > num_cus()) return 0;
+  if (2 * (int64_t)a.M * a.N * 4 > a.ws_bytes) return 0;
+  return 2;
+}
+
 // Weight-gradient plan: S K-slabs of Kc (or Kc + 1: the K/64 - S·Kc leftover tiles, one each
 // to the first slabs) 64-deep tiles on the 8-phase kernel with both operands k-major; only a
 // ragged K % 64 tail goes to the small kernel.
@@ -1504,12 +1557,21 @@ int launch_big(const ste_gemm_args& a, hipStream_t s) {
   return 0;
 }
 
-bool big_ok(const ste_gemm_args& a) {
+bool big_ok_shape(const ste_gemm_args& a) {
   if (a.K % big::BK) return false;
   if (!a.a_kc || a.M < 8) return false;                 // dW reductions stay on the small kernel
   if (!a.b_kc && (a.N % 8)) return false;
+  return true;
+}
+bool big_ok(const ste_gemm_args& a) {
+  if (!big_ok_shape(a)) return false;
   const long tiles = (long)((a.M + 255) / 256) * ((a.N + 255) / 256) * a.batch;
-  return tiles >= 240;
+  static int min_tiles = -1;   // STE_GEMM_MIN_TILES: A/B of the small-kernel threshold
+  if (min_tiles < 0) {
+    const char* e = getenv("STE_GEMM_MIN_TILES");
+    min_tiles = e ? atoi(e) : 240;
+  }
+  return tiles >= min_tiles;
 }
 
 }  // namespace
@@ -1532,6 +1594,7 @@ extern "C" int ste_gemm_kernel(const ste_gemm_args* args) {
   if (a.batch <= 0) a.batch = 1;
   const int variant = (a.a_kc ? 0 : 2) + (a.b_kc ? 0 : 1);
   if (gemm_mode() == 2 && splitk_plan(a).S > 0) return STE_GEMM_KERNEL_SPLITK + variant;
+  if (gemm_mode() == 2 && few_split(a) && big_ok_shape(a)) return STE_GEMM_KERNEL_SPLITK + variant;
   if (gemm_mode() > 0 && big_ok(a)) return (gemm_mode() == 2 ? STE_GEMM_KERNEL_8PH : STE_GEMM_KERNEL_BIG) + variant;
   return STE_GEMM_KERNEL_SMALL + variant;
 }
@@ -1614,6 +1677,25 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
       }
       return 0;
     }
+  }
+  if (mode == 2 && few_split(a) && big_ok_shape(a)) {
+    const int S = few_split(a);
+    ste_gemm_args g = a;
+    const int nk_all = a.K / 64;
+    g.K = (nk_all / S) * 64;
+    g.batch = S;
+    g.ws = nullptr;
+    g.ws_bytes = -(int64_t)(nk_all - S * (nk_all / S) + 1);
+    g.bias = nullptr; g.C2 = nullptr; g.C3 = nullptr; g.R = nullptr; g.Z = nullptr; g.colsum = nullptr;
+    g.row_scale = nullptr; g.act = 0; g.drop_p = 0.f;
+    g.C = a.ws; g.ldc = a.N; g.strideC = (int64_t)a.M * a.N; g.c_bf16 = 0;
+    g.alpha = 1.f; g.beta = 0.f;
+    if (int e = launch_8ph<true, true>(g, s)) return e;
+    const int64_t work = (int64_t)a.M * (a.N / 8);
+    const int blocks = (int)((work + 255) / 256 < 4096 ? (work + 255) / 256 : 4096);
+    hipLaunchKernelGGL(splitk_epi_kernel, dim3(blocks), dim3(256), 0, s, a, (const float*)a.ws, S);
+    STE_CHECK_LAUNCH();
+    return 0;
   }
   if (mode > 0 && big_ok(a)) {
     if (mode == 2) return a.b_kc ? launch_8ph<true, true>(a, s) : launch_8ph<true, false>(a, s);

@@ -115,7 +115,9 @@ class Engine:
     def _dx(self, dy, wname, fused=1, **kw):
         """dX = dY·W of an encoder Linear on the KC-KC GEMM with the cached k-contiguous Wᵀ
         (ParamStore.wt): 15-20 % faster than reading W k-major through transposing LDS reads,
-        and bit-identical to it (same reduction order)."""
+        and bit-identical to it (same reduction order).  Outputs too narrow to fill the CUs with
+        256x256 tiles (the text encoder's N = 768) take ste_gemm's few-tile split-K plan."""
+        kw.setdefault("ws", self.ws)   # narrow outputs (text N = 768) run split-K through it
         return ops.linear(dy, self.s.wt(wname, fused), **kw)
 
     def _db(self, x, bname, fused=1):
@@ -572,7 +574,7 @@ class Engine:
         ops.linear(x1s, s.w2(pre + nm["fi"] + ".weight"), s.p(pre + nm["fi"] + ".bias"), act=ACT_GELU, pre_out=zt,
                    drop_p=act_p, seed=_site_seed(seed, 4), out=hs_[:, :F_], out_bf16_copy=hs_[:, F_:], copy_lo=True)
         y2 = ops.linear(hs_, s.w2(pre + nm["fo"] + ".weight"), s.p(pre + nm["fo"] + ".bias"), residual=x1, drop_p=hp,
-                        seed=_site_seed(seed, 3))
+                        seed=_site_seed(seed, 3), ws=self.ws)   # 96 output tiles: few-tile split-K
         x2 = self._e(M, D)
         x2s = self._e(M, 2 * D, dtype=BF16)
         sv["st2"] = self._ln(y2, pre + nm["ln2"], eps, y=x2, yb=x2s[:, :D], ylo=x2s[:, D:])

@@ -107,6 +107,47 @@ def test_gemm_dw_splitk(ops, M, N, K, ws_mb):
     assert (kern >= 12) == (K >= 16 * 64), kern
 
 
+@pytest.mark.parametrize("M,K", [(8192, 6144),   # text FFN-out, split-bf16 forward: 96 tiles, 2 x 48 K-tiles
+                                 (8192, 2304),   # text QKV input gradient into the residual gradient
+                                 (4000, 2112)])  # ragged M; 33 K-tiles: slab 0 takes the leftover one
+def test_gemm_few_tile_splitk(ops, M, K):
+    """Outputs too narrow for the CUs (N = 768, <= 128 tiles of 256x256) with a workspace run as 2
+    K-slabs on the 8-phase kernel + a reduction that applies the generic epilogue: same results
+    as the fp32 reference and the dropout mask of the tile epilogue (same hash of row, col)."""
+    from speech_transcript_embeddings_amd import _lib
+    torch.manual_seed(K)
+    N = 768
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    b = torch.randn(N, device=DEV)
+    r = torch.randn(M, N, device=DEV)
+    ws = torch.empty(80 << 18, device=DEV)
+    mm = x.float() @ w.float().t()
+    seed, p = 99, 0.1
+    idx = (np.arange(M)[:, None] * N + np.arange(N)[None, :]).astype(np.uint64)
+    dmask = torch.from_numpy(drop_scale(seed, idx, p)).to(DEV)
+    # bias + residual + dropout, fp32 out (the post-LN FFN-out / O-proj)
+    y = ops.linear(x, w, b, residual=r, drop_p=p, seed=seed, ws=ws)
+    assert rel_err(y, (mm + b) * dmask + r) < 1e-5
+    y0 = ops.linear(x, w, b, residual=r, drop_p=p, seed=seed)          # no workspace: one-slab kernel
+    assert torch.equal((y - r) == 0, (y0 - r) == 0)                     # identical dropout mask
+    assert rel_err(y, y0) < 1e-6
+    # GELU with the bf16 pre-activation, bf16 out; activation backward with Z; beta accumulate
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    h = ops.linear(x, w, b, act=_lib.ACT_GELU, pre_out=pre, out_bf16=True, ws=ws)
+    assert rel_err(h, F.gelu(mm + b)) < 5e-3 and rel_err(pre, mm + b) < 5e-3
+    z = torch.randn(M, N, device=DEV).bfloat16()
+    c = torch.randn(M, N, device=DEV)
+    c0 = c.clone()
+    ops.linear(x, w, None, act=_lib.ACT_GELU_BWD, z=z, beta=1.0, out=c, alpha=0.5, ws=ws)
+    zf = z.float()
+    gd = torch.special.ndtr(zf) + zf * torch.exp(-0.5 * zf * zf) / math.sqrt(2 * math.pi)
+    assert rel_err(c, 0.5 * mm * gd + c0) < 1e-5
+    args = _lib.GemmArgs(M=M, N=N, K=K, batch=1, a_kc=1, b_kc=1, A=1, B=1, C=1, ldc=N, lda=K, ldb=K, alpha=1.0,
+                         ws=1, ws_bytes=ws.numel() * 4)
+    assert int(_lib.fn("ste_gemm_kernel")(__import__("ctypes").byref(args))) == 12   # split-K family
+
+
 def _mx8_dequant(q, sc):
     """e4m3 bytes + E8M0 block scales -> fp64 (torch's float8_e4m3fn is the OCP encoding)."""
     v = q.view(torch.float8_e4m3fn).double()
