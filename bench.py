@@ -249,7 +249,9 @@ def hbm_traffic(kernel):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json")))
     if not files:
         return None, None
-    d = json.load(open(files[-1]))
+    # rocprofv3 names the 8-phase GEMM with its MX template argument (", false>"); the library's
+    # kernel query omits it
+    d = {k.replace(", false>", ">"): v for k, v in json.load(open(files[-1])).items()}
     if kernel not in d:
         return None, os.path.relpath(files[-1], ROOT)
     return d[kernel]["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
