@@ -50,6 +50,10 @@ extern "C" {
  * 256x256 tiles cannot fill the chip is split along K into S slabs
  * (S·M·N·4 <= ws_bytes), each reduced by one 256x256 MFMA workgroup, then
  * C = beta·C + alpha·Σ slabs.  ws may be NULL (no split).
+ * Narrow outputs (a_kc=1, b_kc=1, batch 1, no colsum, N%8==0, K%64==0 with >= 32
+ * K-tiles, at most CUs/2 tiles of 256x256, 2·M·N·4 <= ws_bytes): given ws, the
+ * product runs as 2 K-slabs and a reduction that applies the full epilogue (same
+ * results and dropout mask as without ws, up to fp32 summation order).
  */
 enum {
   STE_ACT_NONE = 0,
@@ -79,7 +83,7 @@ typedef struct {
   float alpha, beta;
   int act;
   float drop_p; uint64_t seed; int64_t drop_ld;
-  float* ws; int64_t ws_bytes;      /* split-K workspace for weight gradients (optional) */
+  float* ws; int64_t ws_bytes;      /* split-K workspace: weight gradients, narrow outputs (optional) */
   int c3_lo;                        /* C3 <- bf16(v - bf16(v)), the low half, instead of bf16(v):
                                        with C = bf16(v) the two make the [hi | lo] split image the
                                        next precise-forward GEMM reads (see ste_split_bf16) */
