@@ -293,24 +293,27 @@ __global__ __launch_bounds__(1024) void ln_colsum_kernel(const float* __restrict
 }
 
 template <int MAXC, bool REDUCE>
-__global__ __launch_bounds__(NT) void ln_bwd_kernel(ste_ln_bwd_args a) {
+__global__ __launch_bounds__(NT, REDUCE ? 3 : 1) void ln_bwd_kernel(ste_ln_bwd_args a) {
   __shared__ float red[REDUCE ? NT / 64 : 1][REDUCE ? MAXC * 4 * 64 : 1];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wave = blockIdx.x * (NT / 64) + wid;
   const int nwaves = gridDim.x * (NT / 64);
   LnAcc<MAXC> acc;
   acc.zero();
-  // gamma (beta) preloaded, one row in flight per wave, for both variants: issuing the next row's
-  // x / dy / dres a row ahead (round 3, a6ffbd2) raised the column-sum-free kernel to 154 VGPRs and
-  // 3 waves per SIMD and made it slower, 94.5 -> 126.2 us at c2 rows (2.3 % of the c2 step)
+  // one row in flight per wave: issuing the next row's x / dy / dres a row ahead (round 3,
+  // a6ffbd2) raised the column-sum-free kernel to 154 VGPRs and 3 waves per SIMD and made it
+  // slower, 94.5 -> 126.2 us at c2 rows (2.3 % of the c2 step).  gamma (beta) preloaded without
+  // column sums; with them gamma is read where used (L1-resident) instead, which with the 48
+  // accumulators keeps the kernel at 3 waves per SIMD (<= 168 VGPRs) rather than 2 (180)
   LnParams<MAXC> pa;
-  pa.load(a.gamma, a.act == STE_ACT_SWISH ? a.beta : nullptr, a.cols, lane);
+  if constexpr (!REDUCE) pa.load(a.gamma, a.act == STE_ACT_SWISH ? a.beta : nullptr, a.cols, lane);
   for (int row = wave; row < a.rows; row += nwaves) {
     float x[MAXC * 4], g[MAXC * 4], dr[MAXC * 4];
     load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, x);
     load_row<MAXC>(a.dy, a.dy_bf16, a.lddy, row, a.cols, lane, g);
     if (a.dres) load_row<MAXC>(a.dres, false, a.lddres, row, a.cols, lane, dr);
-    ln_bwd_row<MAXC, true>(a, row, lane, x, g, dr, &pa, acc);
+    if constexpr (REDUCE) ln_bwd_row<MAXC, false, true>(a, row, lane, x, g, dr, nullptr, acc);
+    else ln_bwd_row<MAXC, true>(a, row, lane, x, g, dr, &pa, acc);
   }
   if constexpr (REDUCE) ln_flush<MAXC>(a, acc, red, lane, wid);
 }
@@ -351,7 +354,11 @@ inline int grid_for(int rows, int cap = 1024) {
   return g < cap ? g : cap;
 }
 // column-sum launches: fewer, longer blocks (one partial row or one atomic per column per block)
-inline int grid_bwd(const ste_ln_bwd_args& a, bool reduce) { return grid_for(a.rows, reduce ? 512 : 1024); }
+// (the single column-sum kernel runs 3 waves per SIMD: 768 blocks = 3 per CU; the pair's 2: 512)
+constexpr int LN_REDUCE_BLOCKS = 768, LN_PAIR_REDUCE_BLOCKS = 512;
+inline int grid_bwd(const ste_ln_bwd_args& a, bool reduce) {
+  return grid_for(a.rows, reduce ? LN_REDUCE_BLOCKS : 1024);
+}
 inline bool ws_ok(const ste_ln_bwd_args& a, int nblk) {
   return !a.ws || a.ws_floats >= 3 * (int64_t)nblk * a.cols;
 }
@@ -401,7 +408,7 @@ extern "C" int ste_layernorm_bwd_pair(const ste_ln_bwd_args* a, const ste_ln_bwd
   const bool reduce = a->dgamma || a->dbeta || a->dsum || b->dgamma || b->dbeta || b->dsum;
   // one grid for both: atomics as soon as either LN has no workspace
   const bool use_ws = (a->ws || !(a->dgamma || a->dbeta || a->dsum)) && (b->ws || !(b->dgamma || b->dbeta || b->dsum));
-  const int nblk = grid_for(a->rows, reduce ? 512 : 1024);
+  const int nblk = grid_for(a->rows, reduce ? LN_PAIR_REDUCE_BLOCKS : 1024);
   if (reduce && use_ws && (!ws_ok(*a, nblk) || !ws_ok(*b, nblk))) return STE_ERR_ARG;
   ste_ln_bwd_args aa = *a, bb = *b;
   if (!use_ws) aa.ws = bb.ws = nullptr;
@@ -446,5 +453,5 @@ extern "C" int ste_layernorm_bwd(const ste_ln_bwd_args* a, void* stream) {
 }
 
 extern "C" int64_t ste_layernorm_bwd_ws_floats(int rows, int cols) {
-  return rows <= 0 || cols <= 0 ? 0 : 3 * (int64_t)grid_for(rows, 512) * cols;
+  return rows <= 0 || cols <= 0 ? 0 : 3 * (int64_t)grid_for(rows, LN_REDUCE_BLOCKS) * cols;
 }

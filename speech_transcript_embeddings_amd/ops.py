@@ -196,6 +196,17 @@ def linear_dw(dy, x, **kw):
 
 
 # -------------------------------------------------------------- LayerNorm
+_LN_WS = {}
+
+
+def _ln_ws_floats(rows, cols):
+    """ste_layernorm_bwd_ws_floats (cached per shape)."""
+    n = _LN_WS.get((rows, cols))
+    if n is None:
+        n = _LN_WS[(rows, cols)] = int(_lib.fn("ste_layernorm_bwd_ws_floats")(rows, cols))
+    return n
+
+
 def _ln_fwd_struct(x, gamma, beta, eps, y=None, yb=None, mean=None, rstd=None, row_scale=None, act=_lib.ACT_NONE,
                    drop_p=0.0, seed=0, q8=None, rows=None, cols=None, ylo=None):
     """-> (LnFwdArgs, mean, rstd, algorithmic bytes).  x may be None (pair kernels: the second
@@ -281,7 +292,7 @@ def _ln_bwd_struct(dy, x, mean, rstd, gamma, beta=None, dx=None, dxb=None, dres=
     if (dgamma is not None or dbeta is not None or dsum is not None) and not LN_ATOMIC_COLSUMS:
         # per-block column partials, summed in a fixed order by the library (deterministic; the
         # caching allocator reuses the block stream-ordered, so it may be dropped after the launch)
-        n = 3 * min((rows + 3) // 4, 512) * cols   # == ste_layernorm_bwd_ws_floats(rows, cols)
+        n = _ln_ws_floats(rows, cols)
         ws = torch.empty(n, device=x.device, dtype=F32)
         a.ws, a.ws_floats = ptr(ws), n
     # algorithmic bytes: read dy, x (and dres), write dx / dxb, 8 B/row of statistics
