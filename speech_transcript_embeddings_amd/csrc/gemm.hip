@@ -1513,6 +1513,23 @@ int few_split(const ste_gemm_args& a) {
   return 2;
 }
 
+// Batched weight gradients (both operands k-major, batch > 1: the wav2vec2 conv stack's per-clip
+// dW slabs over strided views, K = frames of one clip, usually ragged): the 8-phase kernel over
+// the whole-64 part of K (the batch fills the chip), the K % 64 tail accumulated by the small
+// kernel.  Plain alpha/beta epilogue only.
+bool batched_dw_ok(const ste_gemm_args& a) {
+  static int on = -1;   // STE_GEMM_BATCHED_DW=0: the small kernel (A/B)
+  if (on < 0) {
+    const char* e = getenv("STE_GEMM_BATCHED_DW");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!on || a.a_kc || a.b_kc || a.batch < 2) return false;
+  if (a.bias || a.C2 || a.C3 || a.R || a.Z || a.colsum || a.row_scale || a.act || a.drop_p > 0.f) return false;
+  if ((a.M & 7) || (a.N & 7) || a.M < 256 || a.N < 256 || a.K < 1024) return false;
+  const long tiles = (long)((a.M + 255) / 256) * ((a.N + 255) / 256) * a.batch;
+  return tiles >= 240;
+}
+
 // Weight-gradient plan: S K-slabs of Kc (or Kc + 1: the K/64 - S·Kc leftover tiles, one each
 // to the first slabs) 64-deep tiles on the 8-phase kernel with both operands k-major; only a
 // ragged K % 64 tail goes to the small kernel.
@@ -1595,6 +1612,7 @@ extern "C" int ste_gemm_kernel(const ste_gemm_args* args) {
   const int variant = (a.a_kc ? 0 : 2) + (a.b_kc ? 0 : 1);
   if (gemm_mode() == 2 && splitk_plan(a).S > 0) return STE_GEMM_KERNEL_SPLITK + variant;
   if (gemm_mode() == 2 && few_split(a) && big_ok_shape(a)) return STE_GEMM_KERNEL_SPLITK + variant;
+  if (gemm_mode() == 2 && batched_dw_ok(a)) return STE_GEMM_KERNEL_8PH + variant;
   if (gemm_mode() > 0 && big_ok(a)) return (gemm_mode() == 2 ? STE_GEMM_KERNEL_8PH : STE_GEMM_KERNEL_BIG) + variant;
   return STE_GEMM_KERNEL_SMALL + variant;
 }
@@ -1677,6 +1695,21 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
       }
       return 0;
     }
+  }
+  if (mode == 2 && batched_dw_ok(a)) {
+    ste_gemm_args g = a;
+    const int64_t kdone = (int64_t)(a.K / 64) * 64;
+    g.K = (int)kdone;
+    if (int e = launch_8ph<false, false>(g, s)) return e;
+    if (kdone < a.K) {  // ragged tail: += on the small kernel, per batch entry
+      ste_gemm_args r = a;
+      r.K = (int)(a.K - kdone);
+      r.A = (const bf16*)a.A + kdone * a.lda;
+      r.B = (const bf16*)a.B + kdone * a.ldb;
+      r.beta = 1.f;
+      return launch_small<false, false>(r, s);
+    }
+    return 0;
   }
   if (mode == 2 && few_split(a) && big_ok_shape(a)) {
     const int S = few_split(a);

@@ -148,6 +148,31 @@ def test_gemm_few_tile_splitk(ops, M, K):
     assert int(_lib.fn("ste_gemm_kernel")(__import__("ctypes").byref(args))) == 12   # split-K family
 
 
+@pytest.mark.parametrize("B,To,k,st", [(24, 1100, 3, 2),    # 17 whole K-tiles + a 12-frame tail
+                                       (32, 1024, 2, 2)])   # K a multiple of 64: no tail launch
+def test_gemm_batched_dw_strided(ops, B, To, k, st):
+    """wav2vec2 conv-stack weight gradient: per-clip dW slabs dz_bᵀ·X_b over the strided im2col
+    view of each clip (both operands k-major, batch = clips) on the 8-phase kernel + the small
+    kernel's ragged-K tail, against fp32 per clip."""
+    from speech_transcript_embeddings_amd import _lib
+    torch.manual_seed(To)
+    cin, cout = 512, 512
+    Ti = (To - 1) * st + k
+    dz = torch.randn(B * To, cout, device=DEV).bfloat16()
+    hin = torch.randn(B * Ti, cin, device=DEV).bfloat16()
+    b = torch.as_strided(hin, (To, k * cin), (st * cin, 1))
+    part = torch.empty(B * cout, k * cin, device=DEV)
+    ops.gemm(dz, b, a_kc=False, b_kc=False, M=cout, N=k * cin, K=To, batch=B, stride_a=To * cout,
+             stride_b=Ti * cin, stride_c=cout * k * cin, out=part)
+    for i in (0, B // 2, B - 1):
+        xi = torch.as_strided(hin, (To, k * cin), (st * cin, 1), i * Ti * cin).float()
+        ref = dz[i * To:(i + 1) * To].float().t() @ xi
+        assert rel_err(part[i * cout:(i + 1) * cout], ref) < 1e-5, i
+    args = _lib.GemmArgs(M=cout, N=k * cin, K=To, batch=B, a_kc=0, b_kc=0, A=1, B=1, C=1, ldc=k * cin, lda=cout,
+                         ldb=st * cin, alpha=1.0)
+    assert int(_lib.fn("ste_gemm_kernel")(__import__("ctypes").byref(args))) == 8 + 3   # 8-phase, KM x KM
+
+
 def _mx8_dequant(q, sc):
     """e4m3 bytes + E8M0 block scales -> fp64 (torch's float8_e4m3fn is the OCP encoding)."""
     v = q.view(torch.float8_e4m3fn).double()
