@@ -50,7 +50,7 @@ extern "C" {
  * 256x256 tiles cannot fill the chip is split along K into S slabs
  * (S·M·N·4 <= ws_bytes), each reduced by one 256x256 MFMA workgroup, then
  * C = beta·C + alpha·Σ slabs.  ws may be NULL (no split).
- * Narrow outputs (a_kc=1, b_kc=1, batch 1, no colsum, N%8==0, K%64==0 with >= 32
+ * Narrow outputs (a_kc=1, b_kc=1, batch 1, no colsum, N%8==0, K%64==0 with >= 40
  * K-tiles, at most CUs/2 tiles of 256x256, 2·M·N·4 <= ws_bytes): given ws, the
  * product runs as 2 K-slabs and a reduction that applies the full epilogue (same
  * results and dropout mask as without ws, up to fp32 summation order).

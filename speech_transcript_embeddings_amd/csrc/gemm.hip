@@ -1497,7 +1497,8 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(ste_gemm_args p, const 
 }
 
 // Few-tile plan: k-contiguous operands, one output image, no column sums, N % 8 == 0, K a
-// multiple of 64 with >= 16 K-tiles per slab pair, fewer 256x256 tiles than CUs / 2: S = 2
+// multiple of 64 with >= 40 K-tiles (at 36 — the text QKV input gradient — the split only broke
+// even in isolation and its 2 x 25 MB of slabs still cost HBM time beside the audio stream), fewer 256x256 tiles than CUs / 2: S = 2
 // slabs (2 x tiles workgroups).  STE_GEMM_FEW_SPLIT=0 disables it (A/B).
 int few_split(const ste_gemm_args& a) {
   static int on = -1;
@@ -1506,7 +1507,7 @@ int few_split(const ste_gemm_args& a) {
     on = (e && e[0] == '0') ? 0 : 1;
   }
   if (!on || !a.a_kc || !a.b_kc || !a.ws || a.batch != 1 || a.colsum) return 0;
-  if ((a.N & 7) || (a.K & 63) || a.K / 64 < 32 || a.M < 2048) return 0;
+  if ((a.N & 7) || (a.K & 63) || a.K / 64 < 40 || a.M < 2048) return 0;
   const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
   if (tiles * 2 > num_cus()) return 0;
   if (2 * (int64_t)a.M * a.N * 4 > a.ws_bytes) return 0;

@@ -108,8 +108,8 @@ def test_gemm_dw_splitk(ops, M, N, K, ws_mb):
 
 
 @pytest.mark.parametrize("M,K", [(8192, 6144),   # text FFN-out, split-bf16 forward: 96 tiles, 2 x 48 K-tiles
-                                 (8192, 2304),   # text QKV input gradient into the residual gradient
-                                 (4000, 2112)])  # ragged M; 33 K-tiles: slab 0 takes the leftover one
+                                 (8192, 3072),   # text FFN-in input gradient into the residual gradient
+                                 (4000, 2624)])  # ragged M; 41 K-tiles: slab 0 takes the leftover one
 def test_gemm_few_tile_splitk(ops, M, K):
     """Outputs too narrow for the CUs (N = 768, <= 128 tiles of 256x256) with a workspace run as 2
     K-slabs on the 8-phase kernel + a reduction that applies the generic epilogue: same results
