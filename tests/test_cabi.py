@@ -66,6 +66,40 @@ def test_gemm_kernel_selection(lib):
     assert lib.fn("ste_gemm_kernel")(C.byref(a)) == 0
 
 
+def test_gemm_split_policies(lib):
+    """Host-side plan choice (no launch): the few-tile split-K of narrow outputs and the batched
+    k-major weight gradients on the 8-phase kernel (kernel ids: include/ste.h)."""
+    k = lib.fn("ste_gemm_kernel")
+    a = lib.GemmArgs()
+    # text FFN-out at c2, split-bf16 forward: 96 tiles, 96 K-tiles, workspace given -> 2 K-slabs
+    a.M, a.N, a.K, a.batch, a.a_kc, a.b_kc = 8192, 768, 6144, 1, 1, 1
+    a.ws, a.ws_bytes = 1, 80 << 20
+    assert k(C.byref(a)) == 12
+    a.ws, a.ws_bytes = None, 0                      # no workspace: the 128x128 kernel
+    assert k(C.byref(a)) == 0
+    a.ws, a.ws_bytes = 1, 2 * 8192 * 768 * 4 - 4    # workspace one float short of 2 slabs
+    assert k(C.byref(a)) == 0
+    a.ws_bytes = 80 << 20
+    a.K = 2304                                      # 36 K-tiles: below the plan's 40
+    assert k(C.byref(a)) == 0
+    a.K, a.colsum = 6144, 1                         # column sums are never split
+    assert k(C.byref(a)) == 0
+    a.colsum = None
+    a.M = 31936                                     # 375 tiles fill the chip: unsplit 8-phase
+    assert k(C.byref(a)) == 8
+    # wav2vec2 conv1 dW at b = 64: per-clip slabs, both operands k-major, ragged K -> 8-phase
+    b = lib.GemmArgs()
+    b.M, b.N, b.K, b.batch, b.a_kc, b.b_kc = 512, 1536, 15999, 64, 0, 0
+    assert k(C.byref(b)) == 11
+    buf = C.create_string_buffer(128)
+    lib.fn("ste_gemm_kernel_name")(C.byref(b), buf, 128)
+    assert buf.value == b"gemm_8ph_kernel<false, false, 0, 0>"
+    b.batch = 4                                     # 48 tiles: stays on the small kernel
+    assert k(C.byref(b)) == 3
+    b.batch, b.bias = 64, 1                         # any epilogue beyond alpha/beta: small kernel
+    assert k(C.byref(b)) == 3
+
+
 def test_argument_errors_return_status_without_launch(lib):
     """Shape/alignment contract violations come back as non-zero status (-> SteError), never a launch."""
     a = lib.GemmArgs()
