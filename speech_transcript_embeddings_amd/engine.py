@@ -117,8 +117,10 @@ class Engine:
         (ParamStore.wt): 15-20 % faster than reading W k-major through transposing LDS reads,
         and bit-identical to it (same reduction order).  Outputs too narrow to fill the CUs with
         256x256 tiles (the text encoder's N = 768) take ste_gemm's few-tile split-K plan."""
-        kw.setdefault("ws", self.ws)   # narrow outputs (text N = 768) run split-K through it
-        return ops.linear(dy, self.s.wt(wname, fused), **kw)
+        wt = self.s.wt(wname, fused)
+        if dy.shape[0] * wt.shape[0] <= 128 * 65536:   # <= 128 output tiles: the plan may apply
+            kw.setdefault("ws", self.ws)
+        return ops.linear(dy, wt, **kw)
 
     def _db(self, x, bname, fused=1):
         g = self.s.fused(bname, fused, "g") if fused > 1 else self.s.g(bname)
