@@ -1481,7 +1481,7 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(ste_gemm_args p, const 
   const int64_t slab = (int64_t)p.M * p.N;
   const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
   const float inv_keep = p.drop_p > 0.f ? 1.0f / (1.0f - p.drop_p) : 1.0f;
-  Csum csum;
+  Csum csum = {};   // unused: the plan excludes column sums
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int row = (int)(i / n8), col = (int)(i - (int64_t)row * n8) * 8;
     const float* w = ws + (int64_t)row * p.N + col;
