@@ -47,6 +47,7 @@ BF16_PEAK_TFLOPS = 2516.6          # MI355X dense bf16 MFMA (256 CU x 4096 FLOP/
 FP8_PEAK_TFLOPS = 5033.2           # dense MX-fp8 (scaled 16x16x128 f8f6f4: 2x the bf16 rate)
 HBM_PEAK_GBPS = 8000.0             # MI355X HBM3E
 GFLOP_PER_PAIR = {3: 1370.4, 5: 1429.5}   # SURVEY §8(d) algorithmic fwd+bwd FLOPs per pair (c2/c3, c4)
+GFLOP_C5_PER_PAIR = 5999.6                 # c5 shape, 30 s clips, every encoder layer trainable
 GFLOP_FWD_PER_PAIR = 641.8                 # SURVEY §8(d) forward only: 615.1 audio + 21.7 text + ≈5 heads
 
 
@@ -151,7 +152,6 @@ def cpu_baseline(args):
     cores = len(os.sched_getaffinity(0))
     omp = os.environ.get("OMP_NUM_THREADS")
     threads = min(cores, _cgroup_cpus() or cores, int(omp) if omp and omp.isdigit() else cores)
-    share = threads
     torch.set_num_threads(threads)
     cfg = R.ModelCfg(use_word_alignment=args.align, text_layers_to_unfreeze=args.unfreeze,
                      audio_layers_to_unfreeze=args.unfreeze)
@@ -217,11 +217,6 @@ def cpu_baseline(args):
     B = args.cpu_batch
     dt_c2 = timed(B, args.seconds, args.tokens)
     dt_c1 = timed(B, 2.0, 16) if not args.eval else None
-    dt_share = None
-    if share != threads:
-        torch.set_num_threads(share)
-        dt_share = timed(B, args.seconds, args.tokens)
-        torch.set_num_threads(threads)
     what = "forward-only evaluation step (numpy fbank + forward + loss, no_grad)" if args.eval else \
         "full train step incl. numpy fbank + clip + two-group AdamW"
     out = {"value": round(B / dt_c2, 4), "unit": "audio-text pairs/s", "cores": threads, "kind": "port",
@@ -231,10 +226,6 @@ def cpu_baseline(args):
                      f"batch {B}; 2 warm-up steps, median of {max(3, args.cpu_steps)} timed steps = {dt_c2:.2f} s/step; "
                      f"threads = every host core this job may use: min(len(os.sched_getaffinity(0)) = {cores}, the "
                      f"cgroup CPU quota, OMP_NUM_THREADS) = {threads} (BASELINE.md §3)"}
-    if dt_share is not None:
-        out["job_share"] = {"value": round(B / dt_share, 4), "unit": "audio-text pairs/s", "cores": share,
-                            "sample": f"the same c2 step at the job's CPU share (min(affinity, OMP_NUM_THREADS) = "
-                                      f"{share} threads), {dt_share:.2f} s/step (median)"}
     if dt_c1 is not None:
         out["c1"] = {"value": round(B / dt_c1, 4), "unit": "audio-text pairs/s",
                      "sample": f"c1 shapes: 2 s clips + 16-token transcripts, batch {B}, {dt_c1:.2f} s/step (median)"}
@@ -330,7 +321,7 @@ def main(argv=None):
                                    audio_embedding_dim=768 if raw else 1024)
     model.audio_cfg.layerdrop = 0.0
     step = TrainStep(model, warmup=100, total_steps=100000, accumulation_steps=acc,
-                     in_batch_weight=args.in_batch_weight)
+                     in_batch_weight=args.in_batch_weight, micro_batch=micro, max_text_length=args.tokens)
     nsamp, L = int(args.seconds * 16000), args.tokens
     # resident synthetic inputs, a different shard per rank and micro-batch
     data = [synthetic_batch(micro, nsamp, L, device=f"cuda:{local}", seed=k, rank=rank) for k in range(acc)]
@@ -422,6 +413,9 @@ def main(argv=None):
     known = args.seconds == 10.0 and args.tokens == 64 and args.freeze == "partial" and \
         (args.unfreeze, args.align) in ((3, False), (5, True))
     gflop = (GFLOP_FWD_PER_PAIR if args.eval else GFLOP_PER_PAIR[args.unfreeze]) if known else None
+    c5 = args.seconds == 30.0 and args.tokens == 64 and args.freeze == "none" and not args.align and not args.eval
+    if c5:
+        gflop = GFLOP_C5_PER_PAIR
     if raw:
         cname = "wav2vec2-base raw-waveform encoder (SURVEY §8f rank 4, not a BASELINE config)"
         gflop = None
@@ -454,6 +448,10 @@ def main(argv=None):
                                             ((1 + (nsamp - 400) // 160) + 1) // 2),
                    "seq_len_text": L, "parallelism": f"dp{world}"},
         "step_roofline_frac": round(pairs * gflop / (world * BF16_PEAK_TFLOPS * 1e3), 4) if gflop else None,
+        # c5 with --fp8: also against the dense MX-fp8 peak (839 pairs/s per GPU)
+        **({"step_roofline_frac_fp8_peak": round(pairs * gflop / (world * FP8_PEAK_TFLOPS * 1e3), 4)}
+           if (gflop and c5 and args.fp8) else {}),
+        "gflop_per_pair": gflop,
         "roofline": {"bound": "mfma", "kernel": dom, "launches_per_step": n_l // args.trace_steps,
                      "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,

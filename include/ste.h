@@ -123,6 +123,11 @@ int ste_gemm_kernel_name(const ste_gemm_args* args, char* buf, int len);
  * of the next MX-fp8 GEMM; args->C may then be NULL (no bf16/fp32 copy). */
 int ste_gemm_mx8(const ste_gemm_args* args, const void* a_scales, const void* b_scales, void* q_out, void* q_scales,
                  void* stream);
+/* Host-only plan query of ste_gemm_mx8 (no launch): 1 = the persistent 8-phase MX kernel
+ * (>= 240 output tiles, a compile-time epilogue, each operand's fp8 bytes M·lda and N·ldb below
+ * 4 GiB because its DMA sources are 32-bit offsets), 0 = the single-stage kernel (64-bit
+ * addressing, any shape).  q_out: whether an MX-fp8 output copy is requested. */
+int ste_gemm_mx8_kernel(const ste_gemm_args* args, int q_out);
 /* bf16 x [rows][K] (row stride ldx) -> e4m3 q [rows][K] and E8M0 scales [rows][K/32]:
  * scale 2^e, e = ceil(log2(amax/448)) per 32-element block (no saturation; zero blocks 2^-127). */
 int ste_mx8_quant(const void* x, int64_t ldx, int rows, int K, void* q, void* scales, void* stream);
@@ -160,7 +165,11 @@ int ste_layernorm_fwd(const ste_ln_fwd_args* a, void* stream);
  * dxb = bf16(dx * dropmask(drop_seed) * out_scale) (optional).
  * Column sums: with a workspace (ws, >= ste_layernorm_bwd_ws_floats(rows, cols) floats, ws_floats
  * its size) every block writes its partials there and a second launch adds them in a fixed
- * order — run-to-run deterministic, no same-address atomics; ws = NULL: fp32 atomics. */
+ * order — run-to-run deterministic, no same-address atomics; ws = NULL: fp32 atomics.
+ * With a workspace the final add is a plain read-modify-write: dgamma, dbeta and dsum must not
+ * alias each other, and no other launch may accumulate into them concurrently (one stream at a
+ * time); a workspace may be reused by later launches on the same stream, not shared across
+ * streams (nor between the two LayerNorms of a pair call). */
 typedef struct {
   int rows, cols;
   const void* dy; int64_t lddy; int dy_bf16;

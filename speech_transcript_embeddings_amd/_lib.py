@@ -134,6 +134,7 @@ _SIGS = {
     "ste_fbank": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p,
                           c_void_p]),
     "ste_gemm_mx8": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ste_gemm_mx8_kernel": (c_int, [C.POINTER(GemmArgs), c_int]),
     "ste_mx8_quant": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "ste_attn_pool_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -1918,6 +1918,33 @@ bool mx8_8ph_on() {
 // MX-fp8 on the persistent 8-phase kernel: the e4m3 operands passed as bf16 pairs (K, lda, ldb
 // halved), compile-time epilogues for the Conformer forward GEMMs without an fp8 output copy,
 // the run-time epilogue (which also writes the fp8 copy) otherwise
+#define STE_MX8_SPECS(X)                                                      \
+  X(EF_BIAS | EF_CBF16, STE_ACT_NONE)                            /* QKV */         \
+  X(EF_CBF16, STE_ACT_NONE)                                      /* pw conv 1 */   \
+  X(EF_BIAS | EF_R, STE_ACT_NONE)                                /* O, FFN out */  \
+  X(EF_BIAS | EF_C2 | EF_CBF16 | EF_Q8, STE_ACT_SWISH)           /* FFN in */      \
+  X(EF_BIAS | EF_C2 | EF_CBF16 | EF_Q8 | EF_NOC, STE_ACT_SWISH)  /* FFN in, frozen: fp8 copy only */
+
+int mx8_ef(const ste_gemm_args& a, bool q_out) { return epi_flags(a) | (q_out ? EF_Q8 : 0) | (a.C ? 0 : EF_NOC); }
+
+// Host-side plan: the persistent 8-phase MX kernel, or the single-stage gemm_mx8_kernel.  The
+// 8-phase kernel's operand and scale DMA sources are 32-bit byte offsets from the operand base
+// (stage_half<.., O32>, stage_scales), so each operand (fp8 bytes, M·lda / N·ldb) must stay
+// below 4 GiB; larger operands, other epilogues and shapes under 240 tiles take the single-stage
+// kernel (64-bit addressing)
+bool mx8_8ph_plan(const ste_gemm_args& a, bool q_out) {
+  if (!mx8_8ph_on() || gemm_mode() != 2) return false;
+  const int64_t nb = (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256);
+  if (nb < 240 || (q_out && (a.N % 256) != 0)) return false;   // fp8 copy per FULL 256-column tile
+  const uint64_t lim = 1ull << 32;
+  if ((uint64_t)a.M * (uint64_t)a.lda >= lim || (uint64_t)a.N * (uint64_t)a.ldb >= lim) return false;
+  const int ef = mx8_ef(a, q_out);
+#define STE_MX_MATCH(E, ACT) if (ef == (E) && a.act == (ACT)) return true;
+  STE_MX8_SPECS(STE_MX_MATCH)
+#undef STE_MX_MATCH
+  return false;
+}
+
 int launch_mx8_8ph(const ste_gemm_args& a8, const Mx8Args& mx, hipStream_t s) {
   ste_gemm_args a = a8;
   a.K = a8.K / 2;
@@ -1925,7 +1952,7 @@ int launch_mx8_8ph(const ste_gemm_args& a8, const Mx8Args& mx, hipStream_t s) {
   a.ldb = a8.ldb / 2;
   const int nb = ((a.M + 255) / 256) * ((a.N + 255) / 256);
   const int grid = nb < num_cus() ? nb : num_cus();
-  const int ef = epi_flags(a) | (mx.q8.q ? EF_Q8 : 0) | (a.C ? 0 : EF_NOC);
+  const int ef = mx8_ef(a, mx.q8.q != nullptr);
 #define STE_MX(E, ACT)                                                                                          \
   if (ef == (E) && a.act == (ACT)) {                                                                            \
     hipLaunchKernelGGL((gemm_8ph_kernel<true, true, (E), (ACT), true>), dim3(grid), dim3(ph8::NT), ph8::LDS_BYTES, \
@@ -1933,15 +1960,16 @@ int launch_mx8_8ph(const ste_gemm_args& a8, const Mx8Args& mx, hipStream_t s) {
     STE_CHECK_LAUNCH();                                                                                         \
     return 0;                                                                                                   \
   }
-  STE_MX(EF_BIAS | EF_CBF16, STE_ACT_NONE)                            /* QKV */
-  STE_MX(EF_CBF16, STE_ACT_NONE)                                      /* pointwise conv 1 */
-  STE_MX(EF_BIAS | EF_R, STE_ACT_NONE)                                /* O-proj, FFN out */
-  STE_MX(EF_BIAS | EF_C2 | EF_CBF16 | EF_Q8, STE_ACT_SWISH)           /* FFN in: bf16 + fp8 copies */
-  STE_MX(EF_BIAS | EF_C2 | EF_CBF16 | EF_Q8 | EF_NOC, STE_ACT_SWISH)  /* FFN in, frozen: fp8 copy only */
+  STE_MX8_SPECS(STE_MX)
 #undef STE_MX
   return -1;   // other epilogues: the single-stage kernel
 }
 }  // namespace
+
+extern "C" int ste_gemm_mx8_kernel(const ste_gemm_args* args, int q_out) {
+  if (!args) return STE_ERR_ARG;
+  return mx8_8ph_plan(*args, q_out != 0) ? 1 : 0;
+}
 
 extern "C" int ste_gemm_mx8(const ste_gemm_args* args, const void* a_scales, const void* b_scales, void* q_out,
                             void* q_scales, void* stream) {
@@ -1963,8 +1991,7 @@ extern "C" int ste_gemm_mx8(const ste_gemm_args* args, const void* a_scales, con
     return STE_ERR_SHAPE;
   const int nb = ((a.M + 255) / 256) * ((a.N + 255) / 256);
   const Q8Out q8o = {(uint8_t*)q_out, (uint8_t*)q_scales, a.N};
-  // the 8-phase kernel's fp8 copy is written per 32-column block of FULL 256-column tiles
-  if (mx8_8ph_on() && gemm_mode() == 2 && nb >= 240 && (!q_out || (a.N % 256) == 0)) {
+  if (mx8_8ph_plan(a, q_out != nullptr)) {
     const Mx8Args mx = {(const uint8_t*)a_scales, (const uint8_t*)b_scales, a.K / 32, a.K / 32, q8o};
     if (launch_mx8_8ph(a, mx, (hipStream_t)stream) == 0) return 0;
   }

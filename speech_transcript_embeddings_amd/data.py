@@ -155,6 +155,8 @@ def to_model_batch(batch, device="cuda", pad_value=1.0, non_blocking=True):
     feats, mask = ops.fbank(wav, lens, T, pad_value=pad_value, mask_mode=0)
     out["input_values"] = feats
     out["attention_mask_audio"] = mask
+    # host-known frame counts: SpecAugment's span sampling reads these instead of the device mask
+    out["audio_lengths"] = [num_frames(int(n)) for n in batch["lengths"].tolist()]
     return out
 
 

@@ -116,11 +116,10 @@ class Engine:
         """dX = dY·W of an encoder Linear on the KC-KC GEMM with the cached k-contiguous Wᵀ
         (ParamStore.wt): 15-20 % faster than reading W k-major through transposing LDS reads,
         and bit-identical to it (same reduction order).  Outputs too narrow to fill the CUs with
-        256x256 tiles (the text encoder's N = 768) take ste_gemm's few-tile split-K plan."""
-        wt = self.s.wt(wname, fused)
-        if dy.shape[0] * wt.shape[0] <= 128 * 65536:   # <= 128 output tiles: the plan may apply
-            kw.setdefault("ws", self.ws)
-        return ops.linear(dy, wt, **kw)
+        256x256 tiles (the text encoder's N = 768) take ste_gemm's few-tile split-K plan; the
+        workspace is always passed and the library decides (ste_gemm_kernel)."""
+        kw.setdefault("ws", self.ws)
+        return ops.linear(dy, self.s.wt(wname, fused), **kw)
 
     def _db(self, x, bname, fused=1):
         g = self.s.fused(bname, fused, "g") if fused > 1 else self.s.g(bname)
@@ -142,10 +141,12 @@ class Engine:
         from .modules import W2V2Config
         return isinstance(self.acfg, W2V2Config)
 
-    def audio_forward(self, feats, mask_i64, train, base_seed, ctx, save=True):
+    def audio_forward(self, feats, mask_i64, train, base_seed, ctx, save=True, lengths=None):
+        """lengths: host list of each clip's valid frames (None: read from mask_i64 when
+        SpecAugment needs them, one device->host sync)."""
         if self.raw_audio:
             from . import wav2vec2
-            return wav2vec2.forward(self, feats, mask_i64, train, base_seed, ctx, save)
+            return wav2vec2.forward(self, feats, mask_i64, train, base_seed, ctx, save, lengths=lengths)
         c = self.acfg
         b, T, fin = feats.shape
         M = b * T
@@ -162,11 +163,13 @@ class Engine:
         spec = None
         if train and getattr(self.m, "spec_augment", False) and c.mask_time_prob > 0:
             # SpecAugment (w2v:944-988): spans drawn on the host with numpy's global RNG exactly as
-            # transformers does (the frame counts cost one host sync, as in the reference)
-            from .specaug import compute_mask_indices
-            sm = compute_mask_indices((b, T), c.mask_time_prob, c.mask_time_length, mask_i64.sum(-1).tolist(),
-                                      c.mask_time_min_masks)
-            spec = torch.from_numpy(sm.astype("int32").reshape(-1)).to(self.s.device)
+            # transformers does, from the host-known clip lengths (TrainStep / to_model_batch pass
+            # them); only a caller with nothing but a device mask pays a device->host sync here
+            from .specaug import compute_mask_indices, upload_mask
+            if lengths is None:
+                lengths = mask_i64.sum(-1).tolist() if mask_i64 is not None else [T] * b
+            sm = compute_mask_indices((b, T), c.mask_time_prob, c.mask_time_length, lengths, c.mask_time_min_masks)
+            spec = upload_mask(sm, self.s.device)
             ops.spec_mask_fwd(x, spec, maskf, self.s.p("audio_encoder.masked_spec_embed"))
         ctx.update(a_b=b, a_T=T, a_maskf=maskf, a_mask32=mask32, a_xin=xin, a_a0=a0, a_st0=st0, a_spec=spec)
         xb = None
@@ -1012,9 +1015,16 @@ class Engine:
         else:
             th, thb = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx, save)
         amask = batch.get("attention_mask_audio")
+        # host-known clip lengths in the mask's units (fbank frames / raw samples), for SpecAugment's
+        # span sampling without a device sync: given by the caller, or summed from a host mask
+        alens = batch.get("audio_lengths")
+        if alens is None and amask is not None and amask.device.type == "cpu":
+            alens = amask.sum(-1).tolist()
+        if amask is not None and amask.device != self.s.device:
+            amask = amask.to(self.s.device, non_blocking=True)
         ah, ahb = self.audio_forward(batch["input_values"].contiguous(),
                                      None if amask is None else amask.contiguous(), train, _site_seed(base_seed, 3),
-                                     ctx, save)
+                                     ctx, save, lengths=None if alens is None else [int(n) for n in alens])
         if side is not None:
             main.wait_stream(side)
         ctx["_thb"], ctx["_ahb"] = thb, ahb

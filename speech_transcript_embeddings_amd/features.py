@@ -109,4 +109,7 @@ def custom_collate_fn(batch):
     out["input_values"] = padded
     out["attention_mask_audio"] = amask
     out["is_corrupted"] = torch.zeros(B, dtype=torch.long, device=dev)
+    # host list of each clip's frames (not a tensor: the reference's loop moves tensors only), so
+    # SpecAugment's span sampling needs no device->host sync once the mask is on the GPU
+    out["audio_lengths"] = [int(a.size(0)) for a in audios]
     return out

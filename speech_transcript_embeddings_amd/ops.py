@@ -265,9 +265,23 @@ def layernorm_fwd_pair(first: dict, second: dict):
 LN_ATOMIC_COLSUMS = os.environ.get("STE_LN_ATOMIC") == "1"
 
 
+_LN_WS_BUF = {}
+
+
+def _ln_ws(dev, rows, cols, slot):
+    """Column-partial workspace of a LayerNorm backward, cached per (stream, shape, slot): the
+    launches of one stream run in order, so consecutive backwards reuse one buffer (a pair
+    kernel's two LayerNorms take slots 0 and 1); concurrent streams get their own."""
+    key = (torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0, rows, cols, slot)
+    w = _LN_WS_BUF.get(key)
+    if w is None:
+        w = _LN_WS_BUF[key] = torch.empty(_ln_ws_floats(rows, cols), device=dev, dtype=F32)
+    return w
+
+
 def _ln_bwd_struct(dy, x, mean, rstd, gamma, beta=None, dx=None, dxb=None, dres=None, dgamma=None, dbeta=None,
                    row_scale=None, act=_lib.ACT_NONE, drop_p=0.0, seed=0, out_scale=1.0, in_drop_p=0.0, in_seed=0,
-                   out_row_scale=None, dsum=None):
+                   out_row_scale=None, dsum=None, _slot=0):
     """-> (LnBwdArgs, algorithmic bytes).  dy may be None (the first LN of a backward pair
     takes its gradient from the second one's, in registers)."""
     rows, cols = x.shape
@@ -290,11 +304,9 @@ def _ln_bwd_struct(dy, x, mean, rstd, gamma, beta=None, dx=None, dxb=None, dres=
     a.out_row_scale, a.dsum = ptr(out_row_scale), ptr(dsum)
     ws = None
     if (dgamma is not None or dbeta is not None or dsum is not None) and not LN_ATOMIC_COLSUMS:
-        # per-block column partials, summed in a fixed order by the library (deterministic; the
-        # caching allocator reuses the block stream-ordered, so it may be dropped after the launch)
-        n = _ln_ws_floats(rows, cols)
-        ws = torch.empty(n, device=x.device, dtype=F32)
-        a.ws, a.ws_floats = ptr(ws), n
+        # per-block column partials, summed in a fixed order by the library (deterministic)
+        ws = _ln_ws(x.device, rows, cols, _slot)
+        a.ws, a.ws_floats = ptr(ws), ws.numel()
     # algorithmic bytes: read dy, x (and dres), write dx / dxb, 8 B/row of statistics
     nbytes = rows * cols * ((dy.element_size() if dy is not None else 0) + x.element_size() +
                             (4 if dres is not None else 0) + (4 if dx is not None else 0) +
@@ -315,7 +327,7 @@ def layernorm_bwd_pair(first: dict, second: dict):
     """Backward of layernorm_fwd_pair in one pass (ste_layernorm_bwd_pair): `second` (the later
     LN, with its dy) runs first and its input gradient feeds `first` in registers (`first` has
     no dy; second's dx output is optional).  Keyword sets as layernorm_bwd."""
-    a, nb1, _wa = _ln_bwd_struct(None, **first)
+    a, nb1, _wa = _ln_bwd_struct(None, **first, _slot=1)
     b, nb2, _wb = _ln_bwd_struct(**second)
     _traced("layernorm_bwd", nb1 + nb2, lambda: call("ste_layernorm_bwd_pair", C.byref(a), C.byref(b), _s()))
 

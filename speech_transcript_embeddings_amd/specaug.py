@@ -13,6 +13,7 @@ masked_spec_embed (ste_spec_mask_bwd).
 from __future__ import annotations
 
 import numpy as np
+import torch
 
 
 def compute_mask_indices(shape, mask_prob: float, mask_length: int, input_lengths=None, min_masks: int = 0):
@@ -50,3 +51,13 @@ def compute_mask_indices(shape, mask_prob: float, mask_length: int, input_length
     spans = np.minimum(spans, seq - 1)
     np.put_along_axis(mask, spans, 1, -1)
     return mask
+
+
+def upload_mask(sm, device):
+    """bool [B, T] host mask -> int32 [B*T] on `device` through pinned memory, without blocking
+    the host on the device queue (the caching host allocator keeps the pinned block alive until
+    the copy has run)."""
+    host = torch.from_numpy(np.ascontiguousarray(sm, dtype=np.int32).reshape(-1))
+    if torch.device(device).type != "cuda":
+        return host.to(device)
+    return host.pin_memory().to(device, non_blocking=True)

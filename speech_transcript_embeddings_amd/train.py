@@ -201,11 +201,13 @@ class GradSync:
     table goes through the dense all-reduce instead.
     The list capacity, and with it the sparse-vs-dense choice, must be identical on every rank
     (one rank in all_gather while another is in all_reduce hangs the job), but ranks may hold
-    different token counts (a short last batch, length-bucketed padding).  plan_words(n_ids),
-    called when a step's final micro-batch starts, all-reduces (MAX) the count asynchronously
-    and copies the result to pinned host memory on a side stream; the text stage reads it
-    after waiting only for that copy (issued a whole forward + backward earlier), never for
-    the step's own kernels.
+    different token counts (a short last batch, length-bucketed padding).  The capacity is fixed
+    per run, never agreed per step: word_capacity = the most token ids one optimizer step can
+    carry (TrainStep: 2 x micro-batch x max_text_length x accumulation; the reference pads every
+    transcript to max_text_length, ref :838-851), or, when the caller cannot say, agreed once by
+    ensure_capacity() (a MAX all-reduce on the first step, before its kernels are queued).  A step
+    with more ids than the capacity raises.  So a step's backward holds no collective of its own
+    and no host wait.
     `finish()` waits for every collective (on the current stream) before clip + AdamW.
     """
 
@@ -216,14 +218,13 @@ class GradSync:
     # embedding: final at the very end); the text encoder (side stream, joined at the end)
     STAGES = ("heads", "audio_layers", "audio", "text")
 
-    def __init__(self, store, bucket_mb: int = 256, pad_id: int = 1):
+    def __init__(self, store, bucket_mb: int = 256, pad_id: int = 1, word_capacity: int | None = None):
         self.store = store
         self.bucket = max(1, bucket_mb * 1024 * 1024 // 4)
         self.pad_id = pad_id
         self.works = []
         self.sparse = None
-        self._plan = None
-        self._plan_stream = None
+        self.capacity = None if word_capacity is None else int(word_capacity)
         grad_slots = [sl for sl in store.slots.values() if sl.segment in ("enc", "head")]
 
         ordered = sorted(grad_slots, key=lambda x: x.offset)
@@ -287,43 +288,23 @@ class GradSync:
                     t.mul_(1.0 / ws)
                 self.works.append(dist.all_reduce(t, op=op, async_op=True))
 
-    def plan_words(self, n_ids: int):
-        """Start agreeing on the word-table exchange capacity (MAX of every rank's token count
-        this step, async); stage_done("text") reads it."""
-        self._plan = None
+    def ensure_capacity(self, n_ids: int) -> int:
+        """The run's word-table exchange capacity: the configured one, or (first call without one)
+        the MAX of every rank's n_ids, agreed once with a blocking all-reduce — called before a
+        step's kernels are queued, so it never stalls a backward.  Raises when a step carries more
+        ids than the capacity (every rank must use the same capacity)."""
         if not self.active() or self.words is None:
-            return
-        dev = self.store.device
-        if dist.get_backend() == "nccl" and dev.type == "cuda":
-            t = torch.tensor([int(n_ids)], dtype=torch.int64, device=dev)
-            work = dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=True)
-            if self._plan_stream is None:
-                self._plan_stream = torch.cuda.Stream(device=dev)
-            host = torch.empty(1, dtype=torch.int64, pin_memory=True)
-            with torch.cuda.stream(self._plan_stream):
-                work.wait()                       # this side stream (not the step's) waits for it
-                host.copy_(t, non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record()
-            self._plan = (ev, host, t)
-        else:                                     # gloo: host tensors, the wait is the collective's
-            t = torch.tensor([int(n_ids)], dtype=torch.int64)
-            self._plan = (dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=True), t, t)
-
-    def agreed_ids(self, n_ids: int) -> int:
-        """The rank-agreed token count of this step (plan_words), or n_ids without a plan."""
-        if self._plan is None:
             return int(n_ids)
-        waiter, host, _keep = self._plan
-        if isinstance(waiter, torch.cuda.Event):
-            waiter.synchronize()
-        else:
-            waiter.wait()
-        self._plan = None
-        n = int(host[0])
-        if n < n_ids:
-            raise RuntimeError(f"word-table capacity {n} < this rank's {n_ids} token ids: plan_words saw another count")
-        return n
+        if self.capacity is None:
+            dev = self.store.device
+            t = torch.tensor([int(n_ids)], dtype=torch.int64,
+                             device=dev if dist.get_backend() == "nccl" and dev.type == "cuda" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            self.capacity = int(t.item())
+        if n_ids > self.capacity:
+            raise RuntimeError(f"{n_ids} token ids in one step exceed the word-table exchange capacity "
+                               f"{self.capacity} (TrainStep(micro_batch=, max_text_length=) sets it)")
+        return self.capacity
 
     def _sparse_words(self, ids, cap_ids):
         st, sl = self.store, self.words
@@ -356,7 +337,7 @@ class GradSync:
             return
         self._reduce(self.ranges[stage])
         if stage == "text" and self.words is not None:
-            n = self.agreed_ids(ids.numel() if ids is not None else 0)
+            n = self.ensure_capacity(ids.numel() if ids is not None else 0)
             if ids is not None and self.sparse_pays(n):   # n, hence the choice, equal on every rank
                 self._sparse_words(ids, n)
             else:
@@ -396,6 +377,9 @@ class EmbeddingExchange:
     ranks before their L2-normalise backward.  With one process the same code runs without
     collectives (NB = B)."""
 
+    # tests: run the collective branches even on a one-rank group (the RCCL path on one GPU)
+    FORCE_COLLECTIVES = False
+
     def __init__(self, tau: float = 0.1, in_batch_weight: float = 0.0):
         self.tau, self.weight = float(tau), float(in_batch_weight)
         self.acc = None
@@ -408,11 +392,14 @@ class EmbeddingExchange:
             return dist.get_world_size(), dist.get_rank()
         return 1, 0
 
+    def _collective(self, ws):
+        return ws > 1 or (self.FORCE_COLLECTIVES and dist.is_available() and dist.is_initialized())
+
     def start(self, an, tn_all):
         ws, rank = self.world()
         B, P = an.shape
         NB = ws * B
-        if ws == 1:
+        if not self._collective(ws):
             self._pending = (an, tn_all, [], B, 1, 0)
             return
         A_g = torch.empty(NB, P, device=an.device, dtype=F32)
@@ -442,14 +429,15 @@ class EmbeddingExchange:
         ops.rowmat(dS, T_g[:NB], dan)                      # d a_i   += Σ_j dS_ij t_j
         dT = torch.zeros(NB, an.shape[1], device=an.device, dtype=F32)
         ops.rowmat(dS, an, dT, transpose_x=True)           # d t_j   += Σ_i dS_ij a_i (every rank's t_j)
-        if ws > 1:
+        if self._collective(ws):
             if dist.get_backend() == "gloo" and dT.is_cuda:   # gloo reduce-scatters host tensors only
                 mine = torch.empty(B, an.shape[1], dtype=F32)
-                dist.reduce_scatter_tensor(mine, dT.cpu(), op=dist.ReduceOp.SUM)
+                dist.reduce_scatter_tensor(mine, dT.cpu(), op=dist.ReduceOp.SUM, async_op=True).wait()
                 mine = mine.to(dT.device)
             else:
+                # RCCL: wait() only makes the current stream wait for the collective's stream
                 mine = e(B, an.shape[1])
-                dist.reduce_scatter_tensor(mine, dT, op=dist.ReduceOp.SUM)
+                dist.reduce_scatter_tensor(mine, dT, op=dist.ReduceOp.SUM, async_op=True).wait()
             ops.axpby(dtp, mine)
         else:
             ops.axpby(dtp, dT)
@@ -483,16 +471,18 @@ class EmbeddingExchange:
             if ws > 1:   # keep the collective matched with ranks that did accumulate
                 raise RuntimeError("epoch_metrics() before any finish() on this rank")
             return {}
+        a = self.acc.cpu().tolist()
         if ws > 1:
+            # the global loss sum is used for the returned value only: acc[5] keeps this rank's own
+            # sum, so a later call (reset=False, or accumulation continuing) never re-reduces a total
             lsum = self.acc[5:6].clone()
             if dist.get_backend() == "gloo" and lsum.is_cuda:
                 lsum = lsum.cpu()
             dist.all_reduce(lsum, op=dist.ReduceOp.SUM)
-            self.acc[5:6].copy_(lsum.to(self.acc.device))
-        if self.acc[4].item() == 0:
-            return {}
-        a = self.acc.cpu().tolist()
+            a[5] = float(lsum.item())
         n = a[4]
+        if n == 0:
+            return {}
         out = {"loss": a[5] / n, "clean_similarity": a[0] / n, "corrupt_similarity": a[1] / n,
                "similarity_gap": (a[0] - a[1]) / n, "pair_accuracy": a[2] / n, "in_batch_top1": a[3] / n,
                "samples": int(n)}
@@ -506,7 +496,7 @@ class TrainStep:
 
     def __init__(self, model: EnhancedAudioTextModel, lr=2.1e-3, warmup=100, total_steps=10000, temperature=0.1,
                  alignment_weight=0.5, corrupt_gamma=0.35, max_norm=1.0, pad_value=1.0, gather_embeddings=True,
-                 accumulation_steps=1, in_batch_weight=0.0):
+                 accumulation_steps=1, in_batch_weight=0.0, micro_batch=None, max_text_length=None):
         """accumulation_steps (ref train_epoch :1064-1117): each call is one micro-batch whose loss
         gradient is scaled by 1/accumulation_steps and summed into the flat gradient buffer; the
         data-parallel sync, clip, AdamW and scheduler step run on every accumulation_steps-th
@@ -516,14 +506,19 @@ class TrainStep:
         metrics); in_batch_weight > 0 adds its optional in-batch-negative InfoNCE term (0 keeps
         the reference's loss exactly).
         Data parallel: rank 0's layerdrop seed is broadcast so every rank drops the same Conformer
-        layers (tf:…wav2vec2_bert…:519-522 draws one number per layer per batch)."""
+        layers (tf:…wav2vec2_bert…:519-522 draws one number per layer per batch).  micro_batch and
+        max_text_length (the reference pads transcripts to it, ref :838-851) fix the word-table
+        exchange capacity (GradSync) up front; without them it is agreed once, on the first step."""
         self.model = model
         self.acc = max(1, int(accumulation_steps))
         self._micro = 0
         self._ids = []
         self.opt = FusedAdamW(model, lr=lr, max_norm=max_norm)
         self.sched = LinearWarmupSchedule(warmup, total_steps)
-        self.gradsync = GradSync(model.store, pad_id=model.text_cfg.pad_token_id)
+        cap = None
+        if micro_batch is not None and max_text_length is not None:
+            cap = 2 * int(micro_batch) * int(max_text_length) * self.acc   # clean + corrupted ids per window
+        self.gradsync = GradSync(model.store, pad_id=model.text_cfg.pad_token_id, word_capacity=cap)
         self.tau, self.aw, self.gamma = temperature, alignment_weight, corrupt_gamma
         self.pad_value = pad_value
         self.gather_embeddings = gather_embeddings or in_batch_weight > 0
@@ -552,14 +547,21 @@ class TrainStep:
             return wave_normalize(wav, lengths), mask
         n = int(wav.shape[1])
         T = ((1 + (n - 400) // 160) + 1) // 2
+        lengths = lengths.to(device=wav.device, dtype=torch.int32, non_blocking=True)
         return ops.fbank(wav, lengths, T, pad_value=self.pad_value, mask_mode=0)
 
     def __call__(self, wav, lengths, ids_pos, mask_pos, ids_neg, mask_neg):
-        """One micro-batch from raw 16 kHz waveforms (GPU fbank first)."""
+        """One micro-batch from raw 16 kHz waveforms (GPU fbank first).  lengths on the host (as a
+        DataLoader delivers them) also give SpecAugment its per-clip frame counts with no
+        device->host sync; on the device they are read back only if SpecAugment is on."""
+        host = lengths.tolist() if lengths.device.type == "cpu" else None
         feats, amask = self.features(wav, lengths)
-        return self.step_batch({"input_ids_pos": ids_pos, "attention_mask_pos": mask_pos, "input_ids_neg": ids_neg,
-                                "attention_mask_neg": mask_neg, "input_values": feats,
-                                "attention_mask_audio": amask})
+        batch = {"input_ids_pos": ids_pos, "attention_mask_pos": mask_pos, "input_ids_neg": ids_neg,
+                 "attention_mask_neg": mask_neg, "input_values": feats, "attention_mask_audio": amask}
+        if host is not None:
+            from .features import num_frames
+            batch["audio_lengths"] = host if self.model.engine.raw_audio else [num_frames(int(x)) for x in host]
+        return self.step_batch(batch)
 
     def step_batch(self, batch):
         """One micro-batch given the reference's collated batch dict (custom_collate_fn layout,
@@ -569,10 +571,10 @@ class TrainStep:
         st = m.store
         st.sync_shadow()
         eng = m.engine
-        if self._micro + 1 == self.acc:   # the window's last micro-batch: agree on the word-table
-            # exchange capacity now (async), a forward + backward before stage "text" needs it
+        if self._micro + 1 == self.acc:   # the window's last micro-batch: check the word-table exchange
+            # capacity (agreed once on the first step if not configured) before any kernel is queued
             n_ids = batch["input_ids_pos"].numel() + batch["input_ids_neg"].numel()
-            self.gradsync.plan_words(n_ids + sum(int(t.numel()) for t in (self._ids if self._micro else [])))
+            self.gradsync.ensure_capacity(n_ids + sum(int(t.numel()) for t in (self._ids if self._micro else [])))
         tf_p, tf_n, af, align, ctx = eng.forward(batch, True)
         B, P = af.shape
         # L2 normalise, similarity matrix S = A·[Tp;Tn]^T (fp32 MFMA), loss on its diagonals
@@ -642,7 +644,6 @@ class TrainStep:
         if self._micro == 0:
             return False
         ids_all = torch.cat(self._ids)
-        self.gradsync.plan_words(ids_all.numel())
         for stg in GradSync.STAGES:
             self.gradsync.stage_done(stg, ids_all)
         self._optimizer_step()

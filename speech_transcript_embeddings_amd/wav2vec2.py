@@ -79,8 +79,9 @@ def _conv_weight(e, l, cin, k):
     return out
 
 
-def forward(e, wave, mask_i64, train, base_seed, ctx, save=True):
-    """Raw waveform fp32 [B, N] (+ sample mask [B, N] or None) -> (hidden fp32 [B*T, D], bf16 copy)."""
+def forward(e, wave, mask_i64, train, base_seed, ctx, save=True, lengths=None):
+    """Raw waveform fp32 [B, N] (+ sample mask [B, N] or None) -> (hidden fp32 [B*T, D], bf16 copy).
+    lengths: host list of each clip's valid samples (SpecAugment's span sampling without a sync)."""
     from .engine import W2V2_NAMES, _site_seed
     c = e.acfg
     s = e.s
@@ -132,10 +133,13 @@ def forward(e, wave, mask_i64, train, base_seed, ctx, save=True):
                    s.p("audio_encoder.feature_projection.projection.bias"), row_scale=maskf, drop_p=p_fp, seed=seed_fp)
     spec = None
     if train and getattr(e.m, "spec_augment", False) and c.mask_time_prob > 0:
-        from .specaug import compute_mask_indices
-        lens = maskf.view(B, T).sum(-1).to(torch.int64).tolist()
+        from .specaug import compute_mask_indices, upload_mask
+        if lengths is not None:   # host sample counts -> frames (the conv stack's output lengths)
+            lens = [max(0, c.frames(int(n))[-1]) for n in lengths]
+        else:                     # only a device mask: one device->host sync
+            lens = maskf.view(B, T).sum(-1).to(torch.int64).tolist()
         sm = compute_mask_indices((B, T), c.mask_time_prob, c.mask_time_length, lens, c.mask_time_min_masks)
-        spec = torch.from_numpy(sm.astype("int32").reshape(-1)).to(s.device)
+        spec = upload_mask(sm, s.device)
         ops.spec_mask_fwd(x, spec, maskf, s.p("audio_encoder.masked_spec_embed"))
     # ---- positional conv + residual + encoder LayerNorm (+ dropout)
     G, Kp = c.num_conv_pos_embedding_groups, c.num_conv_pos_embeddings

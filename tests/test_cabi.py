@@ -100,6 +100,29 @@ def test_gemm_split_policies(lib):
     assert k(C.byref(b)) == 3
 
 
+def test_gemm_mx8_plan(lib):
+    """ste_gemm_mx8's kernel choice (no launch): the 8-phase MX kernel addresses its operands by
+    32-bit byte offsets, so an operand of 4 GiB or more must take the single-stage kernel
+    (ADVICE r3)."""
+    k = lib.fn("ste_gemm_mx8_kernel")
+    a = lib.GemmArgs()
+    # c5 FFN-out: M = 64 x 1499 frames, bias + fp32 residual
+    a.M, a.N, a.K, a.batch, a.a_kc, a.b_kc, a.lda, a.ldb = 95936, 1024, 4096, 1, 1, 1, 4096, 4096
+    a.C, a.bias, a.R = 1, 1, 1
+    assert k(C.byref(a), 0) == 1
+    a.M = (1 << 32) // 4096 + 256                   # M·lda crosses 4 GiB of fp8 bytes
+    assert k(C.byref(a), 0) == 0
+    a.M = (1 << 32) // 4096 - 256                   # just below
+    assert k(C.byref(a), 0) == 1
+    a.M, a.N, a.ldb = 95936, 1024, (1 << 32) // 1024   # B operand over the limit
+    assert k(C.byref(a), 0) == 0
+    a.ldb = 4096
+    a.R = None                                      # bias + fp32 out: no compile-time MX epilogue
+    assert k(C.byref(a), 0) == 0
+    a.R, a.M = 1, 512                               # 8 tiles: single-stage
+    assert k(C.byref(a), 0) == 0
+
+
 def test_argument_errors_return_status_without_launch(lib):
     """Shape/alignment contract violations come back as non-zero status (-> SteError), never a launch."""
     a = lib.GemmArgs()

@@ -84,7 +84,8 @@ class _Recorder:
 def _sync_case(rank, world):
     """Dense blocks + sparse word table; returns (max err vs the all-rank average, untouched tail ok,
     every collective async).  The ranks hold DIFFERENT token counts (the sparse
-    capacity and the sparse-vs-dense choice must still agree), agreed by plan_words."""
+    capacity and the sparse-vs-dense choice must still agree): first with the capacity agreed
+    once by ensure_capacity (MAX over ranks), then with a configured one."""
     from speech_transcript_embeddings_amd import ops
     from speech_transcript_embeddings_amd.train import GradSync
     ops.rows_extract, ops.rows_accumulate = rows_extract_ref, rows_accumulate_ref
@@ -114,15 +115,34 @@ def _sync_case(rank, world):
     gs = GradSync(_Store(g, slots))
     assert all(gs.ranges[k] for k in GradSync.STAGES), gs.ranges   # every stage has a non-empty block
     gs.bucket = 29  # several buckets + ragged ones
+    g0 = g.clone()
+    assert gs.ensure_capacity(ids.numel()) == 10 + 2 * (world - 1)   # agreed once: the MAX over ranks
     with _Recorder() as rec:
-        gs.plan_words(ids.numel())
         for stage in GradSync.STAGES:
             gs.stage_done(stage, ids)
-    assert gs.sparse is not None and gs.sparse[3] == 10 + 2 * (world - 1)   # sparse, at the agreed MAX capacity
+    assert gs.sparse is not None and gs.sparse[3] == 10 + 2 * (world - 1)   # sparse, at the agreed capacity
     gs.finish()
     n = gs.store.n_grad
     all_async = bool(rec.calls) and all(a for _, a in rec.calls)
-    return (g[:n] - expect[:n]).abs().max().item(), bool(torch.all(g[408:] == 7.0 + rank)), all_async
+    err = (g[:n] - expect[:n]).abs().max().item()
+    # a configured capacity (TrainStep(micro_batch=, max_text_length=)): no agreement collective at all
+    g.copy_(g0)
+    gs2 = GradSync(_Store(g, slots), word_capacity=12)   # 2 x 12 rows < half the 50-row table: sparse
+    gs2.bucket = 29
+    with _Recorder() as rec2:
+        for stage in GradSync.STAGES:
+            gs2.stage_done(stage, ids)
+    assert gs2.sparse is not None and gs2.sparse[3] == 12
+    gs2.finish()
+    err = max(err, (g[:n] - expect[:n]).abs().max().item())
+    all_async = all_async and bool(rec2.calls) and all(a for _, a in rec2.calls)
+    try:
+        gs2.ensure_capacity(13)
+        over = False
+    except RuntimeError:
+        over = True
+    assert over, "a step over the configured capacity must raise"
+    return err, bool(torch.all(g[408:] == 7.0 + rank)), all_async
 
 
 def _exchange_stand_ins():
@@ -309,3 +329,241 @@ def test_data_parallel_gloo_world2():
         assert out["layerdrop_same"], r
         assert out["shards_differ"], r
 
+
+
+# --------------------------------------------------------------------------------------------
+# step_batch holds no host synchronisation at world 2: a TrainStep over a fake
+# engine (the forward returns embeddings, the backward finalises the GradSync stages in order)
+# with torch stand-ins for the HIP ops.  Every device->host read (item / tolist / cpu / numpy /
+# bool / float / int), every stream / event / device synchronize and every blocking collective
+# issued from the package's own code is recorded; after the first step there must be none.
+
+class _SyncSpy:
+    PKG = "speech_transcript_embeddings_amd"
+    READS = ("item", "tolist", "cpu", "numpy", "__bool__", "__float__", "__int__")
+
+    def __enter__(self):
+        import sys
+        self.hits, self._orig = [], []
+
+        def from_pkg():
+            f = sys._getframe(2)
+            return self.PKG in f.f_code.co_filename and "test_" not in f.f_code.co_filename
+
+        for name in self.READS:
+            orig = getattr(torch.Tensor, name)
+
+            def wrap(t, *a, _o=orig, _n=name, **k):
+                if from_pkg():
+                    self.hits.append(_n)
+                return _o(t, *a, **k)
+            self._orig.append((torch.Tensor, name, orig))
+            setattr(torch.Tensor, name, wrap)
+        for obj, name in ((torch.cuda, "synchronize"), (torch.cuda.Event, "synchronize"),
+                          (torch.cuda.Stream, "synchronize"), (torch.cuda.Event, "wait")):
+            orig = getattr(obj, name)
+
+            def wrap(*a, _o=orig, _n=name, **k):
+                if from_pkg():
+                    self.hits.append(_n)
+                return _o(*a, **k)
+            self._orig.append((obj, name, orig))
+            setattr(obj, name, wrap)
+        self.rec = _Recorder().__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        self.rec.__exit__(*exc)
+        for obj, name, orig in reversed(self._orig):
+            setattr(obj, name, orig)
+
+    def blocking(self):
+        return self.hits + [n for n, a in self.rec.calls if not a]
+
+
+def _fake_model(B, L, P=8, V=50):
+    """A model object with the attributes TrainStep / FusedAdamW / GradSync read; the engine's
+    forward returns fixed embeddings and its backward writes a gradient per stage."""
+    from speech_transcript_embeddings_amd.store import Slot
+    slots = [("text_encoder.embeddings.word_embeddings.weight", 0, (V, 4), "enc"),
+             ("text_encoder.encoder.layer.1.x", 200, (37,), "enc"),
+             ("audio_encoder.encoder.layers.0.x", 240, (101,), "enc"),
+             ("audio_encoder.feature_projection.projection.weight", 344, (13,), "enc"),
+             ("text_proj.weight", 360, (45,), "head")]
+
+    class Store:
+        device = torch.device("cpu")
+        n_grad = 405
+        seg_range = {"enc": (0, 357), "head": (357, 405)}
+
+        def __init__(self):
+            self.grad = torch.zeros(405)
+            self.master = torch.randn(405)
+            self.shadow = self.master.clone()
+            self.slots = {n: Slot(n, o, int(np.prod(s)), s, g) for n, o, s, g in slots}
+
+        def sync_shadow(self):
+            pass
+
+        def mark_synced(self):
+            pass
+
+        def refresh_transposes(self, stream=None):
+            pass
+
+    class Engine:
+        layerdrop_gen = None
+
+        def __init__(self, store):
+            self.store = store
+
+        def _side_stream(self):
+            return None
+
+        def forward(self, batch, train):
+            g = torch.Generator().manual_seed(int(batch["input_ids_pos"].sum()))
+            t_ids = torch.cat([batch["input_ids_pos"], batch["input_ids_neg"]])
+            e = lambda: torch.randn(B, P, generator=g)  # noqa: E731
+            return e(), e(), e(), None, {"t_ids": t_ids}
+
+        def backward(self, ctx, d_tp, d_tn, d_af, d_align, stage_done=None):
+            gr = self.store.grad
+            gr[360:405] += d_af.sum()
+            if stage_done:
+                stage_done("heads")
+            gr[240:341] += d_tp.sum()
+            if stage_done:
+                stage_done("audio_layers")
+            gr[344:357] += 1.0
+            if stage_done:
+                stage_done("audio")
+            gr[200:237] += d_tn.sum()
+            for i in ctx["t_ids"].reshape(-1):
+                gr[int(i) * 4:int(i) * 4 + 4] += 0.5      # (test code: host reads are fine here)
+            if stage_done:
+                stage_done("text")
+
+    class Model:
+        freeze_encoders = "partial"
+
+        class text_cfg:
+            pad_token_id = 1
+
+        def __init__(self):
+            self.store = Store()
+            self.engine = Engine(self.store)
+
+        def train(self):
+            pass
+    return Model()
+
+
+def _head_stand_ins():
+    import torch.nn.functional as F
+    from speech_transcript_embeddings_amd import ops
+    _exchange_stand_ins()
+
+    def l2norm_fwd(x, out, nrm):
+        nrm.copy_(x.norm(dim=1))
+        out.copy_(F.normalize(x, dim=1))
+
+    def l2norm_bwd(t, nrm, dt, g):
+        g.copy_((dt - (dt * t).sum(1, keepdim=True) * t) / nrm[:, None])
+
+    def pair_loss_fwd(S, B, align, B2, L, tau, aw, gamma, sp, sn, loss):
+        i = torch.arange(B)
+        sp.copy_(S[i, i])
+        sn.copy_(S[i, B + i])
+        loss.copy_(F.softplus((sn - sp) / tau).mean().view(1))
+
+    def pair_loss_bwd(sp, sn, align, B, L, tau, aw, gamma, gscale, dsp, dsn, dal):
+        w = torch.sigmoid((sn - sp) / tau) / (tau * B)
+        if gscale is not None:
+            w = w * gscale
+        dsp.copy_(-w)
+        dsn.copy_(w)
+
+    def pair_sim_bwd(an, tp, tn, dsp, dsn, dan, dtp, dtn):
+        dan.copy_(dsp[:, None] * tp + dsn[:, None] * tn)
+        dtp.copy_(dsp[:, None] * an)
+        dtn.copy_(dsn[:, None] * an)
+
+    def sumsq(g, acc):
+        acc += (g.double() ** 2).sum()
+
+    def adamw(master, grad, m, v, shadow, lr, beta1, beta2, eps, wd, step, sumsq_acc=None, max_norm=1.0):
+        clip = torch.clamp(max_norm / (sumsq_acc.sqrt() + 1e-6), max=1.0).float() if sumsq_acc is not None else 1.0
+        g = grad * clip
+        m.mul_(beta1).add_((1 - beta1) * g)
+        v.mul_(beta2).add_((1 - beta2) * g * g)
+        master.sub_(lr * (m / (v.sqrt() + eps) + wd * master))
+        shadow.copy_(master)
+    ops.l2norm_fwd, ops.l2norm_bwd, ops.pair_loss_fwd, ops.pair_loss_bwd, ops.pair_sim_bwd = \
+        l2norm_fwd, l2norm_bwd, pair_loss_fwd, pair_loss_bwd, pair_sim_bwd
+    ops.sumsq, ops.adamw = sumsq, adamw
+    ops.rows_extract, ops.rows_accumulate = rows_extract_ref, rows_accumulate_ref
+
+
+def _nosync_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from speech_transcript_embeddings_amd.train import TrainStep
+        _head_stand_ins()
+        B, L = 3, 4
+        out = {}
+        for mode in ("configured", "agreed_once"):
+            for acc in (1, 2):
+                model = _fake_model(B, L)
+                kw = dict(micro_batch=B, max_text_length=L) if mode == "configured" else {}
+                step = TrainStep(model, warmup=1, total_steps=10, accumulation_steps=acc, in_batch_weight=0.3, **kw)
+                g = torch.Generator().manual_seed(10 + rank)
+                hits = []
+                for it in range(3 * acc):
+                    ids = torch.randint(2, 50, (B, L), generator=g)
+                    neg = torch.randint(2, 50, (B, L), generator=g)
+                    batch = {"input_ids_pos": ids, "attention_mask_pos": torch.ones(B, L, dtype=torch.long),
+                             "input_ids_neg": neg, "attention_mask_neg": torch.ones(B, L, dtype=torch.long)}
+                    with _SyncSpy() as spy:
+                        step.step_batch(batch)
+                    # the unconfigured capacity is agreed once, on the first optimizer step's
+                    # final micro-batch (before any of its work is queued); nothing after that
+                    first = mode == "agreed_once" and it == acc - 1
+                    if not first:
+                        hits += spy.blocking()
+                out[f"{mode}/acc{acc}"] = hits
+                out[f"{mode}/acc{acc}/steps"] = step.opt.t
+                out[f"{mode}/acc{acc}/finite"] = bool(torch.isfinite(model.store.master).all())
+        q.put((rank, out))
+    except Exception:
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_step_batch_no_host_sync_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_nosync_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, out = q.get(timeout=170)
+        res[r] = out
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r, out in res.items():
+        assert "error" not in out, out.get("error")
+        for mode in ("configured", "agreed_once"):
+            for acc in (1, 2):
+                k = f"{mode}/acc{acc}"
+                assert out[k] == [], (r, k, out[k])      # no host read, no sync, no blocking collective
+                assert out[k + "/steps"] == 3 and out[k + "/finite"], (r, k)

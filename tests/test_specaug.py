@@ -76,11 +76,9 @@ def test_oracle_with_spec_mask_matches_reference():
     assert np.linalg.norm(g - ref) <= 1e-4 * np.linalg.norm(ref)
 
 
-@pytest.mark.gpu
-def test_hip_specaug_train_step_matches_reference():
-    from speech_transcript_embeddings_amd.model import AlignmentAwareInfoNCE, EnhancedAudioTextModel
+def _hip_model(meta):
+    from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
     from speech_transcript_embeddings_amd.modules import AudioConfig, TextConfig
-    meta, z = _golden()
     a, t, m = meta["audio"], meta["text"], meta["mini"]
     acfg = AudioConfig(hidden_size=a["hidden_size"], num_hidden_layers=a["num_hidden_layers"],
                        num_attention_heads=a["num_attention_heads"], intermediate_size=a["intermediate_size"],
@@ -96,6 +94,14 @@ def test_hip_specaug_train_step_matches_reference():
     sd = model.state_dict()
     vals = det_init.state_dict_values([(n, v.shape) for n, v in sd.items()])
     model.load_state_dict({n: torch.from_numpy(v) for n, v in vals.items()})
+    return model
+
+
+@pytest.mark.gpu
+def test_hip_specaug_train_step_matches_reference():
+    from speech_transcript_embeddings_amd.model import AlignmentAwareInfoNCE, EnhancedAudioTextModel
+    meta, z = _golden()
+    model = _hip_model(meta)
     model.train()
     batch = _batch(z, "cuda")
     np.random.seed(meta["seed"])
@@ -132,3 +138,41 @@ def test_hip_specaug_train_step_matches_reference():
     with torch.no_grad():
         EnhancedAudioTextModel.compute_pos_neg_embeddings(model, batch)
     assert np.array_equal(np.random.get_state()[1], st[1])
+
+
+@pytest.mark.gpu
+def test_specaug_host_lengths_no_device_readback():
+    """with the clip lengths known on the host (custom_collate_fn / to_model_batch /
+    TrainStep put them in batch["audio_lengths"]) the span sampling reads nothing back from the
+    device, and draws exactly the mask the device-mask route draws (same numpy seed -> identical
+    embeddings)."""
+    from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
+    meta, z = _golden()
+    model = _hip_model(meta)
+    model.train()
+    model.dropout = 0.0
+    batch = _batch(z, "cuda")
+    np.random.seed(meta["seed"])
+    torch.manual_seed(0)
+    with torch.no_grad():
+        ref = EnhancedAudioTextModel.compute_pos_neg_embeddings(model, batch)
+    torch.cuda.synchronize()
+    hb = dict(batch, audio_lengths=[int(n) for n in z["attention_mask_audio"].sum(-1)])
+    reads = []
+    tolist = torch.Tensor.tolist
+
+    def spy(t, *a, **k):
+        if t.is_cuda:
+            reads.append(tuple(t.shape))
+        return tolist(t, *a, **k)
+    torch.Tensor.tolist = spy
+    try:
+        np.random.seed(meta["seed"])
+        torch.manual_seed(0)
+        with torch.no_grad():
+            got = EnhancedAudioTextModel.compute_pos_neg_embeddings(model, hb)
+    finally:
+        torch.Tensor.tolist = tolist
+    assert reads == [], reads
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
