@@ -1,0 +1,266 @@
+"""Precision probe of the audio encoder's gradients — test tooling, imports oracle/.
+
+Question: the HIP path's full-size per-tensor gradient errors against the fp32 oracle peak at
+1.75-2.06 % on the trainable Conformer layers' linear_q/k, distance_embedding and the audio
+pooling scorer (profiles/r3_parity.txt).  Is that the bf16 floor of the reference graph itself,
+and which rounding point carries it?
+
+Method (CPU, no GPU): the w2v-bert-2.0 Conformer (24 x 1024, full c2 shapes: B = 2 clips of
+10 s = 499 frames, 3 trainable layers + the feature projection, eval mode) and the audio
+attentive pooling, with a fixed random cotangent on the pooled output, run
+  * in fp32 (the oracle's math, oracle/ref_model.py:84-150, 197-203), and
+  * with bf16 rounding injected at the points the HIP path rounds (engine._conformer_fwd/_bwd,
+    csrc/attention.hip attn_bwd_*_rel3), each point behind a flag:
+      w    GEMM weight operands and the distance table E in bf16 (ParamStore's shadow)
+      fa   forward activations stored bf16: every GEMM's A operand (LayerNorm yb outputs, the
+           swish outputs, O), the q/k/v, pw1 and depthwise-conv outputs
+      bdy  backward GEMM dY operands in bf16 (dx·0.5 / dx / dqkv as the dX and dW GEMMs read them)
+      bdx  backward dX GEMM outputs in bf16 (the out_bf16 input gradients feeding LayerNorm and
+           attention backwards)
+      ads  attention dS and its distance-bin sums G rounded to bf16 for dQ = dS·K + G·E and
+           dK = dSᵀ·Q (pack_acc in attn_bwd_dq_rel3 / dkv_rel3)
+      apb  attention P rounded to bf16 for dV = Pᵀ·dO
+    (the forward's P·V runs on P = hi + lo, ~fp32, as the saving forward does; the pooling
+    scorer reads the fp32 states — the [hi | lo] split image — with bf16 W.)
+Per-tensor gradient error = ||g - g_fp32|| / ||g_fp32||, printed for every flag set: all on
+(the HIP path's rounding), all off, the reference graph under bf16 autocast (scores and
+probabilities in bf16 storage as CUDA autocast leaves them), and all-on-minus-one.
+
+    python tests/precision_probe.py [--layers 24] [--threads 8] [--sets all,hip,...]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+from oracle import fbank_ref, ref_model as R  # noqa: E402
+
+FLAGS = ("w", "fa", "bdy", "bdx", "ads", "apb")
+
+
+def bf(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+class _Q(torch.autograd.Function):
+    """Round to bf16 in the forward (f) and/or the incoming gradient in the backward (b)."""
+
+    @staticmethod
+    def forward(ctx, x, f, b):
+        ctx.b = b
+        return bf(x) if f else x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return (bf(g) if ctx.b else g), None, None
+
+
+def q(x, f, b):
+    return _Q.apply(x, bool(f), bool(b)) if (f or b) else x
+
+
+class Probe:
+    def __init__(self, fl, autocast=False):
+        self.fl = {k: bool(fl.get(k, False)) for k in FLAGS}
+        self.ac = autocast   # reference-under-autocast: scores / probabilities in bf16 storage too
+
+    def lin(self, x, W, b=None, out_bf16=False, dx_round=True, x_is_op=True):
+        """nn.Linear as ste_gemm: A operand bf16 (fa, and its gradient bf16 if dx_round & bdx),
+        B operand bf16 (w), fp32 accumulation, output bf16 storage (fa & out_bf16) and the dY
+        operand of the backward GEMMs bf16 (bdy)."""
+        fl = self.fl
+        xa = q(x, fl["fa"] and x_is_op, fl["bdx"] and dx_round)
+        Wa = q(W, fl["w"], False)
+        y = F.linear(xa, Wa, b)
+        return q(y, fl["fa"] and out_bf16, fl["bdy"])
+
+    def ln(self, p, name, x, eps=1e-5):
+        return F.layer_norm(x, (x.shape[-1],), p[name + ".weight"], p[name + ".bias"], eps)
+
+    # ------------------------------------------------------------------ Conformer pieces
+    def ffn(self, p, pre, a):
+        z = self.lin(a, p[pre + "intermediate_dense.weight"], p[pre + "intermediate_dense.bias"])
+        h = q(F.silu(z), self.fl["fa"], False)     # swish epilogue, stored bf16; dz rounded by the GEMM's bdy
+        return self.lin(h, p[pre + "output_dense.weight"], p[pre + "output_dense.bias"], dx_round=False)
+
+    def attn(self, p, pre, a, cfg):
+        B, T, D = a.shape
+        H, d = cfg.heads, D // cfg.heads
+        W = torch.cat([p[pre + "linear_q.weight"], p[pre + "linear_k.weight"], p[pre + "linear_v.weight"]], 0)
+        bq = torch.cat([p[pre + "linear_q.bias"], p[pre + "linear_k.bias"], p[pre + "linear_v.bias"]], 0)
+        qkv = self.lin(a, W, bq, out_bf16=True)
+        qh, kh, vh = (t.reshape(B, T, H, d).transpose(1, 2) for t in qkv.split(D, -1))
+        E = q(p[pre + "distance_embedding.weight"], self.fl["w"], False)
+        o = _Attn.apply(qh, kh, vh, E, 1.0 / math.sqrt(d), cfg.left, cfg.right, self)
+        o = o.transpose(1, 2).reshape(B, T, D)
+        return self.lin(o, p[pre + "linear_out.weight"], p[pre + "linear_out.bias"])
+
+    def conv(self, p, pre, x2, cfg):
+        a = self.ln(p, pre + "layer_norm", x2, cfg.eps)
+        D = a.shape[-1]
+        pw1 = self.lin(a, p[pre + "pointwise_conv1.weight"].view(2 * D, D), None, out_bf16=True)
+        g = F.glu(pw1, dim=-1).transpose(1, 2)
+        g = F.pad(g, (cfg.conv_k - 1, 0))
+        cv = F.conv1d(g, p[pre + "depthwise_conv.weight"], groups=D).transpose(1, 2)
+        cv = q(cv, self.fl["fa"], self.fl["bdx"])          # cv bf16; its gradient (dcv) bf16
+        sw = F.silu(self.ln(p, pre + "depthwise_layer_norm", cv, cfg.eps))
+        return self.lin(sw, p[pre + "pointwise_conv2.weight"].view(D, D), None)
+
+    def encoder(self, p, feats, cfg, layers):
+        x = self.ln(p, "audio_encoder.feature_projection.layer_norm", feats, cfg.eps)
+        h = self.lin(x, p["audio_encoder.feature_projection.projection.weight"],
+                     p["audio_encoder.feature_projection.projection.bias"])
+        for i in range(cfg.layers - layers, cfg.layers):
+            pre = f"audio_encoder.encoder.layers.{i}."
+            h = h + 0.5 * self.ffn(p, pre + "ffn1.", self.ln(p, pre + "ffn1_layer_norm", h, cfg.eps))
+            h = h + self.attn(p, pre + "self_attn.", self.ln(p, pre + "self_attn_layer_norm", h, cfg.eps), cfg)
+            h = h + self.conv(p, pre + "conv_module.", h, cfg)
+            h = h + 0.5 * self.ffn(p, pre + "ffn2.", self.ln(p, pre + "ffn2_layer_norm", h, cfg.eps))
+            h = self.ln(p, pre + "final_layer_norm", h, cfg.eps)
+        return h
+
+    def pool(self, p, h):
+        """AttentivePooling as the HIP path runs it: fp32 states (split image), bf16 W1, fp32 rest."""
+        W1 = q(p["audio_pooling.attention.0.weight"], self.fl["w"], False)
+        t = torch.tanh(F.linear(h, W1, p["audio_pooling.attention.0.bias"]))
+        s = F.linear(t, p["audio_pooling.attention.2.weight"], p["audio_pooling.attention.2.bias"]).squeeze(-1)
+        w = torch.softmax(s, dim=1)
+        return torch.bmm(w.unsqueeze(1), h).squeeze(1)
+
+
+class _Attn(torch.autograd.Function):
+    """Relative-key attention (w2v:229-327) with the HIP kernels' rounding points."""
+
+    @staticmethod
+    def forward(ctx, qh, kh, vh, E, scale, left, right, pr):
+        B, H, T, d = qh.shape
+        pos = torch.arange(T)
+        dist = ((pos.view(1, -1) - pos.view(-1, 1)).clamp(-left, right) + left)
+        s = qh @ kh.transpose(-1, -2)
+        qe = qh @ E.t()
+        s = (s + torch.gather(qe, 3, dist.view(1, 1, T, T).expand(B, H, T, T))) * scale
+        if pr.ac:
+            s = bf(s)
+        p = torch.softmax(s, -1)
+        o = (bf(p) if pr.ac else p) @ vh
+        if pr.ac:
+            o = bf(o)
+        ctx.save_for_backward(qh, kh, vh, E, p, o)
+        ctx.dist, ctx.scale, ctx.pr = dist, scale, pr
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qh, kh, vh, E, p, o = ctx.saved_tensors
+        fl, ac = ctx.pr.fl, ctx.pr.ac
+        B, H, T, d = qh.shape
+        nrel = E.shape[0]
+        dp = do @ vh.transpose(-1, -2)
+        delta = (do * o).sum(-1, keepdim=True)
+        ds = p * (dp - delta)
+        if ac:
+            ds = bf(ds)
+        G = torch.zeros(B, H, T, nrel).scatter_add_(3, ctx.dist.view(1, 1, T, T).expand(B, H, T, T), ds)
+        dsr = bf(ds) if fl["ads"] else ds
+        Gr = bf(G) if fl["ads"] else G
+        dq = (dsr @ kh + Gr @ E) * ctx.scale
+        dk = (dsr.transpose(-1, -2) @ qh) * ctx.scale
+        pb = bf(p) if (fl["apb"] or ac) else p
+        dv = pb.transpose(-1, -2) @ do
+        dE = (G.transpose(-1, -2) @ qh).sum((0, 1)) * ctx.scale
+        return dq, dk, dv, dE, None, None, None, None
+
+
+def init_params(cfg, seed=0):
+    """The GPU model's init rule (model.py _init_params): encoder weights N(0, 0.02), LayerNorms
+    1/0, encoder biases 0, heads as nn.Linear defaults."""
+    g = torch.Generator().manual_seed(seed)
+    p = {}
+    for n, shp in R.param_shapes(cfg, spec_augment=False):
+        if not (n.startswith("audio_encoder") or n.startswith("audio_pooling")):
+            continue
+        leaf = n.rsplit(".", 1)[-1]
+        if ("norm" in n.lower()) and leaf in ("weight", "bias"):
+            t = torch.ones(shp) if leaf == "weight" else torch.zeros(shp)
+        elif n.startswith("audio_encoder"):
+            t = torch.zeros(shp) if leaf == "bias" else torch.randn(shp, generator=g) * 0.02
+        else:
+            fan_in = shp[-1] if len(shp) > 1 else shp[0]
+            t = (torch.rand(shp, generator=g) * 2 - 1) * fan_in ** -0.5
+        p[n] = t
+    return p
+
+
+def run(p0, feats, cot, cfg, layers, trainable, fl, autocast=False):
+    pr = Probe(fl, autocast)
+    p = {n: t.clone().requires_grad_(n in trainable) for n, t in p0.items()}
+    h = pr.encoder(p, feats, cfg, layers)
+    pooled = pr.pool(p, h)
+    pooled.backward(cot)
+    return {n: p[n].grad.clone() for n in trainable if p[n].grad is not None}, pooled.detach()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", type=int, default=24)
+    ap.add_argument("--unfreeze", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=2)
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--sets", default="hip,autocast,minus")
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args(argv)
+    torch.set_num_threads(args.threads)
+    cfg = R.ModelCfg()
+    ac = cfg.audio
+    p0 = init_params(cfg)
+    n = int(args.seconds * 16000)
+    feats, _ = fbank_ref.collate([fbank_ref.extract(fbank_ref.synth_wave(1000 + i, n))[0] for i in range(args.batch)])
+    feats = torch.as_tensor(np.asarray(feats), dtype=torch.float32)
+    top = [f"audio_encoder.encoder.layers.{i}." for i in range(ac.layers - args.unfreeze, ac.layers)]
+    trainable = {k for k in p0 if k.startswith("audio_encoder.feature_projection") or k.startswith("audio_pooling")
+                 or any(k.startswith(t) for t in top)}
+    cot = torch.randn(args.batch, ac.hidden, generator=torch.Generator().manual_seed(5))
+    t0 = time.time()
+    ref, out_ref = run(p0, feats, cot, ac, args.layers, trainable, {})
+    print(f"fp32 reference: {time.time() - t0:.1f} s, {len(ref)} gradient tensors", flush=True)
+    sets = []
+    want = args.sets.split(",")
+    allon = {k: True for k in FLAGS}
+    if "hip" in want:
+        sets.append(("hip (all flags)", allon, False))
+    if "autocast" in want:
+        sets.append(("reference under bf16 autocast", {"w": True, "fa": True, "bdy": True, "bdx": True, "ads": True,
+                                                       "apb": True}, True))
+    if "minus" in want:
+        sets += [(f"hip minus {k}", {**allon, k: False}, False) for k in FLAGS]
+    for k in FLAGS:
+        if f"only_{k}" in want:
+            sets.append((f"only {k}", {k: True}, False))
+    results = {}
+    for name, fl, acm in sets:
+        t0 = time.time()
+        g, out = run(p0, feats, cot, ac, args.layers, trainable, fl, acm)
+        errs = sorted(((((g[k] - ref[k]).norm() / ref[k].norm()).item(), k) for k in ref
+                       if ref[k].norm() > 1e-8 and not k.endswith(("linear_k.bias", "attention.2.bias"))), reverse=True)
+        med = errs[len(errs) // 2][0]
+        oerr = ((out - out_ref).norm() / out_ref.norm()).item()
+        results[name] = {"worst": errs[:6], "median": med, "pooled_err": oerr}
+        print(f"[{name}] {time.time() - t0:.0f}s pooled {oerr:.2e} median {med:.2e} worst "
+              + ", ".join(f"{e:.4f} {k.replace('audio_encoder.encoder.', '')}" for e, k in errs[:5]), flush=True)
+    if args.json:
+        Path(args.json).write_text(json.dumps(results, indent=1))
+
+
+if __name__ == "__main__":
+    main()
