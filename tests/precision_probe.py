@@ -46,6 +46,8 @@ sys.path.insert(0, str(ROOT))
 from oracle import fbank_ref, ref_model as R  # noqa: E402
 
 FLAGS = ("w", "fa", "bdy", "bdx", "ads", "apb")
+# weight classes for the "w" attribution sets (w_<class>): which GEMMs read bf16 weights
+WCLASSES = ("qkv", "E", "o", "ffn", "conv", "pool", "fp")
 
 
 def bf(t):
@@ -70,19 +72,38 @@ def q(x, f, b):
 
 
 class Probe:
-    def __init__(self, fl, autocast=False):
+    def __init__(self, fl, autocast=False, wclasses=WCLASSES, wlayers=None, fasites=None, falayers=None):
         self.fl = {k: bool(fl.get(k, False)) for k in FLAGS}
         self.ac = autocast   # reference-under-autocast: scores / probabilities in bf16 storage too
+        self.wclasses = set(wclasses)
+        self.wlayers = wlayers   # None: every layer's weights bf16 (with "w"); else a set of layer indices
+        self.layer = None
+        self.fasites = None if fasites is None else set(fasites)   # None: every site rounds (with "fa")
+        self.falayers = falayers
 
-    def lin(self, x, W, b=None, out_bf16=False, dx_round=True, x_is_op=True):
-        """nn.Linear as ste_gemm: A operand bf16 (fa, and its gradient bf16 if dx_round & bdx),
-        B operand bf16 (w), fp32 accumulation, output bf16 storage (fa & out_bf16) and the dY
-        operand of the backward GEMMs bf16 (bdy)."""
+    def fa(self, site):
+        """forward rounding of an activation at `site` (qkv_in, qkv_out, o, ffn_in, ffn_h, conv_in,
+        pw1, cv, sw, fp_in)"""
+        if not self.fl["fa"]:
+            return False
+        if self.fasites is not None and site not in self.fasites:
+            return False
+        return self.falayers is None or self.layer is None or self.layer in self.falayers
+
+    def wq(self, W, cls):
+        on = self.fl["w"] and cls in self.wclasses and (self.wlayers is None or self.layer is None or
+                                                       self.layer in self.wlayers)
+        return q(W, on, False)
+
+    def lin(self, x, W, b=None, out_site=None, dx_round=True, in_site="ffn_in", cls="ffn"):
+        """nn.Linear as ste_gemm: A operand bf16 (fa at in_site, and its gradient bf16 if dx_round
+        & bdx), B operand bf16 (w), fp32 accumulation, output bf16 storage (fa at out_site) and the
+        dY operand of the backward GEMMs bf16 (bdy)."""
         fl = self.fl
-        xa = q(x, fl["fa"] and x_is_op, fl["bdx"] and dx_round)
-        Wa = q(W, fl["w"], False)
+        xa = q(x, self.fa(in_site), fl["bdx"] and dx_round)
+        Wa = self.wq(W, cls)
         y = F.linear(xa, Wa, b)
-        return q(y, fl["fa"] and out_bf16, fl["bdy"])
+        return q(y, out_site is not None and self.fa(out_site), fl["bdy"])
 
     def ln(self, p, name, x, eps=1e-5):
         return F.layer_norm(x, (x.shape[-1],), p[name + ".weight"], p[name + ".bias"], eps)
@@ -90,48 +111,52 @@ class Probe:
     # ------------------------------------------------------------------ Conformer pieces
     def ffn(self, p, pre, a):
         z = self.lin(a, p[pre + "intermediate_dense.weight"], p[pre + "intermediate_dense.bias"])
-        h = q(F.silu(z), self.fl["fa"], False)     # swish epilogue, stored bf16; dz rounded by the GEMM's bdy
-        return self.lin(h, p[pre + "output_dense.weight"], p[pre + "output_dense.bias"], dx_round=False)
+        h = q(F.silu(z), self.fa("ffn_h"), False)     # swish epilogue, stored bf16; dz rounded by the GEMM's bdy
+        return self.lin(h, p[pre + "output_dense.weight"], p[pre + "output_dense.bias"], dx_round=False,
+                        in_site="ffn_h")
 
     def attn(self, p, pre, a, cfg):
         B, T, D = a.shape
         H, d = cfg.heads, D // cfg.heads
         W = torch.cat([p[pre + "linear_q.weight"], p[pre + "linear_k.weight"], p[pre + "linear_v.weight"]], 0)
         bq = torch.cat([p[pre + "linear_q.bias"], p[pre + "linear_k.bias"], p[pre + "linear_v.bias"]], 0)
-        qkv = self.lin(a, W, bq, out_bf16=True)
+        qkv = self.lin(a, W, bq, out_site="qkv_out", in_site="qkv_in", cls="qkv")
         qh, kh, vh = (t.reshape(B, T, H, d).transpose(1, 2) for t in qkv.split(D, -1))
-        E = q(p[pre + "distance_embedding.weight"], self.fl["w"], False)
+        E = self.wq(p[pre + "distance_embedding.weight"], "E")
         o = _Attn.apply(qh, kh, vh, E, 1.0 / math.sqrt(d), cfg.left, cfg.right, self)
         o = o.transpose(1, 2).reshape(B, T, D)
-        return self.lin(o, p[pre + "linear_out.weight"], p[pre + "linear_out.bias"])
+        return self.lin(o, p[pre + "linear_out.weight"], p[pre + "linear_out.bias"], in_site="o", cls="o")
 
     def conv(self, p, pre, x2, cfg):
         a = self.ln(p, pre + "layer_norm", x2, cfg.eps)
         D = a.shape[-1]
-        pw1 = self.lin(a, p[pre + "pointwise_conv1.weight"].view(2 * D, D), None, out_bf16=True)
+        pw1 = self.lin(a, p[pre + "pointwise_conv1.weight"].view(2 * D, D), None, out_site="pw1", in_site="conv_in",
+                       cls="conv")
         g = F.glu(pw1, dim=-1).transpose(1, 2)
         g = F.pad(g, (cfg.conv_k - 1, 0))
         cv = F.conv1d(g, p[pre + "depthwise_conv.weight"], groups=D).transpose(1, 2)
-        cv = q(cv, self.fl["fa"], self.fl["bdx"])          # cv bf16; its gradient (dcv) bf16
+        cv = q(cv, self.fa("cv"), self.fl["bdx"])          # cv bf16; its gradient (dcv) bf16
         sw = F.silu(self.ln(p, pre + "depthwise_layer_norm", cv, cfg.eps))
-        return self.lin(sw, p[pre + "pointwise_conv2.weight"].view(D, D), None)
+        return self.lin(sw, p[pre + "pointwise_conv2.weight"].view(D, D), None, in_site="sw", cls="conv")
 
     def encoder(self, p, feats, cfg, layers):
         x = self.ln(p, "audio_encoder.feature_projection.layer_norm", feats, cfg.eps)
         h = self.lin(x, p["audio_encoder.feature_projection.projection.weight"],
-                     p["audio_encoder.feature_projection.projection.bias"])
+                     p["audio_encoder.feature_projection.projection.bias"], in_site="fp_in", cls="fp")
         for i in range(cfg.layers - layers, cfg.layers):
+            self.layer = i
             pre = f"audio_encoder.encoder.layers.{i}."
             h = h + 0.5 * self.ffn(p, pre + "ffn1.", self.ln(p, pre + "ffn1_layer_norm", h, cfg.eps))
             h = h + self.attn(p, pre + "self_attn.", self.ln(p, pre + "self_attn_layer_norm", h, cfg.eps), cfg)
             h = h + self.conv(p, pre + "conv_module.", h, cfg)
             h = h + 0.5 * self.ffn(p, pre + "ffn2.", self.ln(p, pre + "ffn2_layer_norm", h, cfg.eps))
             h = self.ln(p, pre + "final_layer_norm", h, cfg.eps)
+        self.layer = None
         return h
 
     def pool(self, p, h):
         """AttentivePooling as the HIP path runs it: fp32 states (split image), bf16 W1, fp32 rest."""
-        W1 = q(p["audio_pooling.attention.0.weight"], self.fl["w"], False)
+        W1 = self.wq(p["audio_pooling.attention.0.weight"], "pool")
         t = torch.tanh(F.linear(h, W1, p["audio_pooling.attention.0.bias"]))
         s = F.linear(t, p["audio_pooling.attention.2.weight"], p["audio_pooling.attention.2.bias"]).squeeze(-1)
         w = torch.softmax(s, dim=1)
@@ -201,8 +226,10 @@ def init_params(cfg, seed=0):
     return p
 
 
-def run(p0, feats, cot, cfg, layers, trainable, fl, autocast=False):
-    pr = Probe(fl, autocast)
+def run(p0, feats, cot, cfg, layers, trainable, fl, autocast=False, round_feats=False, **kw):
+    pr = Probe(fl, autocast, **kw)
+    if round_feats:
+        feats = bf(feats)
     p = {n: t.clone().requires_grad_(n in trainable) for n, t in p0.items()}
     h = pr.encoder(p, feats, cfg, layers)
     pooled = pr.pool(p, h)
@@ -247,10 +274,40 @@ def main(argv=None):
     for k in FLAGS:
         if f"only_{k}" in want:
             sets.append((f"only {k}", {k: True}, False))
+    if "now" in want:
+        sets.append(("hip, bf16-exact weights", {**allon, "w": False}, False))
+    if "nowminus" in want:   # bf16-representable weights (no weight rounding), then one more point off
+        now = {**allon, "w": False}
+        sets.append(("hip, bf16-exact weights", now, False))
+        sets += [(f"hip, bf16-exact weights, minus {k}", {**now, k: False}, False) for k in FLAGS if k != "w"]
+    FASITES = ("qkv_in", "qkv_out", "o", "ffn_in", "ffn_h", "conv_in", "pw1", "cv", "sw", "fp_in")
+    if "fasite" in want:   # bf16-exact weights, forward rounding at one site only
+        now = {**allon, "w": False}
+        sets += [(f"hip, bf16-exact weights, fwd rounding only at {st}", now, False, dict(fasites=(st,)))
+                 for st in FASITES]
+    if "falayers" in want:
+        now = {**allon, "w": False}
+        topl = set(range(ac.layers - args.unfreeze, ac.layers))
+        sets += [("hip, bf16-exact weights, fwd rounding only in the trainable layers", now, False,
+                  dict(falayers=topl)),
+                 ("hip, bf16-exact weights, fwd rounding only in the frozen layers", now, False,
+                  dict(falayers=set(range(ac.layers)) - topl))]
+    if "wclass" in want:   # everything else on, bf16 weights in one class only
+        sets += [(f"hip, bf16 weights only in {c}", allon, False, dict(wclasses=(c,))) for c in WCLASSES]
+    if "wlayers" in want:  # bf16 weights only in the trainable / frozen layers
+        topl = set(range(ac.layers - args.unfreeze, ac.layers))
+        sets += [("hip, bf16 weights only in the trainable layers", allon, False, dict(wlayers=topl)),
+                 ("hip, bf16 weights only in the frozen layers", allon, False,
+                  dict(wlayers=set(range(ac.layers)) - topl))]
+    if "inputs" in want:   # conditioning: the fp32 graph on input features rounded to bf16 (one ulp)
+        sets.append(("fp32 graph, input features rounded to bf16", {}, False, dict(round_feats=True)))
+        sets.append(("fp32 graph, weights rounded to bf16", {"w": True}, False))
     results = {}
-    for name, fl, acm in sets:
+    for item in sets:
+        name, fl, acm = item[:3]
+        kw = item[3] if len(item) > 3 else {}
         t0 = time.time()
-        g, out = run(p0, feats, cot, ac, args.layers, trainable, fl, acm)
+        g, out = run(p0, feats, cot, ac, args.layers, trainable, fl, acm, **kw)
         errs = sorted(((((g[k] - ref[k]).norm() / ref[k].norm()).item(), k) for k in ref
                        if ref[k].norm() > 1e-8 and not k.endswith(("linear_k.bias", "attention.2.bias"))), reverse=True)
         med = errs[len(errs) // 2][0]

@@ -11,9 +11,17 @@ Checked: the three normalised embeddings and alignment scores (bf16 bound of nor
 1e-2 relative), and the gradient of every parameter that receives one, for random cotangents
 on the outputs (the loss-derived cotangent is a near-cancelling pos/neg difference, see
 test_model_gpu.py::test_forward_backward_matches_golden_and_oracle).  Gradients are compared
-tensor-wise by relative L2 norm of the difference: median within 1e-2, worst within 3e-2
-(measured: median 0.66 %, worst 2.3 % for c2 and c4 shapes; with the alignment head the
-oracle re-runs with the HIP path's ReLU gate).
+tensor-wise by relative L2 norm of the difference; with the alignment head the oracle re-runs
+with the HIP path's ReLU gate.
+
+Weights: every config runs on bf16-exact weights (kref.bf16_exact: the same values on both
+sides, representable in the GEMMs' operand format), so the comparison measures the kernels'
+arithmetic; c2_fp32w repeats c2 end to end with arbitrary fp32 master weights, whose bf16
+rounding the GEMMs read.  The bf16 floor of the reference graph (tests/precision_probe.py,
+profiles/r4_bf16_floor.txt, CPU, c2 shapes): the fp32 graph with only its weights rounded to
+bf16 moves the worst tensor by 1.33 %, with only the forward activations stored bf16 at the
+HIP path's rounding points by ~1.0 %, and the reference under bf16 autocast by 4.8 %; the HIP
+path is at 0.93 % (bf16-exact weights) / 1.8 % (fp32 weights).
 
 The gradients cross all 24 Conformer layers (feature_projection is trainable) on bf16 MFMA
 operands.  Random-init encoders produce activations that are nearly identical across frames
@@ -29,16 +37,19 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from kref import bf16_exact_model_
 from oracle import ref_model as R
 
 pytestmark = pytest.mark.gpu
 
-CONFIGS = {  # name: (batch, samples, tokens, unfreeze k, align, freeze_encoders, fp8)
-    "c1": (4, 32000, 16, 3, False, "partial", False),
-    "c2": (2, 160000, 64, 3, False, "partial", False),
-    "c4": (2, 160000, 64, 5, True, "partial", False),
-    "c5": (1, 480000, 64, 3, False, "none", False),
-    "c5_fp8": (1, 480000, 64, 3, False, "none", True),
+CONFIGS = {  # name: (batch, samples, tokens, unfreeze k, align, freeze_encoders, fp8, bf16-exact weights)
+    "c1": (4, 32000, 16, 3, False, "partial", False, True),
+    "c2": (2, 160000, 64, 3, False, "partial", False, True),
+    "c4": (2, 160000, 64, 5, True, "partial", False, True),
+    "c5": (1, 480000, 64, 3, False, "none", False, True),
+    "c5_fp8": (1, 480000, 64, 3, False, "none", True, True),
+    # end to end with arbitrary fp32 master weights: the bf16 quantisation of the weights included
+    "c2_fp32w": (2, 160000, 64, 3, False, "partial", False, False),
 }
 
 
@@ -52,10 +63,12 @@ def _rel(a, b):
 def test_full_size_vs_oracle(cname):
     from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
     from speech_transcript_embeddings_amd.train import synthetic_batch
-    B, N, L, k, align, freeze, fp8 = CONFIGS[cname]
+    B, N, L, k, align, freeze, fp8, exact = CONFIGS[cname]
     torch.manual_seed(0)
     model = EnhancedAudioTextModel(use_word_alignment=align, text_layers_to_unfreeze=k, audio_layers_to_unfreeze=k,
                                    freeze_encoders=freeze, device="cuda", fp8_gemm=fp8)
+    if exact:
+        bf16_exact_model_(model)
     model.eval()
     wav, lens, ids, mask, neg, nmask = synthetic_batch(B, N, L, device="cuda", seed=3)
     from speech_transcript_embeddings_amd import ops
@@ -142,14 +155,26 @@ def test_full_size_vs_oracle(cname):
     errs.sort(reverse=True)
     assert len(errs) > 50
     median = errs[len(errs) // 2][0]
-    print(f"[{cname}] grad rel err: worst {errs[:6]}, median {median:.2e}, n={len(errs)}, gate flips {flips}")
+    print(f"[{cname}] grad rel err ({'bf16-exact' if exact else 'fp32 master'} weights): worst {errs[:6]}, "
+          f"median {median:.2e}, n={len(errs)}, gate flips {flips}")
     if fp8:
         # elementwise vs fp32 with fp8-quantised forward activations (straight-through bf16
         # backward): measured median 12 %, worst 26 % (bf16 c5: 0.7 % / 2.1 %)
         assert median < 2e-1 and errs[0][0] < 4e-1, (median, errs[:5])
+    elif exact:
+        # the kernels' arithmetic on bf16-exact weights.  c2 / c4 shapes: within north_star's 1e-2
+        # (measured 0.93 / 0.98 %).  c1 (2 s clips) and c5 (T = 1,499, every layer trainable) sit
+        # at the bf16-activation floor of the graph itself: the fp32 oracle with bf16 storage of
+        # the forward activations at the HIP path's rounding points and nothing else changed gives
+        # 1.02 % (c1) and 1.14 % (c5) on the same tensors (tests/precision_probe.py, measured
+        # 1.31 / 1.30 % here) — the trained layers' q/k, distance table and pooling-scorer gradients
+        # of a random-init encoder (near-uniform attention) amplify any 2^-9 perturbation of the
+        # hidden states; 1.5e-2 there
+        assert median < 5e-3, median
+        assert errs[0][0] < (1e-2 if cname in ("c2", "c4") else 1.5e-2), errs[:5]
     else:
-        # measured (r3): median 0.6 %, worst 1.75 % (c2 / c4) and 2.0 % (c1), the audio pooling
-        # scorer and the deepest trainable layers' q/k: the audio encoder's bf16 forward rounding of
-        # frames that share a large common component (see the module docstring)
+        # arbitrary fp32 weights: the GEMMs read their bf16 rounding.  The fp32 reference graph
+        # itself, evaluated with bf16-rounded weights and nothing else changed, moves these
+        # tensors by 1.33 % worst, and under bf16 autocast by 4.8 % (profiles/r4_bf16_floor.txt)
         assert median < 1e-2, median
         assert errs[0][0] < 2.5e-2, errs[:5]
