@@ -37,7 +37,7 @@ extern "C" {
  *   act in {*_BWD}: v *= act'(Z[m,n])           (Z: bf16, row stride ldz)
  *   drop_p>0: v *= keep(seed, m*drop_ld+n)/(1-drop_p)
  *   row_scale: v *= row_scale[m]
- *   colsum: colsum[n] += v                      (fp32 atomics; bias gradients)
+ *   colsum: colsum[n] += v                      (bias gradients; see below)
  *   R: v += R[m,n]                              (fp32, or bf16 if r_bf16)
  *   beta != 0: v += beta*C[m,n]
  *   C <- v (fp32, or bf16 if c_bf16);  C3 <- bf16(v) (optional)
@@ -50,6 +50,10 @@ extern "C" {
  * 256x256 tiles cannot fill the chip is split along K into S slabs
  * (S·M·N·4 <= ws_bytes), each reduced by one 256x256 MFMA workgroup, then
  * C = beta·C + alpha·Σ slabs.  ws may be NULL (no split).
+ * Column sums are run-to-run deterministic when ws holds at least
+ * ste_gemm_colsum_ws_floats(args) floats: each wave writes its rows' partial sums there
+ * and ste_rowsum_ordered adds them in a fixed order (colsum launches are never split, so
+ * ws is free for them); without such a ws they go through fp32 atomics.
  * Narrow outputs (a_kc=1, b_kc=1, batch 1, no colsum, N%8==0, K%64==0 with >= 40
  * K-tiles, at most CUs/2 tiles of 256x256, 2·M·N·4 <= ws_bytes): given ws, the
  * product runs as 2 K-slabs and a reduction that applies the full epilogue (same
@@ -90,6 +94,9 @@ typedef struct {
 } ste_gemm_args;
 
 int ste_gemm(const ste_gemm_args* args, void* stream);
+/* Workspace floats for deterministic column sums of this launch (0 without colsum): an upper
+ * bound over ste_gemm and ste_gemm_f32's tile shapes. */
+int64_t ste_gemm_colsum_ws_floats(const ste_gemm_args* args);
 
 /* The same contract with fp32 A, B (and fp32 C2 / Z) on the exact-f32 matrix core
  * (v_mfma_f32_16x16x4_f32): the projection, cross-attention query / output, fusion and text
@@ -257,11 +264,14 @@ int ste_attention_bwd(const ste_attn_args* a, void* stream);
  * GLU over channels then causal depthwise conv (left pad K-1), no bias.
  * Replaces tf:…wav2vec2_bert…:198-207 (glu, F.pad(K-1,0), depthwise_conv).
  * pre: bf16 [B*T, 2C]; w: fp32 [C, K]; out: bf16 [B*T, C].
- * Backward: dout bf16 [B*T, C] -> dpre bf16 [B*T, 2C]; dw fp32 [C,K] += (optional).
+ * Backward: dout bf16 [B*T, C] -> dpre bf16 [B*T, 2C]; dw fp32 [C,K] += (optional; with ws
+ * of ste_glu_dwconv_bwd_ws_floats floats the per-block partials are summed in a fixed order,
+ * run-to-run deterministic; ws = NULL: fp32 atomics).
  */
 int ste_glu_dwconv_fwd(const void* pre, const float* w, void* out, int B, int T, int C, int K, void* stream);
 int ste_glu_dwconv_bwd(const void* pre, const float* w, const void* dout, void* dpre, float* dw,
-                       int B, int T, int C, int K, void* stream);
+                       int B, int T, int C, int K, float* ws, int64_t ws_floats, void* stream);
+int64_t ste_glu_dwconv_bwd_ws_floats(int B, int T, int C, int K);
 
 /* ------------------------------------------------------------------ fbank --
  * Batched Kaldi-style log-mel fbank + per-utterance CMVN + stride-2 stacking:
@@ -293,7 +303,7 @@ int ste_attn_pool_fwd(const void* t, const float* w2, const float* b2, const voi
  * two-pass weight-gradient GEMM), dw2 fp32 [Hh] (+=), db2 fp32 [1] (+=), db1 fp32 [Hh] (+=,
  * the first Linear's bias gradient Σ_l dt_l summed in fp32; may be NULL).
  * work: fp32 scratch of ste_attn_pool_bwd_work_floats(B, L, Hh) floats (dscore [B*L], then
- * per-row-chunk column-sum partials).  Hh <= 1024.  mask: the forward's int32 [B*L] mask or
+ * per-row-chunk column-sum partials, then the per-sample db2 terms; every sum in a fixed order).  Hh <= 1024.  mask: the forward's int32 [B*L] mask or
  * NULL; masked positions get no score gradient (masked_fill's backward, ref:199-200).  Replaces the
  * autograd of ref:184-211. */
 int ste_attn_pool_bwd_work_floats(int B, int L, int Hh);
@@ -421,9 +431,14 @@ int ste_pair_sim_bwd(const float* a, const float* tp, const float* tn, const flo
  * [B*L, D] (LayerNorm runs through ste_layernorm_fwd).  pos_ids int32 [B*L] saved. */
 int ste_text_embed_fwd(const int64_t* ids, int B, int L, int D, int pad_idx, const float* word, const float* pos,
                        const float* type0, float* out, int32_t* pos_ids, void* stream);
-/* Backward scatter-add (nn.Embedding padding_idx rows get no gradient). */
+/* Backward (nn.Embedding padding_idx rows get no gradient): dword / dpos rows += the sum of the
+ * token rows carrying that id, in row order (one writer per table row, no atomics); dtype0 +=
+ * the column sum of every row, ordered through ws (ste_text_embed_bwd_ws_floats floats; NULL:
+ * atomics).  D % 4 == 0, D <= 1024.  Run-to-run deterministic with ws. */
 int ste_text_embed_bwd(const int64_t* ids, const int32_t* pos_ids, const float* dout, int B, int L, int D,
-                       int pad_idx, float* dword, float* dpos, float* dtype0, void* stream);
+                       int pad_idx, float* dword, float* dpos, float* dtype0, float* ws, int64_t ws_floats,
+                       void* stream);
+int64_t ste_text_embed_bwd_ws_floats(int B, int L, int D);
 
 /* Row-sparse exchange of the word-embedding gradient between data-parallel ranks
  * (replaces all-reducing the dense 250,002 x 768 table that
@@ -440,10 +455,11 @@ int ste_rows_accumulate(float* grad, int D, const int32_t* ids, const float* row
 /* ------------------------------------------------------------- optimizer --
  * torch.nn.utils.clip_grad_norm_ + torch.optim.AdamW.step
  * (ref:training/trainer_unfreeze.py:1108-1110, groups :1487-1511).
- * ste_sumsq accumulates Σg² of n fp32 values into *acc (fp64 atomics).
+ * ste_sumsq accumulates Σg² of n fp32 values into *acc in fp64: with part (double[2048]) the
+ * per-block sums are added in block order (deterministic), part = NULL: fp64 atomics.
  * ste_adamw: reads clip coefficient min(1, max_norm/(sqrt(*sumsq)+1e-6)) on device
  * when sumsq != NULL, then decoupled-decay AdamW; writes bf16 shadow if non-NULL. */
-int ste_sumsq(const float* g, int64_t n, double* acc, void* stream);
+int ste_sumsq(const float* g, int64_t n, double* acc, double* part, void* stream);
 int ste_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
               float beta2, float eps, float wd, int step, const double* sumsq, float max_norm, void* stream);
 
@@ -466,18 +482,28 @@ int ste_copy2d(void* y, int64_t ldy, const void* x, int64_t ldx, int64_t rows, i
 /* SpecAugment time masking of the audio encoder input (tf:…wav2vec2_bert…:944-988, training mode):
  * forward x[r,:] = embed for rows with spec[r] != 0 and valid[r] != 0 (x fp32 [rows, cols], row
  * stride ld; spec int32 [rows]; valid = the frame mask as float); backward dembed += Σ dx[r,:]
- * over the same rows (fp32 atomics; dembed may be NULL) and dx[r,:] = 0. */
+ * over the same rows (dembed may be NULL; with ws of ste_spec_mask_bwd_ws_floats floats the
+ * per-block sums are added in a fixed order, ws = NULL: fp32 atomics) and dx[r,:] = 0. */
 int ste_spec_mask_fwd(float* x, int64_t ld, const int32_t* spec, const float* valid, const float* embed,
                       int64_t rows, int cols, void* stream);
 int ste_spec_mask_bwd(float* dx, int64_t ld, const int32_t* spec, const float* valid, float* dembed,
-                      int64_t rows, int cols, void* stream);
+                      int64_t rows, int cols, float* ws, int64_t ws_floats, void* stream);
+int64_t ste_spec_mask_bwd_ws_floats(int64_t rows, int cols);
 /* y[c, r] = x[r, c] for 2-byte elements (row strides ldx >= cols, ldy >= rows, in elements).
  * Builds the k-contiguous copies Wᵀ [in, out] of the nn.Linear weights that the input-gradient
  * GEMMs dX = dY·W read as their KC operand (replaces reading W k-major in the backward of
  * every encoder Linear: tf:…wav2vec2_bert…:119-226, tf:…xlm_roberta…:186-398). */
 int ste_transpose16(void* y, int64_t ldy, const void* x, int64_t ldx, int64_t rows, int cols, void* stream);
-/* out[c] += Σ_r x[r, c] over a row-major [rows, cols] fp32/bf16 matrix (bias gradients). */
-int ste_colsum(const void* x, int is_bf16, int64_t rows, int cols, int64_t ld, float* out, void* stream);
+/* out[c] += Σ_r x[r, c] over a row-major [rows, cols] fp32/bf16 matrix (bias gradients): with ws
+ * (>= ste_colsum_ws_floats(rows, cols) floats) one partial row per 512-row chunk, added in chunk
+ * order (run-to-run deterministic); ws = NULL: fp32 atomics. */
+int ste_colsum(const void* x, int is_bf16, int64_t rows, int cols, int64_t ld, float* out, float* ws,
+               int64_t ws_floats, void* stream);
+int64_t ste_colsum_ws_floats(int64_t rows, int cols);
+/* out[b·cols + c] += Σ_{r < rows} part[(b·rows + r)·cols + c], summed in a fixed order (the
+ * ordered second pass of every deterministic column sum: GEMM bias gradients, ste_colsum, the
+ * depthwise-conv and SpecAugment-embedding gradients, the pooling scorer bias). */
+int ste_rowsum_ordered(const float* part, int64_t rows, int cols, int batch, float* out, void* stream);
 /* y[r, c] = x[r, c] * scale[r]  (fp32, row stride ld) */
 int ste_scale_rows(float* x, const float* scale, int64_t rows, int cols, int64_t ld, void* stream);
 int ste_mask_i64_to_f32(const int64_t* m, float* f, int32_t* i32, int64_t n, void* stream);

@@ -115,6 +115,7 @@ _SIGS = {
     "ste_gemm": (c_int, [C.POINTER(GemmArgs), c_void_p]),
     "ste_gemm_f32": (c_int, [C.POINTER(GemmArgs), c_void_p]),
     "ste_gemm_kernel": (c_int, [C.POINTER(GemmArgs)]),
+    "ste_gemm_colsum_ws_floats": (c_int64, [C.POINTER(GemmArgs)]),
     "ste_gemm_kernel_name": (c_int, [C.POINTER(GemmArgs), c_char_p, c_int]),
     "ste_rows_extract": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                  c_void_p, c_void_p]),
@@ -130,7 +131,8 @@ _SIGS = {
     "ste_split_bf16": (c_int, [c_void_p, c_int64, c_int64, c_int, c_void_p, c_int, c_int, c_void_p]),
     "ste_glu_dwconv_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "ste_glu_dwconv_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                                   c_void_p]),
+                                   c_void_p, c_int64, c_void_p]),
+    "ste_glu_dwconv_bwd_ws_floats": (c_int64, [c_int, c_int, c_int, c_int]),
     "ste_fbank": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p,
                           c_void_p]),
     "ste_gemm_mx8": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -189,17 +191,22 @@ _SIGS = {
     "ste_text_embed_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
     "ste_text_embed_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
-                                   c_void_p, c_void_p]),
-    "ste_sumsq": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+                                   c_void_p, c_void_p, c_int64, c_void_p]),
+    "ste_text_embed_bwd_ws_floats": (c_int64, [c_int, c_int, c_int]),
+    "ste_sumsq": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "ste_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                           c_float, c_float, c_int, c_void_p, c_float, c_void_p]),
     "ste_cast_f32_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
-    "ste_colsum": (c_int, [c_void_p, c_int, c_int64, c_int, c_int64, c_void_p, c_void_p]),
+    "ste_colsum": (c_int, [c_void_p, c_int, c_int64, c_int, c_int64, c_void_p, c_void_p, c_int64, c_void_p]),
+    "ste_colsum_ws_floats": (c_int64, [c_int64, c_int]),
+    "ste_rowsum_ordered": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p]),
     "ste_axpby2d": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_float, c_float, c_void_p]),
     "ste_copy2d": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_int, c_void_p]),
     "ste_transpose16": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p]),
     "ste_spec_mask_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
-    "ste_spec_mask_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "ste_spec_mask_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64,
+                                  c_void_p]),
+    "ste_spec_mask_bwd_ws_floats": (c_int64, [c_int64, c_int]),
     "ste_scale_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int64, c_void_p]),
     "ste_mask_i64_to_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "ste_w2v_conv0_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,

@@ -93,7 +93,8 @@ __global__ __launch_bounds__(NT) void glu_dwconv_fwd_kernel(const bf16* __restri
 template <int K, bool DW>
 __global__ __launch_bounds__(NT) void glu_dwconv_bwd_kernel(const bf16* __restrict__ pre, const float* __restrict__ w,
                                                           const bf16* __restrict__ dout, bf16* __restrict__ dpre,
-                                                          float* __restrict__ dw, int T, int C) {
+                                                          float* __restrict__ dw, int T, int C,
+                                                          float* __restrict__ part) {
   constexpr int ROWS = TT + K - 1;
   __shared__ float lds[(DW ? 2 : 1) * ROWS * CC];
   __shared__ float sw[CC * K];
@@ -193,7 +194,10 @@ __global__ __launch_bounds__(NT) void glu_dwconv_bwd_kernel(const bf16* __restri
     float sum = 0.f;
 #pragma unroll
     for (int g = 0; g < 4; ++g) sum += sred[(g * CC + cc) * (K + 1) + k];
-    atomicAdd(dw + (c0 + cc) * K + k, sum);
+    // ordered mode: the block's partial row (batch, row-tile group) of [C·K], summed in order by
+    // ste_rowsum_ordered; else one atomic per (channel, tap) per block
+    if (part) part[((int64_t)blockIdx.z * gridDim.x + blockIdx.x) * C * K + (c0 + cc) * K + k] = sum;
+    else atomicAdd(dw + (c0 + cc) * K + k, sum);
   }
 }
 
@@ -209,21 +213,34 @@ extern "C" int ste_glu_dwconv_fwd(const void* pre, const float* w, void* out, in
   return 0;
 }
 
+namespace {
+// ~8 row tiles per dW block: 8x fewer partials (or same-address atomics) on dW, still >= 2
+// blocks per CU at B = 64 (measured 1/2/4/8/24 tiles: 237/200/196/186/188 us at T = 499)
+constexpr unsigned DW_TILES_PER_BLOCK = 8;
+unsigned dw_row_groups(int T) { return ((T + TT - 1) / TT + DW_TILES_PER_BLOCK - 1) / DW_TILES_PER_BLOCK; }
+}  // namespace
+
+extern "C" int64_t ste_glu_dwconv_bwd_ws_floats(int B, int T, int C, int K) {
+  return (int64_t)B * dw_row_groups(T) * C * K;
+}
+
 extern "C" int ste_glu_dwconv_bwd(const void* pre, const float* w, const void* dout, void* dpre, float* dw, int B,
-                                  int T, int C, int K, void* stream) {
+                                  int T, int C, int K, float* ws, int64_t ws_floats, void* stream) {
   if (B <= 0 || T <= 0 || C <= 0 || (C % CC) != 0 || K != KMAX) return STE_ERR_SHAPE;
   dim3 grid((T + TT - 1) / TT, C / CC, B);
   if (dw) {
-    // ~8 row tiles per block: 8x fewer same-address atomics on dW (their contention, not the
-    // arithmetic, was most of this variant's time), still >= 2 blocks per CU at B = 64
-    const unsigned per = 8;   // measured 1/2/4/8/24 tiles: 237/200/196/186/188 us at T = 499
-    grid.x = (grid.x + per - 1) / per;
+    grid.x = dw_row_groups(T);
+    // with a workspace: per-block partial rows summed in order afterwards (deterministic dW)
+    const int64_t rows = (int64_t)B * grid.x;
+    float* part = (ws && ws_floats >= rows * C * K) ? ws : nullptr;
     hipLaunchKernelGGL((glu_dwconv_bwd_kernel<KMAX, true>), grid, dim3(NT), 0, (hipStream_t)stream, (const bf16*)pre,
-                       w, (const bf16*)dout, (bf16*)dpre, dw, T, C);
+                       w, (const bf16*)dout, (bf16*)dpre, dw, T, C, part);
+    STE_CHECK_LAUNCH();
+    if (part) return ste_rowsum_ordered(part, rows, C * K, 1, dw, stream);
+    return 0;
   }
-  else
-    hipLaunchKernelGGL((glu_dwconv_bwd_kernel<KMAX, false>), grid, dim3(NT), 0, (hipStream_t)stream, (const bf16*)pre,
-                       w, (const bf16*)dout, (bf16*)dpre, dw, T, C);
+  hipLaunchKernelGGL((glu_dwconv_bwd_kernel<KMAX, false>), grid, dim3(NT), 0, (hipStream_t)stream, (const bf16*)pre,
+                     w, (const bf16*)dout, (bf16*)dpre, dw, T, C, nullptr);
   STE_CHECK_LAUNCH();
   return 0;
 }

@@ -35,27 +35,56 @@ __global__ __launch_bounds__(NT) void embed_fwd_kernel(const int64_t* ids, int L
   }
 }
 
-// rows per block reduce the token-type gradient locally; word/position rows scatter with atomics
-__global__ __launch_bounds__(NT) void embed_bwd_kernel(const int64_t* ids, const int32_t* pos_ids, const float* dout,
-                                                     int rows, int D, int pad, float* dword, float* dpos,
-                                                     float* dtype0, int rows_per_block) {
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(rows, r0 + rows_per_block);
-  for (int c = threadIdx.x; c < D; c += NT) {
-    float tsum = 0.f;
-    for (int r = r0; r < r1; ++r) {
-      const float g = dout[(int64_t)r * D + c];
-      tsum += g;
-      const int64_t id = ids[r];
-      if (dword && id != pad) atomicAdd(dword + id * D + c, g);
-      const int p = pos_ids[r];
-      if (dpos && p != pad) atomicAdd(dpos + (int64_t)p * D + c, g);
+// word / position table rows of the embedding backward, deterministically: one wave per token row
+// r; the first row of each id sums the rows carrying that id in row order (ids cached in LDS as
+// int32 when they fit) and adds the sum to its table row — one writer per row, no atomics, so the
+// gradient is run-to-run identical (the rows of BOS / EOS and of each position repeat once per
+// transcript).  pad ids get nothing (nn.Embedding(padding_idx)).  D % 4 == 0, D <= 1024.
+constexpr int EMB_WAVES = 16;
+constexpr int EMB_LDS_IDS = 16384;
+template <typename IdT>
+__global__ __launch_bounds__(EMB_WAVES * 64) void embed_rows_ordered_kernel(const IdT* __restrict__ ids, int rows,
+                                                                          int D, int pad,
+                                                                          const float* __restrict__ dout,
+                                                                          float* __restrict__ table) {
+  extern __shared__ int sids[];
+  const bool in_lds = rows <= EMB_LDS_IDS;
+  if (in_lds)
+    for (int i = threadIdx.x; i < rows; i += EMB_WAVES * 64) sids[i] = (int)ids[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, r = blockIdx.x * EMB_WAVES + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  auto id_at = [&](int j) { return in_lds ? sids[j] : (int)ids[j]; };
+  const int id = id_at(r);
+  if (id == pad || id < 0) return;
+  for (int j0 = 0; j0 < r; j0 += 64) {   // an earlier row with this id owns the sum
+    const int j = j0 + lane;
+    if (__ballot(j < r && id_at(j) == id)) return;
+  }
+  f32x4 acc[4] = {};
+  for (int j0 = r; j0 < rows; j0 += 64) {
+    const int j = j0 + lane;
+    uint64_t m = __ballot(j < rows && id_at(j) == id);
+    while (m) {
+      const int k = __builtin_ctzll(m);
+      m &= m - 1;
+      const float* src = dout + (int64_t)(j0 + k) * D;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = (lane + 64 * q) * 4;
+        if (c < D) acc[q] += *reinterpret_cast<const f32x4*>(src + c);
+      }
     }
-    if (dtype0) atomicAdd(dtype0 + c, tsum);
+  }
+  float* dst = table + (int64_t)id * D;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = (lane + 64 * q) * 4;
+    if (c < D) *reinterpret_cast<f32x4*>(dst + c) += acc[q];
   }
 }
 
-__global__ __launch_bounds__(NT) void sumsq_kernel(const float* g, int64_t n, double* acc) {
+__global__ __launch_bounds__(NT) void sumsq_kernel(const float* g, int64_t n, double* acc, double* part) {
   __shared__ double red[NT / 64];
   double s = 0.0;
   float sf = 0.f;
@@ -77,8 +106,18 @@ __global__ __launch_bounds__(NT) void sumsq_kernel(const float* g, int64_t n, do
   if (threadIdx.x == 0) {
     double t = 0.0;
     for (int i = 0; i < NT / 64; ++i) t += red[i];
-    atomicAdd(acc, t);
+    if (part) part[blockIdx.x] = t;   // summed in block order by sumsq_final_kernel
+    else atomicAdd(acc, t);
   }
+}
+
+// acc += Σ_b part[b] (one wave: lane l sums blocks l, l+64, ... in order, then a fixed butterfly):
+// the deterministic second pass of sumsq_kernel
+__global__ __launch_bounds__(64) void sumsq_final_kernel(const double* part, int nb, double* acc) {
+  double t = 0.0;
+  for (int b = threadIdx.x; b < nb; b += 64) t += part[b];
+  t = wave_sum_d(t);
+  if (threadIdx.x == 0) acc[0] += t;
 }
 
 __global__ __launch_bounds__(NT) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
@@ -219,24 +258,44 @@ extern "C" int ste_text_embed_fwd(const int64_t* ids, int B, int L, int D, int p
   return 0;
 }
 
+extern "C" int64_t ste_text_embed_bwd_ws_floats(int B, int L, int D) {
+  return ste_colsum_ws_floats((int64_t)B * L, D);
+}
+
 extern "C" int ste_text_embed_bwd(const int64_t* ids, const int32_t* pos_ids, const float* dout, int B, int L, int D,
-                                  int pad_idx, float* dword, float* dpos, float* dtype0, void* stream) {
+                                  int pad_idx, float* dword, float* dpos, float* dtype0, float* ws, int64_t ws_floats,
+                                  void* stream) {
   const int rows = B * L;
-  if (rows <= 0) return STE_ERR_SHAPE;
-  const int rpb = 32;
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3((rows + rpb - 1) / rpb), dim3(NT), 0, (hipStream_t)stream, ids, pos_ids,
-                     dout, rows, D, pad_idx, dword, dpos, dtype0, rpb);
-  STE_CHECK_LAUNCH();
+  if (rows <= 0 || (D & 3) || D > 1024) return STE_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((rows + EMB_WAVES - 1) / EMB_WAVES);
+  const size_t lds = rows <= EMB_LDS_IDS ? (size_t)rows * 4 : 0;
+  if (dword) {
+    hipLaunchKernelGGL(embed_rows_ordered_kernel<int64_t>, grid, dim3(EMB_WAVES * 64), lds, s, ids, rows, D, pad_idx,
+                       dout, dword);
+    STE_CHECK_LAUNCH();
+  }
+  if (dpos) {
+    hipLaunchKernelGGL(embed_rows_ordered_kernel<int32_t>, grid, dim3(EMB_WAVES * 64), lds, s, pos_ids, rows, D,
+                       pad_idx, dout, dpos);
+    STE_CHECK_LAUNCH();
+  }
+  // token-type row 0: every row's gradient (ordered column sum with a workspace, else atomics)
+  if (dtype0) return ste_colsum(dout, 0, rows, D, D, dtype0, ws, ws_floats, stream);
   return 0;
 }
 
-extern "C" int ste_sumsq(const float* g, int64_t n, double* acc, void* stream) {
+extern "C" int ste_sumsq(const float* g, int64_t n, double* acc, double* part, void* stream) {
   if (n <= 0) return 0;
   if (((uintptr_t)g) & 15) return STE_ERR_ARG;
   unsigned gr = grid_for(n);
   if (gr > 2048) gr = 2048;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(gr), dim3(NT), 0, (hipStream_t)stream, g, n, acc);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(gr), dim3(NT), 0, (hipStream_t)stream, g, n, acc, part);
   STE_CHECK_LAUNCH();
+  if (part) {
+    hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, part, (int)gr, acc);
+    STE_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -224,7 +224,11 @@ STE_DEV void epilogue_tile(const ste_gemm_args& p, const float* epi, int nrows, 
   }
 }
 
-STE_DEV void colsum_flush(const ste_gemm_args& p, Csum csum, int col0, int col1, int batch, int lane) {
+// the wave's column sums: with a workspace (p.ws, ordered mode, see cs_plan) into partial row prow
+// = (batch·num_m + tile_m)·2 + wave row (the ordered second pass sums the rows in order: run-to-run
+// deterministic bias gradients), else one fp32 atomic per column
+STE_DEV void colsum_flush(const ste_gemm_args& p, Csum csum, int col0, int col1, int batch, int lane,
+                          int64_t prow) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
 #pragma unroll
@@ -236,6 +240,20 @@ STE_DEV void colsum_flush(const ste_gemm_args& p, Csum csum, int col0, int col1,
   const int cl = (lane & 7) * 8;
   const int col = cl < 32 ? col0 + cl : col1 + (cl - 32);
   if (lane < 8) {
+    if (p.ws) {
+      float* out = p.ws + prow * p.N + col;
+      if (col + 8 <= p.N && !(p.N & 3)) {
+        *reinterpret_cast<f32x4*>(out) = csum.lo;
+        *reinterpret_cast<f32x4*>(out + 4) = csum.hi;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (col + e < p.N) out[e] = csum.lo[e];
+          if (col + 4 + e < p.N) out[4 + e] = csum.hi[e];
+        }
+      }
+      return;
+    }
     float* out = p.colsum + (int64_t)batch * p.N + col;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -713,7 +731,8 @@ __global__ __launch_bounds__(small::NT, 2) void gemm_bf16_kernel(ste_gemm_args p
   __builtin_amdgcn_wave_barrier();
   Csum csum = {};
   epilogue_tile(p, epi, 64, m0 + wm * 64, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane, csum);
-  if (p.colsum) colsum_flush(p, csum, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane);
+  if (p.colsum)
+    colsum_flush(p, csum, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane, ((int64_t)batch * num_m + tm) * 2 + wm);
 }
 
 // ================================================================= big kernel
@@ -830,7 +849,8 @@ __global__ __launch_bounds__(big::NT, 2) void gemm_big_kernel(ste_gemm_args p) {
   STE_EPI_PASS(0) STE_EPI_PASS(1) STE_EPI_PASS(2) STE_EPI_PASS(3)
 #undef EPI_COL0
 #undef EPI_COL1
-  if (p.colsum) colsum_flush(p, csum, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane);
+  if (p.colsum)
+    colsum_flush(p, csum, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane, ((int64_t)batch * num_m + tm) * 2 + wm);
 }
 
 // ============================================================ 8-phase kernel
@@ -1052,7 +1072,8 @@ STE_DEV void epilogue_8ph(const ste_gemm_args& p, const f32x4 (&acc)[8][4], floa
 #undef STE_EPI_ROW0
 #undef STE_EPI_LOAD
 #undef STE_EPI_STORE
-  if (EF < 0 ? p.colsum != nullptr : (EF & EF_COLSUM) != 0) colsum_flush(p, csum, c0, c1, batch, lane);
+  if (EF < 0 ? p.colsum != nullptr : (EF & EF_COLSUM) != 0)
+    colsum_flush(p, csum, c0, c1, batch, lane, ((int64_t)batch * ((p.M + 255) >> 8) + (m0 >> 8)) * 2 + wm);
 }
 
 // steady-state operand wait: W pieces stay in flight (4 half-tiles = 8; MX adds the K-tile's scale
@@ -1731,15 +1752,38 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
     STE_CHECK_LAUNCH();
     return 0;
   }
-  if (mode > 0 && big_ok(a)) {
-    if (mode == 2) return a.b_kc ? launch_8ph<true, true>(a, s) : launch_8ph<true, false>(a, s);
-    if (a.b_kc) return launch_big<true, true>(a, s);
-    return launch_big<true, false>(a, s);
+  // column sums (bias gradients): with a large enough workspace every tile row writes its two waves'
+  // partial rows there and one ordered pass adds them up (run-to-run deterministic); without one,
+  // fp32 atomics.  The plans above never take a colsum launch, so ws is free for the partials.
+  const bool use_big = mode > 0 && big_ok(a);
+  int64_t cs_rows = 0;
+  if (a.colsum) {
+    const int bm = use_big ? 256 : small::BM;
+    const int64_t rows = 2 * (int64_t)((a.M + bm - 1) / bm);
+    if (a.ws && a.ws_bytes >= rows * a.batch * a.N * 4) cs_rows = rows;
   }
-  if (a.a_kc && a.b_kc) return launch_small<true, true>(a, s);
-  if (a.a_kc && !a.b_kc) return launch_small<true, false>(a, s);
-  if (!a.a_kc && !a.b_kc) return launch_small<false, false>(a, s);
-  return launch_small<false, true>(a, s);
+  if (!cs_rows) a.ws = nullptr;
+  int e;
+  if (use_big) {
+    if (mode == 2) e = a.b_kc ? launch_8ph<true, true>(a, s) : launch_8ph<true, false>(a, s);
+    else e = a.b_kc ? launch_big<true, true>(a, s) : launch_big<true, false>(a, s);
+  } else if (a.a_kc && a.b_kc) {
+    e = launch_small<true, true>(a, s);
+  } else if (a.a_kc && !a.b_kc) {
+    e = launch_small<true, false>(a, s);
+  } else if (!a.a_kc && !a.b_kc) {
+    e = launch_small<false, false>(a, s);
+  } else {
+    e = launch_small<false, true>(a, s);
+  }
+  if (e == 0 && cs_rows) e = ste_rowsum_ordered(a.ws, cs_rows, a.N, a.batch, a.colsum, stream);
+  return e;
+}
+
+extern "C" int64_t ste_gemm_colsum_ws_floats(const ste_gemm_args* args) {
+  if (!args || !args->colsum) return 0;
+  const int bm = 64;   // the smallest row tile of any GEMM kernel (ste_gemm_f32): an upper bound
+  return 2 * (int64_t)((args->M + bm - 1) / bm) * (args->batch > 0 ? args->batch : 1) * args->N;
 }
 
 // ============================================================ MX-fp8 GEMM (config 5)
@@ -1880,7 +1924,8 @@ __global__ __launch_bounds__(mx8::NT, 1) void gemm_mx8_kernel(ste_gemm_args p, c
 #undef STE_EPI_PASS
 #undef EPI_COL0
 #undef EPI_COL1
-  if (p.colsum) colsum_flush(p, csum, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane);
+  if (p.colsum)
+    colsum_flush(p, csum, n0 + wn * 64, n0 + wn * 64 + 32, batch, lane, ((int64_t)batch * num_m + tm) * 2 + wm);
 }
 
 // bf16 [rows][K] (row stride ld) -> e4m3 [rows][K] + E8M0 [rows][K/32].  Block scale 2^e with

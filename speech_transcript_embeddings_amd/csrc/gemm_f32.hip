@@ -163,10 +163,15 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(ste_gemm_args p, int kc) {
         }
         if (p.C3) ((bf16*)p.C3)[(int64_t)row * p.ldc3 + col] = (bf16)(p.c3_lo ? v - (float)(bf16)v : v);
       }
-    if (p.colsum) {  // the column's 4 lane groups hold disjoint rows: sum them, one atomic per column
+    if (p.colsum) {  // the column's 4 lane groups hold disjoint rows: sum them
       cs += __shfl_xor(cs, 16, 64);
       cs += __shfl_xor(cs, 32, 64);
-      if (g == 0 && cv) atomicAdd(p.colsum + col, cs);
+      // ordered mode: this wave's partial row (tile row x wave row) in ws, summed in order by the
+      // host's second pass; else one atomic per column
+      if (g == 0 && cv) {
+        if (p.ws) p.ws[((int64_t)blockIdx.x * 2 + (w & 1)) * p.N + col] = cs;
+        else atomicAdd(p.colsum + col, cs);
+      }
     }
   }
 }
@@ -239,8 +244,18 @@ extern "C" int ste_gemm_f32(const ste_gemm_args* args, void* stream) {
       return 0;
     }
   }
-  if (a.a_kc && a.b_kc) return launch<true, true>(a, s);
-  if (a.a_kc) return launch<true, false>(a, s);
-  if (a.b_kc) return launch<false, true>(a, s);
-  return launch<false, false>(a, s);
+  // column sums: ordered partial rows in ws when it is large enough (deterministic), else atomics
+  int64_t cs_rows = 0;
+  if (a.colsum) {
+    const int64_t rows = 2 * (int64_t)((a.M + BM - 1) / BM);
+    if (a.ws && a.ws_bytes >= rows * a.N * 4) cs_rows = rows;
+  }
+  if (!cs_rows) a.ws = nullptr;
+  int e;
+  if (a.a_kc && a.b_kc) e = launch<true, true>(a, s);
+  else if (a.a_kc) e = launch<true, false>(a, s);
+  else if (a.b_kc) e = launch<false, true>(a, s);
+  else e = launch<false, false>(a, s);
+  if (e == 0 && cs_rows) e = ste_rowsum_ordered(a.ws, cs_rows, a.N, 1, a.colsum, stream);
+  return e;
 }

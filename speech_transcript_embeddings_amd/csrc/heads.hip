@@ -145,7 +145,7 @@ __global__ __launch_bounds__(NT) void pool_dp_kernel(const T* h, const float* dp
 // masked positions get ds = 0 (the forward's masked_fill cuts their score gradient): that only
 // matters for an all-masked sample, whose weights are uniform rather than 0 at those positions
 __global__ __launch_bounds__(NT) void pool_dscore_kernel(const float* weights, const int32_t* mask, int L, float* dsc,
-                                                       float* db2) {
+                                                       float* db2, float* db2_part) {
   __shared__ float red[8];
   const int b = blockIdx.x, tid = threadIdx.x;
   float acc = 0.f;
@@ -159,7 +159,10 @@ __global__ __launch_bounds__(NT) void pool_dscore_kernel(const float* weights, c
     dbs += ds;
   }
   dbs = block_sum(dbs, red);
-  if (tid == 0 && db2) atomicAdd(db2, dbs);
+  if (tid == 0 && db2) {   // the sample's term; summed over samples in order by the host's second pass
+    if (db2_part) db2_part[b] = dbs;
+    else atomicAdd(db2, dbs);
+  }
 }
 
 template <typename T>
@@ -745,7 +748,7 @@ extern "C" int ste_attn_pool_fwd_f32(const float* t, const float* w2, const floa
 extern "C" int ste_attn_pool_bwd_work_floats(int B, int L, int Hh) {
   if (B <= 0 || L <= 0 || Hh <= 0) return STE_ERR_SHAPE;
   const int rows = pool_dz_rows(B, L);
-  return B * L + B * ((L + rows - 1) / rows) * 2 * Hh;
+  return B * L + B * ((L + rows - 1) / rows) * 2 * Hh + B;   // + the scorer bias' per-sample terms
 }
 
 template <typename T>
@@ -755,11 +758,15 @@ static int attn_pool_bwd(const T* t, const float* w2, const T* h, const float* w
   if (B <= 0 || L <= 0 || (Hh & 3) || (H & 3) || Hh > 4 * NT || !work || !dt) return STE_ERR_SHAPE;
   const int rows = pool_dz_rows(B, L), nchunk = (L + rows - 1) / rows;
   float* part = work + (int64_t)B * L;
+  float* db2_part = part + (int64_t)B * nchunk * 2 * Hh;
   hipLaunchKernelGGL(pool_dp_kernel<T>, dim3(B, (L + POOL_DP_ROWS - 1) / POOL_DP_ROWS), dim3(NT), 0, s, h, dpooled, L,
                      H, work);
   STE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(pool_dscore_kernel, dim3(B), dim3(NT), 0, s, weights, mask, L, work, db2);
+  hipLaunchKernelGGL(pool_dscore_kernel, dim3(B), dim3(NT), 0, s, weights, mask, L, work, db2, db2_part);
   STE_CHECK_LAUNCH();
+  if (db2) {
+    if (int e = ste_rowsum_ordered(db2_part, B, 1, 1, db2, s)) return e;
+  }
   hipLaunchKernelGGL(pool_dz_kernel<T>, dim3(B, nchunk), dim3(NT), 0, s, t, w2, weights, dpooled, work, L, Hh, H, dh,
                      dt, dt_lo, part, rows);
   STE_CHECK_LAUNCH();

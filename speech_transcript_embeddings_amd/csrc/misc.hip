@@ -54,7 +54,7 @@ __global__ void mask_cvt_kernel(const int64_t* m, float* f, int32_t* i32, int64_
 }
 // out[c] += Σ_r x[r, c]; block = 64-column stripe x row chunk, 256 threads = 16 cols x 16 row lanes (x4 vector)
 __global__ void colsum_kernel(const void* x, int is_bf16, int64_t rows, int cols, int64_t ld, float* out,
-                              int64_t rows_per_block) {
+                              int64_t rows_per_block, float* part) {
   __shared__ float red[16][65];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int c = blockIdx.x * 64 + tx * 4;
@@ -75,7 +75,41 @@ __global__ void colsum_kernel(const void* x, int is_bf16, int64_t rows, int cols
     float s = 0.f;
 #pragma unroll
     for (int y = 0; y < 16; ++y) s += red[y][threadIdx.x];
-    if (cc < cols) atomicAdd(out + cc, s);
+    if (cc < cols) {
+      if (part) part[(int64_t)blockIdx.y * cols + cc] = s;   // this row chunk's partial (ordered 2nd pass)
+      else atomicAdd(out + cc, s);
+    }
+  }
+}
+// out[b·cols + c] += Σ_r part[(b·R + r)·cols + c] in a fixed order (16 interleaved slices of the
+// rows, then the slices in order): the ordered second pass of every deterministic column sum
+// (GEMM bias gradients, ste_colsum, depthwise-conv and SpecAugment gradients).  grid
+// (ceil(cols / 64), batch), 1024 threads, 8 loads in flight per thread
+__global__ __launch_bounds__(1024) void rowsum_ordered_kernel(const float* __restrict__ part, int64_t R, int cols,
+                                                              float* out) {
+  __shared__ float red[16][64];
+  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + c;
+  float acc = 0.f;
+  if (col < cols) {
+    const float* p = part + (int64_t)blockIdx.y * R * cols + col;
+    int64_t r = sl;
+    for (; r + 7 * 16 < R; r += 8 * 16) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(r + 16 * u) * cols];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; r < R; r += 16) acc += p[r * cols];
+  }
+  red[sl][c] = acc;
+  __syncthreads();
+  if (sl == 0 && col < cols) {
+    float t = red[0][c];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t += red[k][c];
+    out[(int64_t)blockIdx.y * cols + col] += t;
   }
 }
 // y[r, c] = alpha * x[r, c] + beta * y[r, c] (fp32, strided rows)
@@ -149,7 +183,7 @@ __global__ __launch_bounds__(256) void spec_mask_fwd_kernel(float* x, int64_t ld
 }
 __global__ __launch_bounds__(256) void spec_mask_bwd_kernel(float* dx, int64_t ld, const int32_t* spec,
                                                             const float* valid, float* dembed, int64_t rows,
-                                                            int cols) {
+                                                            int cols, float* part) {
   for (int c0 = 0; c0 < cols; c0 += blockDim.x) {
     const int c = c0 + threadIdx.x;
     float acc = 0.f;
@@ -160,7 +194,11 @@ __global__ __launch_bounds__(256) void spec_mask_bwd_kernel(float* dx, int64_t l
         dx[r * ld + c] = 0.f;
       }
     }
-    if (dembed && c < cols && acc != 0.f) atomicAdd(dembed + c, acc);
+    if (part) {
+      if (c < cols) part[(int64_t)blockIdx.x * cols + c] = acc;
+    } else if (dembed && c < cols && acc != 0.f) {
+      atomicAdd(dembed + c, acc);
+    }
   }
 }
 }  // namespace
@@ -176,13 +214,28 @@ extern "C" int ste_spec_mask_fwd(float* x, int64_t ld, const int32_t* spec, cons
   return 0;
 }
 
+extern "C" int64_t ste_spec_mask_bwd_ws_floats(int64_t rows, int cols) {
+  return (rows < 512 ? rows : 512) * (int64_t)cols;
+}
+
 extern "C" int ste_spec_mask_bwd(float* dx, int64_t ld, const int32_t* spec, const float* valid, float* dembed,
-                                 int64_t rows, int cols, void* stream) {
+                                 int64_t rows, int cols, float* ws, int64_t ws_floats, void* stream) {
   if (rows <= 0 || cols <= 0) return 0;
   if (!dx || !spec || !valid) return STE_ERR_ARG;
   const int blocks = (int)(rows < 512 ? rows : 512);
+  float* part = (dembed && ws && ws_floats >= (int64_t)blocks * cols) ? ws : nullptr;
   hipLaunchKernelGGL(spec_mask_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dx, ld, spec, valid,
-                     dembed, rows, cols);
+                     dembed, rows, cols, part);
+  STE_CHECK_LAUNCH();
+  if (part) return ste_rowsum_ordered(part, blocks, cols, 1, dembed, stream);
+  return 0;
+}
+
+extern "C" int ste_rowsum_ordered(const float* part, int64_t rows, int cols, int batch, float* out, void* stream) {
+  if (rows <= 0 || cols <= 0 || batch <= 0) return 0;
+  if (!part || !out) return STE_ERR_ARG;
+  hipLaunchKernelGGL(rowsum_ordered_kernel, dim3((cols + 63) / 64, batch), dim3(1024), 0, (hipStream_t)stream, part,
+                     rows, cols, out);
   STE_CHECK_LAUNCH();
   return 0;
 }
@@ -217,13 +270,22 @@ extern "C" int ste_copy2d(void* y, int64_t ldy, const void* x, int64_t ldx, int6
   return 0;
 }
 
-extern "C" int ste_colsum(const void* x, int is_bf16, int64_t rows, int cols, int64_t ld, float* out, void* stream) {
+extern "C" int64_t ste_colsum_ws_floats(int64_t rows, int cols) {
+  return (rows + 511) / 512 * (int64_t)cols;
+}
+
+extern "C" int ste_colsum(const void* x, int is_bf16, int64_t rows, int cols, int64_t ld, float* out, float* ws,
+                          int64_t ws_floats, void* stream) {
   if (rows <= 0) return 0;
   if ((cols & 3) || (ld & 3)) return STE_ERR_SHAPE;
   const int64_t rpb = 512;
-  dim3 grid((cols + 63) / 64, (unsigned)((rows + rpb - 1) / rpb));
-  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, is_bf16, rows, cols, ld, out, rpb);
+  const int64_t chunks = (rows + rpb - 1) / rpb;
+  float* part = (ws && ws_floats >= chunks * cols) ? ws : nullptr;
+  dim3 grid((cols + 63) / 64, (unsigned)chunks);
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, is_bf16, rows, cols, ld, out, rpb,
+                     part);
   STE_CHECK_LAUNCH();
+  if (part) return ste_rowsum_ordered(part, chunks, cols, 1, out, stream);
   return 0;
 }
 

@@ -28,6 +28,31 @@ def _ld(t: torch.Tensor) -> int:
     return t.stride(-2)
 
 
+# True: column / table-row reductions through the library's fp32 atomics (its workspace-free path;
+# A/B runs and tests; STE_ATOMIC_SUMS=1 sets it for a whole run).  Default: ordered partial sums,
+# run-to-run deterministic gradients.
+ATOMIC_SUMS = os.environ.get("STE_ATOMIC_SUMS") == "1"
+_RED_WS = {}
+
+
+def _red_ws(dev, floats):
+    """Partial-sum workspace of the current stream for the ordered reductions (GEMM bias gradients,
+    ste_colsum, depthwise-conv / embedding / SpecAugment gradients), grown on demand.  Launches of
+    one stream run in order, so consecutive reductions reuse it; concurrent streams get their own.
+    None under ATOMIC_SUMS."""
+    if ATOMIC_SUMS or floats <= 0:
+        return None
+    key = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
+    w = _RED_WS.get(key)
+    if w is None or w.numel() < floats:
+        w = _RED_WS[key] = torch.empty(max(int(floats), 1 << 20), device=dev, dtype=F32)
+    return w
+
+
+def _ws_args(w):
+    return (None, 0) if w is None else (ptr(w), w.numel())
+
+
 # ------------------------------------------------------------------- GEMM
 def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf16=False, bias=None,
          act=_lib.ACT_NONE, pre_out=None, z=None, residual=None, alpha=1.0, beta=0.0, colsum=None,
@@ -84,7 +109,12 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
         args.row_scale = ptr(row_scale)
     args.alpha, args.beta, args.act = float(alpha), float(beta), int(act)
     args.drop_p, args.seed, args.drop_ld = float(drop_p), int(seed) & (2**64 - 1), int(drop_ld)
-    if ws is not None:  # split-K workspace (weight gradients), see include/ste.h
+    if colsum is not None and mx8 is None and not ATOMIC_SUMS:
+        # deterministic bias gradients: the ordered partial-sum plan needs a workspace this large
+        need = int(fn("ste_gemm_colsum_ws_floats")(C.byref(args)))
+        if ws is None or ws.numel() < need:
+            ws = _red_ws(a.device, need)
+    if ws is not None:  # split-K workspace (weight gradients) / column-sum partials, see include/ste.h
         assert ws.dtype == F32 and ws.is_contiguous()
         args.ws, args.ws_bytes = ptr(ws), ws.numel() * 4
     if mx8 is not None:
@@ -423,7 +453,9 @@ def glu_dwconv_fwd(pre, w, out, B, T):
 
 def glu_dwconv_bwd(pre, w, dout, dpre, dw, B, T):
     C_ = w.shape[0]
-    call("ste_glu_dwconv_bwd", ptr(pre), ptr(w), ptr(dout), ptr(dpre), ptr(dw), B, T, C_, w.shape[-1], _s())
+    ws = _red_ws(pre.device, int(fn("ste_glu_dwconv_bwd_ws_floats")(B, T, C_, w.shape[-1]))) if dw is not None else None
+    call("ste_glu_dwconv_bwd", ptr(pre), ptr(w), ptr(dout), ptr(dpre), ptr(dw), B, T, C_, w.shape[-1], *_ws_args(ws),
+         _s())
     return dpre
 
 
@@ -535,7 +567,8 @@ def xattn_bwd(q, k, v, probs, dout, B, S, nh, dq, dk, dv, seeds, drop_p=0.0, col
              float((P // nh) ** -0.5), float(drop_p), int(seeds[0]) & (2**64 - 1), int(seeds[-1]) & (2**64 - 1),
              ptr(dq), ptr(dk), ptr(dv), _ld(dk), ptr(part), _s())
         if colsum is not None:
-            call("ste_colsum", ptr(part), 0, B, 2 * P, 2 * P, ptr(colsum), _s())
+            w = _red_ws(q.device, int(fn("ste_colsum_ws_floats")(B, 2 * P)))
+            call("ste_colsum", ptr(part), 0, B, 2 * P, 2 * P, ptr(colsum), *_ws_args(w), _s())
         return
     assert colsum is None
     call("ste_xattn_bwd", ptr(q), ptr(k), ptr(v), _ld(k), ptr(probs), ptr(dout), ptr(mask), B, S, P, nh, nq,
@@ -622,13 +655,22 @@ def text_embed_fwd(ids, pad_idx, word, pos, type0, out, pos_ids):
 
 def text_embed_bwd(ids, pos_ids, dout, pad_idx, dword, dpos, dtype0):
     B, L = ids.shape
+    ws = _red_ws(dout.device, int(fn("ste_text_embed_bwd_ws_floats")(B, L, dout.shape[-1]))) if dtype0 is not None \
+        else None
     call("ste_text_embed_bwd", ptr(ids), ptr(pos_ids), ptr(dout), B, L, dout.shape[-1], pad_idx, ptr(dword),
-         ptr(dpos), ptr(dtype0), _s())
+         ptr(dpos), ptr(dtype0), *_ws_args(ws), _s())
 
 
 # -------------------------------------------------------------- optimizer
-def sumsq(g, acc):
-    call("ste_sumsq", ptr(g), g.numel(), ptr(acc), _s())
+SUMSQ_PARTS = 2048   # ste_sumsq's per-block fp64 partials (its grid is capped at 2048 blocks)
+
+
+def sumsq(g, acc, part=None):
+    """acc[0] += Σ g² (fp64); part (fp64 [SUMSQ_PARTS]): block sums added in block order."""
+    if ATOMIC_SUMS:
+        part = None
+    assert part is None or (part.dtype == torch.float64 and part.numel() >= SUMSQ_PARTS)
+    call("ste_sumsq", ptr(g), g.numel(), ptr(acc), ptr(part), _s())
 
 
 def adamw(p, g, m, v, p_bf16, *, lr, beta1, beta2, eps, wd, step, sumsq_acc=None, max_norm=1.0):
@@ -665,7 +707,10 @@ def spec_mask_fwd(x, spec, valid, embed):
 
 def spec_mask_bwd(dx, spec, valid, dembed=None):
     """dembed += Σ dx[r] over the SpecAugment rows, and dx[r] = 0 there."""
-    call("ste_spec_mask_bwd", ptr(dx), _ld(dx), ptr(spec), ptr(valid), ptr(dembed), dx.shape[0], dx.shape[1], _s())
+    ws = _red_ws(dx.device, int(fn("ste_spec_mask_bwd_ws_floats")(dx.shape[0], dx.shape[1]))) if dembed is not None \
+        else None
+    call("ste_spec_mask_bwd", ptr(dx), _ld(dx), ptr(spec), ptr(valid), ptr(dembed), dx.shape[0], dx.shape[1],
+         *_ws_args(ws), _s())
 
 
 def transpose16(src, dst=None):
@@ -680,8 +725,9 @@ def transpose16(src, dst=None):
 
 
 def colsum(x, out):
-    """out[c] += Σ_r x[r, c]."""
-    call("ste_colsum", ptr(x), int(x.dtype == BF16), x.shape[0], x.shape[1], _ld(x), ptr(out), _s())
+    """out[c] += Σ_r x[r, c] (ordered partial sums: run-to-run deterministic)."""
+    ws = _red_ws(x.device, int(fn("ste_colsum_ws_floats")(x.shape[0], x.shape[1])))
+    call("ste_colsum", ptr(x), int(x.dtype == BF16), x.shape[0], x.shape[1], _ld(x), ptr(out), *_ws_args(ws), _s())
     return out
 
 

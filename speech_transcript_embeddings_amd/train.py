@@ -67,6 +67,7 @@ class FusedAdamW:
         self.exp_avg = torch.zeros(st.n_grad, device=st.device, dtype=F32)
         self.exp_avg_sq = torch.zeros(st.n_grad, device=st.device, dtype=F32)
         self.sumsq = torch.zeros(1, device=st.device, dtype=torch.float64)
+        self.sumsq_part = torch.zeros(ops.SUMSQ_PARTS, device=st.device, dtype=torch.float64)  # ordered Σg²
         self.t = 0
         self.last_factor = 1.0
 
@@ -165,7 +166,7 @@ class FusedAdamW:
         self.last_factor = lr_factor
         self.sumsq.zero_()
         if self.max_norm is not None:
-            ops.sumsq(st.grad[: st.n_grad], self.sumsq)
+            ops.sumsq(st.grad[: st.n_grad], self.sumsq, self.sumsq_part)
         for gr in self.groups:
             a, b = gr["range"]
             if b <= a:

@@ -488,7 +488,7 @@ def _head_stand_ins():
         dtp.copy_(dsp[:, None] * an)
         dtn.copy_(dsn[:, None] * an)
 
-    def sumsq(g, acc):
+    def sumsq(g, acc, part=None):
         acc += (g.double() ** 2).sum()
 
     def adamw(master, grad, m, v, shadow, lr, beta1, beta2, eps, wd, step, sumsq_acc=None, max_norm=1.0):
