@@ -71,8 +71,40 @@ def q(x, f, b):
     return _Q.apply(x, bool(f), bool(b)) if (f or b) else x
 
 
+def mx8(x):
+    """OCP MX-fp8 round trip along the last dim (ste_mx8_quant): blocks of 32, scale
+    2^ceil(log2(amax / 448)) (no saturation), e4m3 round-to-nearest-even, dequantised."""
+    shp = x.shape
+    xb = x.reshape(-1, shp[-1] // 32, 32)
+    amax = xb.abs().amax(-1, keepdim=True)
+    e = torch.ceil(torch.log2(torch.clamp(amax, min=1e-30) / 448.0))
+    scale = torch.where(amax > 0, torch.exp2(e), torch.full_like(amax, 2.0 ** -127))
+    qv = (xb / scale).to(torch.float8_e4m3fn).to(torch.float32)
+    return (qv * scale).reshape(shp)
+
+
+class _LinMX8(torch.autograd.Function):
+    """config 5's fp8 forward GEMM: y = mx8(x)·mx8(W)ᵀ + b; straight-through backward on the bf16
+    operands (dX = dY·W, dW = dYᵀ·x), as engine.py's fp8_gemm path runs it."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return F.linear(mx8(x), mx8(W), b)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W = ctx.saved_tensors
+        gx = g @ W
+        gW = g.reshape(-1, g.shape[-1]).t() @ x.reshape(-1, x.shape[-1])
+        gb = g.reshape(-1, g.shape[-1]).sum(0) if ctx.has_b else None
+        return gx, gW, gb
+
+
 class Probe:
-    def __init__(self, fl, autocast=False, wclasses=WCLASSES, wlayers=None, fasites=None, falayers=None):
+    def __init__(self, fl, autocast=False, wclasses=WCLASSES, wlayers=None, fasites=None, falayers=None,
+                 fp8=()):
         self.fl = {k: bool(fl.get(k, False)) for k in FLAGS}
         self.ac = autocast   # reference-under-autocast: scores / probabilities in bf16 storage too
         self.wclasses = set(wclasses)
@@ -80,6 +112,7 @@ class Probe:
         self.layer = None
         self.fasites = None if fasites is None else set(fasites)   # None: every site rounds (with "fa")
         self.falayers = falayers
+        self.fp8 = set(fp8)   # GEMM classes (qkv, o, ffn, conv) on MX-fp8 forward operands (config 5)
 
     def fa(self, site):
         """forward rounding of an activation at `site` (qkv_in, qkv_out, o, ffn_in, ffn_h, conv_in,
@@ -102,7 +135,7 @@ class Probe:
         fl = self.fl
         xa = q(x, self.fa(in_site), fl["bdx"] and dx_round)
         Wa = self.wq(W, cls)
-        y = F.linear(xa, Wa, b)
+        y = _LinMX8.apply(xa, Wa, b) if (cls in self.fp8 and self.layer is not None) else F.linear(xa, Wa, b)
         return q(y, out_site is not None and self.fa(out_site), fl["bdy"])
 
     def ln(self, p, name, x, eps=1e-5):
@@ -299,6 +332,12 @@ def main(argv=None):
         sets += [("hip, bf16 weights only in the trainable layers", allon, False, dict(wlayers=topl)),
                  ("hip, bf16 weights only in the frozen layers", allon, False,
                   dict(wlayers=set(range(ac.layers)) - topl))]
+    if "fp8" in want:   # config 5: MX-fp8 forward GEMMs of the Conformer layers, by GEMM class
+        allc = ("qkv", "o", "ffn", "conv")
+        sets.append(("hip + fp8 forward GEMMs (all classes)", allon, False, dict(fp8=allc)))
+        sets += [(f"hip + fp8 forward GEMMs except {c}", allon, False, dict(fp8=tuple(x for x in allc if x != c)))
+                 for c in allc]
+        sets += [(f"hip + fp8 forward GEMMs only {c}", allon, False, dict(fp8=(c,))) for c in allc]
     if "inputs" in want:   # conditioning: the fp32 graph on input features rounded to bf16 (one ulp)
         sets.append(("fp32 graph, input features rounded to bf16", {}, False, dict(round_feats=True)))
         sets.append(("fp32 graph, weights rounded to bf16", {"w": True}, False))
