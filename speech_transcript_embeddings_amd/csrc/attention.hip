@@ -623,58 +623,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(ste_attn_args a) {
   }
 }
 
-// ================================================ dE[j][d] += scale * Σ_rows G[row][j] Q[row][d]
-// rows = (b, h, q); 256 threads each own 20 (j, d) outputs; rows staged 32 at a time.
-__global__ __launch_bounds__(256) void attn_rel_dE_kernel(ste_attn_args a, int64_t rows_per_block) {
-  __shared__ float sG[32][NREL];
-  __shared__ float sQ[32][HD];
-  const int tid = threadIdx.x;
-  const int nrel = a.rel_left + a.rel_right + 1;
-  const int64_t total = (int64_t)a.B * a.H * a.T;
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t r1 = r0 + rows_per_block < total ? r0 + rows_per_block : total;
-  float acc[20];
-#pragma unroll
-  for (int i = 0; i < 20; ++i) acc[i] = 0.f;
-  for (int64_t rb = r0; rb < r1; rb += 32) {
-    __syncthreads();
-    for (int i = tid; i < 32 * NREL; i += 256) {
-      int rr = i / NREL, j = i % NREL;
-      int64_t row = rb + rr;
-      sG[rr][j] = row < r1 ? a.gwork[row * NREL + j] : 0.f;
-    }
-    for (int i = tid; i < 32 * HD; i += 256) {
-      int rr = i / HD, d = i % HD;
-      int64_t row = rb + rr;
-      float v = 0.f;
-      if (row < r1) {
-        int q = row % a.T;
-        int64_t bh = row / a.T;
-        int h = bh % a.H, b = bh / a.H;
-        v = (float)((const bf16*)a.q)[(int64_t)(b * a.T + q) * a.ldq + h * HD + d];
-      }
-      sQ[rr][d] = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 20; ++i) {
-      const int o = tid + 256 * i;
-      if (o < NREL * HD) {
-        const int j = o / HD, d = o % HD;
-        float s = acc[i];
-#pragma unroll 8
-        for (int rr = 0; rr < 32; ++rr) s += sG[rr][j] * sQ[rr][d];
-        acc[i] = s;
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 20; ++i) {
-    const int o = tid + 256 * i;
-    if (o < nrel * HD) atomicAdd(a.dE + o, acc[i] * a.scale);
-  }
-}
-
 // ============================================== relative-key forward, v2 (audio self-attention)
 // 4 waves x 32 queries (two 16-row groups that share every K/V fragment read, halving LDS
 // traffic per MFMA), 128 queries per block.  K/V tiles of 64 keys and their key-mask words
@@ -2253,49 +2201,44 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
 }
 
 // ============================== dE[j][d] += scale * Σ_(b,h,t) G[(b,h,t)][j] · Q[b*T+t][h*64+d]
-// One block per (batch, head): its T rows of G (fp32 [T][80]) and Q (bf16 columns h*64..)
-// are staged 64 rows at a time; 256 threads each own 20 of the 80 x 64 outputs (j = tid/16
-// + 16k, d = 4*(tid%16)..+3) and accumulate in fp32; one atomic add per output per block.
+// The small-T form (T < 64, where the MFMA kernel below has no room for its partial): block k
+// owns bins 16k..16k+15 (thread: bin 16k + tid/16, d = 4*(tid%16)..+3) and walks every (b,h) and
+// every row in a fixed order, staging 64 rows of G and Q at a time; one plain store per output,
+// so dE is run-to-run identical.  Grid: ceil(nrel / 16) blocks.
 __global__ __launch_bounds__(256) void attn_rel_dE2_kernel(ste_attn_args a) {
-  __shared__ float sG[64][NREL + 4];
+  __shared__ float sG[64][16];
   __shared__ float sQ[64][HD];
   const int tid = threadIdx.x;
-  const int bh = blockIdx.x, h = bh % a.H, b = bh / a.H;
-  const int T = a.T;
+  const int T = a.T, nbh = a.B * a.H;
   const int nrel = a.rel_left + a.rel_right + 1;
-  const int jr = tid >> 4, d0 = (tid & 15) * 4;
-  f32x4 acc[5];
+  const int j0 = 16 * blockIdx.x, jr = tid >> 4, d0 = (tid & 15) * 4;
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int bh = 0; bh < nbh; ++bh) {
+    const int h = bh % a.H, b = bh / a.H;
+    const float* G = a.gwork + (int64_t)bh * T * NREL + j0;
+    const bf16* Q = (const bf16*)a.q + (int64_t)b * T * a.ldq + h * HD;
+    for (int t0 = 0; t0 < T; t0 += 64) {
+      const int nr = min(64, T - t0);
+      __syncthreads();
+      {
+        const int r = tid >> 2, c = (tid & 3) * 4;
+        const f32x4 v = r < nr ? *reinterpret_cast<const f32x4*>(G + (int64_t)(t0 + r) * NREL + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(&sG[r][c]) = v;
+      }
+      for (int i = tid; i < 64 * (HD / 8); i += 256) {
+        const int r = i / (HD / 8), c = (i % (HD / 8)) * 8;
+        const bf16x8 v = r < nr ? *reinterpret_cast<const bf16x8*>(Q + (int64_t)(t0 + r) * a.ldq + c) : bf16x8{};
 #pragma unroll
-  for (int k = 0; k < 5; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float* G = a.gwork + (int64_t)bh * T * NREL;
-  const bf16* Q = (const bf16*)a.q + (int64_t)b * T * a.ldq + h * HD;
-  for (int t0 = 0; t0 < T; t0 += 64) {
-    const int nr = min(64, T - t0);
-    __syncthreads();
-    for (int i = tid; i < 64 * (NREL / 4); i += 256) {
-      const int r = i / (NREL / 4), c = (i % (NREL / 4)) * 4;
-      const f32x4 v = r < nr ? *reinterpret_cast<const f32x4*>(G + (int64_t)(t0 + r) * NREL + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-      *reinterpret_cast<f32x4*>(&sG[r][c]) = v;
-    }
-    for (int i = tid; i < 64 * (HD / 8); i += 256) {
-      const int r = i / (HD / 8), c = (i % (HD / 8)) * 8;
-      const bf16x8 v = r < nr ? *reinterpret_cast<const bf16x8*>(Q + (int64_t)(t0 + r) * a.ldq + c) : bf16x8{};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) sQ[r][c + e] = (float)v[e];
-    }
-    __syncthreads();
-    for (int r = 0; r < nr; ++r) {
-      const f32x4 q = *reinterpret_cast<const f32x4*>(&sQ[r][d0]);
-#pragma unroll
-      for (int k = 0; k < 5; ++k) acc[k] += q * sG[r][jr + 16 * k];
+        for (int e = 0; e < 8; ++e) sQ[r][c + e] = (float)v[e];
+      }
+      __syncthreads();
+      for (int r = 0; r < nr; ++r) acc += *reinterpret_cast<const f32x4*>(&sQ[r][d0]) * sG[r][jr];
     }
   }
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const int j = jr + 16 * k;
-    if (j < nrel)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(a.dE + j * HD + d0 + e, acc[k][e] * a.scale);
+  const int j = j0 + jr;
+  if (j < nrel) {
+    f32x4* o = reinterpret_cast<f32x4*>(a.dE + j * HD + d0);
+    *o = *o + acc * a.scale;
   }
 }
 
@@ -2414,7 +2357,7 @@ constexpr int DKV_LDS = 4 * TILE + NREL * 128 + 64 * NREL * 4 + 2 * 128 * 4;
 template <template <bool, bool> class K>
 struct Dispatch;
 
-// STE_ATTN_DE=2: the VALU dE kernel (atomics) instead of the MFMA one (A/B runs)
+// STE_ATTN_DE=2: the small-T VALU dE kernel instead of the MFMA one at every T (A/B runs)
 bool rel_de3() {
   static int v = -1;
   if (v < 0) {
@@ -2472,6 +2415,21 @@ int check(const ste_attn_args* a) {
   return 0;
 }
 
+// dE from the per-row G rows every backward variant leaves in gwork ([(b,h,t)][NREL] fp32):
+// the MFMA kernel + ordered partial sum when T >= 64, else the small-T kernel; both fixed-order.
+int launch_dE(const ste_attn_args* a, hipStream_t s) {
+  const int nrel = a->rel_left + a->rel_right + 1;
+  if (a->T >= rel_de::MIN_T && rel_de3()) {
+    hipLaunchKernelGGL(attn_rel_dE3_kernel, dim3((unsigned)(a->B * a->H)), dim3(256), rel_de::LDS, s, *a);
+    STE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(attn_rel_dE3_sum_kernel, dim3((unsigned)nrel), dim3(1024), 0, s, *a);
+  } else {
+    hipLaunchKernelGGL(attn_rel_dE2_kernel, dim3((unsigned)((nrel + 15) / 16)), dim3(256), 0, s, *a);
+  }
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace
 
 extern "C" int ste_attention_fwd(const ste_attn_args* a, void* stream) {
@@ -2508,7 +2466,6 @@ extern "C" int ste_attention_bwd(const ste_attn_args* a, void* stream) {
   if ((a->lddo & 7) || (a->lddq & 3) || (a->lddk & 3) || (a->lddv & 3)) return STE_ERR_SHAPE;
   if (a->dE && (!a->gwork || !a->rel_E)) return STE_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  const int64_t nrow = (int64_t)a->B * a->T * a->H;
   if (a->rel_E && a->drop_p == 0.f && rel_v2()) {
     if (rel_dq_v3() && a->rel_left + a->rel_right + 1 < rel2::GT3) {   // bin GT3-1 is the spare slot
       dim3 gq((unsigned)(((a->T + rel2::DQ3_Q - 1) / rel2::DQ3_Q) * a->H * a->B));
@@ -2522,17 +2479,7 @@ extern "C" int ste_attention_bwd(const ste_attn_args* a, void* stream) {
     if (rel_bwd_v3()) hipLaunchKernelGGL(attn_bwd_dkv_rel3_kernel, gk, dim3(NT), rel2::DKV3_LDS, s, *a);
     else hipLaunchKernelGGL(attn_bwd_dkv_rel2_kernel, gk, dim3(NT), rel2::DKV_LDS, s, *a);
     STE_CHECK_LAUNCH();
-    if (a->dE) {
-      if (a->T >= rel_de::MIN_T && rel_de3()) {
-        hipLaunchKernelGGL(attn_rel_dE3_kernel, dim3((unsigned)(a->B * a->H)), dim3(256), rel_de::LDS, s, *a);
-        STE_CHECK_LAUNCH();
-        hipLaunchKernelGGL(attn_rel_dE3_sum_kernel, dim3((unsigned)(a->rel_left + a->rel_right + 1)), dim3(1024), 0, s,
-                           *a);
-      } else {
-        hipLaunchKernelGGL(attn_rel_dE2_kernel, dim3((unsigned)(a->B * a->H)), dim3(256), 0, s, *a);
-      }
-      STE_CHECK_LAUNCH();
-    }
+    if (a->dE) return launch_dE(a, s);
     return 0;
   }
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)(((int64_t)a->B * a->T + 3) / 4)), dim3(256), 0, s, *a);
@@ -2548,11 +2495,6 @@ extern "C" int ste_attention_bwd(const ste_attn_args* a, void* stream) {
   STE_LAUNCH2(attn_bwd_dq_kernel, DQ_LDS)
   STE_LAUNCH2(attn_bwd_dkv_kernel, DKV_LDS)
 #undef STE_LAUNCH2
-  if (a->dE) {
-    const int blocks = 512;
-    int64_t rpb = (nrow + blocks - 1) / blocks;
-    hipLaunchKernelGGL(attn_rel_dE_kernel, dim3(blocks), dim3(256), 0, s, *a, rpb);
-    STE_CHECK_LAUNCH();
-  }
+  if (a->dE) return launch_dE(a, s);
   return 0;
 }

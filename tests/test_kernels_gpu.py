@@ -676,15 +676,17 @@ def _attn_case(ops, B, T, H, rel, masked, drop_p, seed=7, qk_scale=0.7, v_common
     return errs
 
 
-@pytest.mark.parametrize("T", [40, 99, 150, 499])   # T < 64: the atomic dE kernel; else the MFMA one
+@pytest.mark.parametrize("T", [40, 99, 150, 499])   # T < 64: the small-T dE kernel; else the MFMA one
 def test_attention_relkey(ops, T):
     _attn_case(ops, B=2, T=T, H=2, rel=True, masked=True, drop_p=0.0)
 
 
-def test_attention_relkey_dE_deterministic(ops):
-    """The MFMA dE kernel writes one partial per (batch, head) and sums them in a fixed order:
+@pytest.mark.parametrize("T", [40, 130])
+def test_attention_relkey_dE_deterministic(ops, T):
+    """The MFMA dE kernel (T >= 64) writes one partial per (batch, head) and sums them in a fixed
+    order; the small-T kernel walks every (batch, head) and row in order, one block per 16 bins:
     two identical backward calls give bit-identical dE (16 partials here, > one 16-way lane group)."""
-    B, T, H, D = 4, 130, 4, 64
+    B, H, D = 4, 4, 64
     W = H * D
     torch.manual_seed(7)
     qkv = (torch.randn(B * T, 3 * W, device=DEV) * 0.5).bfloat16()
