@@ -1123,60 +1123,77 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
       const bool all_lo = (kb + TK - 1) - q0g <= -left;
       const bool all_hi = kb - (q0g + 15) >= right;
       const bool band = !(all_lo || all_hi || (STE_ABLATE & 512));
-      if (!band) {
-        const float bc = all_lo ? blo[gq] : bhi[gq];
+      // raise the running max only when a row grew past m + THRESH (deferred rescale)
+      auto rescale = [&](float tmax) {
+        if (__builtin_amdgcn_ballot_w64(tmax > m[gq] + THRESH) != 0ull) {
+          const float mnew = fmaxf(m[gq], tmax);
+          const float alpha = __builtin_amdgcn_exp2f(m[gq] - mnew);
+          if (SPLIT) lp[gq] *= alpha;
+          else lsum[gq] *= alpha;
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_fmaf(s[gq][t][r], c2, bc);
-      } else {
-        const float* qrow = reinterpret_cast<const float*>(sm + qe_off) + (w * WQ + 16 * gq + li) * QS + PADL;
-        const int d0 = kb + 4 * g - myq + left;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const float* qp = qrow + med3i(d0 + 16 * t, -PADL, nrel);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_fmaf(s[gq][t][r], c2, qp[r]);
+          for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
+          m[gq] = mnew;
         }
-      }
-      if constexpr (MASKED) {   // key kb+16t+4g+r: past T -> -inf, masked -> finfo.min (as rel2)
-        const uint64_t okb = okw_of(kt);
-        const uint32_t wlo = (uint32_t)(okb >> (4 * g)), whi = (uint32_t)(okb >> (32 + 4 * g));
-        const int lim = T - kb - 4 * g;
+      };
+      // row max as a depth-3 tree (a sequential max3 chain serialises 8 dependent VALU ops)
+      auto tile_max = [&]() {
+        const float t0 = max3f(s[gq][0][0], s[gq][0][1], s[gq][0][2]);
+        const float t1 = max3f(s[gq][0][3], s[gq][1][0], s[gq][1][1]);
+        const float t2 = max3f(s[gq][1][2], s[gq][1][3], s[gq][2][0]);
+        const float t3 = max3f(s[gq][2][1], s[gq][2][2], s[gq][2][3]);
+        const float t4 = max3f(s[gq][3][0], s[gq][3][1], s[gq][3][2]);
+        const float u0 = max3f(t0, t1, t2), u1 = max3f(t3, t4, s[gq][3][3]);
+        return max3f(u0, u1, u1);
+      };
+      if (!band && !MASKED) {
+        // outside the distance band every key of the tile has the same bias bc: the max runs on the
+        // raw scores (c2 > 0), and p = exp2(s*c2 + (bc - m)) is one fma + exp per score
+        const float bc = all_lo ? blo[gq] : bhi[gq];
+        rescale(rowmax4(__builtin_fmaf(tile_max(), c2, bc)));
+        const float cb = bc - m[gq];
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const uint32_t wd = t < 2 ? wlo : whi;
-            const bool ok = (wd >> (16 * (t & 1) + r)) & 1u;
-            const float fill = 16 * t + r < lim ? NEG_MASK : -INFINITY;
-            s[gq][t][r] = ok ? s[gq][t][r] : fill;
+          for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[gq][t][r], c2, cb));
+      } else {
+        if (!band) {
+          const float bc = all_lo ? blo[gq] : bhi[gq];
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_fmaf(s[gq][t][r], c2, bc);
+        } else {
+          const float* qrow = reinterpret_cast<const float*>(sm + qe_off) + (w * WQ + 16 * gq + li) * QS + PADL;
+          const int d0 = kb + 4 * g - myq + left;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const float* qp = qrow + med3i(d0 + 16 * t, -PADL, nrel);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_fmaf(s[gq][t][r], c2, qp[r]);
           }
+        }
+        if constexpr (MASKED) {   // key kb+16t+4g+r: past T -> -inf, masked -> finfo.min (as rel2)
+          const uint64_t okb = okw_of(kt);
+          const uint32_t wlo = (uint32_t)(okb >> (4 * g)), whi = (uint32_t)(okb >> (32 + 4 * g));
+          const int lim = T - kb - 4 * g;
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t wd = t < 2 ? wlo : whi;
+              const bool ok = (wd >> (16 * (t & 1) + r)) & 1u;
+              const float fill = 16 * t + r < lim ? NEG_MASK : -INFINITY;
+              s[gq][t][r] = ok ? s[gq][t][r] : fill;
+            }
+        }
+        rescale(rowmax4(tile_max()));
+        const float mg = m[gq];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            s[gq][t][r] = (STE_ABLATE & 128) ? s[gq][t][r] - mg : __builtin_amdgcn_exp2f(s[gq][t][r] - mg);
       }
-      // row max as a depth-3 tree (a sequential max3 chain serialises 8 dependent VALU ops)
-      const float t0 = max3f(s[gq][0][0], s[gq][0][1], s[gq][0][2]);
-      const float t1 = max3f(s[gq][0][3], s[gq][1][0], s[gq][1][1]);
-      const float t2 = max3f(s[gq][1][2], s[gq][1][3], s[gq][2][0]);
-      const float t3 = max3f(s[gq][2][1], s[gq][2][2], s[gq][2][3]);
-      const float t4 = max3f(s[gq][3][0], s[gq][3][1], s[gq][3][2]);
-      const float u0 = max3f(t0, t1, t2), u1 = max3f(t3, t4, s[gq][3][3]);
-      const float tmax = rowmax4(max3f(u0, u1, u1));
-      // deferred rescale: raise the running max only when a row grew past m + THRESH
-      if (__builtin_amdgcn_ballot_w64(tmax > m[gq] + THRESH) != 0ull) {
-        const float mnew = fmaxf(m[gq], tmax);
-        const float alpha = __builtin_amdgcn_exp2f(m[gq] - mnew);
-        if (SPLIT) lp[gq] *= alpha;
-        else lsum[gq] *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
-        m[gq] = mnew;
-      }
-      const float mg = m[gq];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          s[gq][t][r] = (STE_ABLATE & 128) ? s[gq][t][r] - mg : __builtin_amdgcn_exp2f(s[gq][t][r] - mg);
       if (SPLIT) {   // the row sum of p itself (hi + lo P sums to p within 2^-16): fp32 adds, not 2 MFMAs per u
         f32x4 t01 = (s[gq][0] + s[gq][1]) + (s[gq][2] + s[gq][3]);
         lp[gq] += (t01[0] + t01[1]) + (t01[2] + t01[3]);
@@ -2088,8 +2105,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
       }
       if (g == 0) {   // (addresses from a regenerated lane id: see lane_now)
         const int l16 = lane_now() & 15;
-        elo[16 * w + l16] = qrow[0] * c2;
-        ehi[16 * w + l16] = qrow[nrel - 1] * c2;
+        const float nl = sL[16 * w + l16] * -LOG2E;   // the row's -LSE, folded into its edge biases
+        elo[16 * w + l16] = qrow[0] * c2 + nl;
+        ehi[16 * w + l16] = qrow[nrel - 1] * c2 + nl;
       }
     }
     __syncthreads();
@@ -2098,6 +2116,14 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       f32x4 sc[2][2], dp[2][2];
+      // per-lane query vectors (queries 16n + 4g + r): lse, and -delta as dP's initial accumulator
+      // (dP - delta leaves the MFMA chain ready)
+      f32x4 lsev[2], ndl[2];
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) {
+        lsev[nn] = *reinterpret_cast<const f32x4*>(sL + 16 * (2 * u + nn) + 4 * g);
+        ndl[nn] = -*reinterpret_cast<const f32x4*>(sL + 64 + 16 * (2 * u + nn) + 4 * g);
+      }
 #pragma unroll
       for (int nn = 0; nn < 2; ++nn) {
         const int n = 2 * u + nn;
@@ -2110,7 +2136,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
 #pragma unroll
         for (int gk = 0; gk < 2; ++gk) {
           sc[gk][nn] = mfma16(qa[0], kf[gk][0], f32x4{0.f, 0.f, 0.f, 0.f});
-          dp[gk][nn] = mfma16(da[0], vf[gk][0], f32x4{0.f, 0.f, 0.f, 0.f});
+          dp[gk][nn] = mfma16(da[0], vf[gk][0], ndl[nn]);
           sc[gk][nn] = mfma16(qa[1], kf[gk][1], sc[gk][nn]);
           dp[gk][nn] = mfma16(da[1], vf[gk][1], dp[gk][nn]);
         }
@@ -2124,13 +2150,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
         trd[dt] = frag_tr_asm(tD, dt * 16, u, lane);
         trq[dt] = frag_tr_asm(tQ, dt * 16, u, lane);
       }
-      // per-lane query vectors (queries 16n + 4g + r): lse, delta
-      f32x4 lsev[2], dlt[2];
-#pragma unroll
-      for (int nn = 0; nn < 2; ++nn) {
-        lsev[nn] = *reinterpret_cast<const f32x4*>(sL + 16 * (2 * u + nn) + 4 * g);
-        dlt[nn] = *reinterpret_cast<const f32x4*>(sL + 64 + 16 * (2 * u + nn) + 4 * g);
-      }
       bf16x8 pv[2], pk[2];
 #pragma unroll
       for (int gk = 0; gk < 2; ++gk) {
@@ -2140,12 +2159,12 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
 #pragma unroll
         for (int nn = 0; nn < 2; ++nn) {
           const int n = 2 * u + nn;
-          const f32x4 nl2 = lsev[nn] * -LOG2E;
-          if (all_lo || all_hi) {
+          if (all_lo || all_hi) {   // edge bias - LSE per query, precomputed
             const f32x4 eb = *reinterpret_cast<const f32x4*>((all_lo ? elo : ehi) + 16 * n + 4 * g);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r], c2, eb[r] + nl2[r]));
+            for (int r = 0; r < 4; ++r) sc[gk][nn][r] = __builtin_amdgcn_exp2f(fmaf(sc[gk][nn][r], c2, eb[r]));
           } else {
+            const f32x4 nl2 = lsev[nn] * -LOG2E;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int ql = 16 * n + 4 * g + r;
@@ -2163,7 +2182,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
             for (int r = 0; r < 4; ++r)
               if (qb + 16 * n + 4 * g + r >= T) sc[gk][nn][r] = 0.f;
           }
-          dp[gk][nn] = sc[gk][nn] * (dp[gk][nn] - dlt[nn]) * a.scale;   // dS * scale (for dK)
+          dp[gk][nn] = sc[gk][nn] * dp[gk][nn];   // dS (its scale applied to dK at the store)
         }
         pv[gk] = pack_acc(sc[gk][0], sc[gk][1]);
         pk[gk] = pack_acc(dp[gk][0], dp[gk][1]);
@@ -2193,7 +2212,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args 
       bf16* dV = (bf16*)a.dv + (int64_t)(bT + key) * a.lddv + h * HD;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        store_bf16x4(dK + 16 * dt + 4 * g, dk[gk][dt]);
+        store_bf16x4(dK + 16 * dt + 4 * g, dk[gk][dt] * a.scale);
         store_bf16x4(dV + 16 * dt + 4 * g, dv[gk][dt]);
       }
     }

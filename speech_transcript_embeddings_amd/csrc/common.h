@@ -47,15 +47,41 @@ STE_DEV void store_bf16x4_split(bf16* hi_p, bf16* lo_p, f32x4 v) {
 }
 
 // ---------------------------------------------------------------- wave reductions
+// Cross-lane steps without LDS: DPP within each 16-lane row (quad_perm xor 1, xor 2, then
+// row_half_mirror and row_mirror, which pair the row's quads and halves), then
+// v_permlane32_swap / v_permlane16_swap across the rows (__shfl_xor compiles to ds_bpermute:
+// an LDS round trip and an lgkmcnt drain per step).  Every step adds the same two values in
+// both partner lanes, so all 64 lanes end with the same bits.  Call with every lane active.
+template <int CTRL>
+STE_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+STE_DEV float xrow32_sum(float v) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, v);
+  auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  const float y = __builtin_bit_cast(float, (uint32_t)p[0]) + __builtin_bit_cast(float, (uint32_t)p[1]);
+  const uint32_t w = __builtin_bit_cast(uint32_t, y);
+  auto q = __builtin_amdgcn_permlane16_swap(w, w, false, false);
+  return __builtin_bit_cast(float, (uint32_t)q[0]) + __builtin_bit_cast(float, (uint32_t)q[1]);
+}
 STE_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]: lane ^ 1
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]: lane ^ 2
+  v += dpp_f<0x141>(v);   // row_half_mirror: the other quad of the 8-lane half
+  v += dpp_f<0x140>(v);   // row_mirror: the other half of the 16-lane row
+  return xrow32_sum(v);
 }
 STE_DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  const uint32_t u = __builtin_bit_cast(uint32_t, v);
+  auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  const float y = fmaxf(__builtin_bit_cast(float, (uint32_t)p[0]), __builtin_bit_cast(float, (uint32_t)p[1]));
+  const uint32_t w = __builtin_bit_cast(uint32_t, y);
+  auto q = __builtin_amdgcn_permlane16_swap(w, w, false, false);
+  return fmaxf(__builtin_bit_cast(float, (uint32_t)q[0]), __builtin_bit_cast(float, (uint32_t)q[1]));
 }
 STE_DEV double wave_sum_d(double v) {
 #pragma unroll

@@ -1462,33 +1462,32 @@ int launch_8ph(const ste_gemm_args& a, hipStream_t s) {
   return 0;
 }
 
-// C = beta*C + alpha*sum_s ws[s]  (fp32 [M,N] slabs, 4 columns per thread)
+// C = beta*C + alpha*sum_s ws[s]  (fp32 [M,N] slabs): one thread per 4 columns over the whole
+// output, its MAXS slab loads (clamped to the last slab past S) issued together with C's, then
+// summed in slab order (run-to-run identical); S > MAXS (MAXS = 16) continues in a loop.
+template <int MAXS>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ C, int64_t ldc,
                                                             const float* __restrict__ ws, int M, int N, int S,
                                                             float alpha, float beta) {
   const int n4 = N >> 2;
-  const int64_t total = (int64_t)M * n4;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)M * n4) return;
   const int64_t slab = (int64_t)M * N;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int m = (int)(i / n4), c = (int)(i - (int64_t)m * n4) * 4;
-    const float* w = ws + (int64_t)m * N + c;
-    float* cp = C + (int64_t)m * ldc + c;
-    const f32x4 cv = beta != 0.f ? *reinterpret_cast<const f32x4*>(cp) : f32x4{0.f, 0.f, 0.f, 0.f};
-    // up to 8 slab loads in flight, summed in slab order (run-to-run identical)
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < S; k0 += 8) {
-      f32x4 v[8];
+  const int m = (int)(i / n4), c = (int)(i - (int64_t)m * n4) * 4;
+  const float* w = ws + (int64_t)m * N + c;
+  float* cp = C + (int64_t)m * ldc + c;
+  f32x4 v[MAXS];
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        v[k] = k0 + k < S ? *reinterpret_cast<const f32x4*>(w + (k0 + k) * slab) : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < MAXS; ++k) v[k] = *reinterpret_cast<const f32x4*>(w + (k < S ? k : S - 1) * slab);
+  const f32x4 cv = beta != 0.f ? *reinterpret_cast<const f32x4*>(cp) : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 acc = v[0];
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (k0 + k < S) acc = k0 + k == 0 ? v[k] : acc + v[k];
-    }
-    f32x4 out = acc * alpha;
-    if (beta != 0.f) out += cv * beta;
-    *reinterpret_cast<f32x4*>(cp) = out;
-  }
+  for (int k = 1; k < MAXS; ++k)
+    if (k < S) acc += v[k];
+  for (int k = MAXS; k < S; ++k) acc += *reinterpret_cast<const f32x4*>(w + k * slab);
+  f32x4 out = acc * alpha;
+  if (beta != 0.f) out += cv * beta;
+  *reinterpret_cast<f32x4*>(cp) = out;
 }
 
 // Few-tile split-K: C = epilogue(sum_s ws[s]) for the forward / input-gradient GEMMs whose
@@ -1701,9 +1700,16 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
       g.alpha = 1.f; g.beta = 0.f;
       if (int e = launch_8ph<false, false>(g, s)) return e;
       const int64_t work = (int64_t)a.M * (a.N / 4);
-      const int blocks = (int)((work + 255) / 256 < 2048 ? (work + 255) / 256 : 2048);
-      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, (float*)a.C, a.ldc, a.ws, a.M, a.N,
-                         pl.S, a.alpha, a.beta);
+      const dim3 rgrid((unsigned)((work + 255) / 256));
+      if (pl.S <= 4)
+        hipLaunchKernelGGL(splitk_reduce_kernel<4>, rgrid, dim3(256), 0, s, (float*)a.C, a.ldc, a.ws, a.M, a.N, pl.S,
+                           a.alpha, a.beta);
+      else if (pl.S <= 8)
+        hipLaunchKernelGGL(splitk_reduce_kernel<8>, rgrid, dim3(256), 0, s, (float*)a.C, a.ldc, a.ws, a.M, a.N, pl.S,
+                           a.alpha, a.beta);
+      else
+        hipLaunchKernelGGL(splitk_reduce_kernel<16>, rgrid, dim3(256), 0, s, (float*)a.C, a.ldc, a.ws, a.M, a.N, pl.S,
+                           a.alpha, a.beta);
       STE_CHECK_LAUNCH();
       const int64_t kdone = (int64_t)nk_all * 64;
       if (kdone < a.K) {  // the ragged K % 64 tail: accumulate on the small kernel

@@ -86,9 +86,9 @@ STE_DEV void ln_fwd_row(const ste_ln_fwd_args& a, const LnParams<MAXC>& pr, int 
     else if (a.yb) store_bf16x4((bf16*)a.yb + (int64_t)row * a.ldyb + col, y);
     if (a.q8) {  // MX-fp8 copy: 8 lanes x 4 columns = one 32-column block
       float am = fmaxf(fmaxf(fabsf(y[0]), fabsf(y[1])), fmaxf(fabsf(y[2]), fabsf(y[3])));
-      am = fmaxf(am, __shfl_xor(am, 1));
-      am = fmaxf(am, __shfl_xor(am, 2));
-      am = fmaxf(am, __shfl_xor(am, 4));
+      am = fmaxf(am, dpp_f<0xB1>(am));    // lane ^ 1
+      am = fmaxf(am, dpp_f<0x4E>(am));    // lane ^ 2
+      am = fmaxf(am, dpp_f<0x141>(am));   // the other quad of the 8 lanes
       const int ex = mx8_exp(am);
       const float inv = ldexpf(1.0f, -ex);
       uint32_t w = 0;
