@@ -1123,77 +1123,60 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
       const bool all_lo = (kb + TK - 1) - q0g <= -left;
       const bool all_hi = kb - (q0g + 15) >= right;
       const bool band = !(all_lo || all_hi || (STE_ABLATE & 512));
-      // raise the running max only when a row grew past m + THRESH (deferred rescale)
-      auto rescale = [&](float tmax) {
-        if (__builtin_amdgcn_ballot_w64(tmax > m[gq] + THRESH) != 0ull) {
-          const float mnew = fmaxf(m[gq], tmax);
-          const float alpha = __builtin_amdgcn_exp2f(m[gq] - mnew);
-          if (SPLIT) lp[gq] *= alpha;
-          else lsum[gq] *= alpha;
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
-          m[gq] = mnew;
-        }
-      };
-      // row max as a depth-3 tree (a sequential max3 chain serialises 8 dependent VALU ops)
-      auto tile_max = [&]() {
-        const float t0 = max3f(s[gq][0][0], s[gq][0][1], s[gq][0][2]);
-        const float t1 = max3f(s[gq][0][3], s[gq][1][0], s[gq][1][1]);
-        const float t2 = max3f(s[gq][1][2], s[gq][1][3], s[gq][2][0]);
-        const float t3 = max3f(s[gq][2][1], s[gq][2][2], s[gq][2][3]);
-        const float t4 = max3f(s[gq][3][0], s[gq][3][1], s[gq][3][2]);
-        const float u0 = max3f(t0, t1, t2), u1 = max3f(t3, t4, s[gq][3][3]);
-        return max3f(u0, u1, u1);
-      };
-      if (!band && !MASKED) {
-        // outside the distance band every key of the tile has the same bias bc: the max runs on the
-        // raw scores (c2 > 0), and p = exp2(s*c2 + (bc - m)) is one fma + exp per score
+      if (!band) {
         const float bc = all_lo ? blo[gq] : bhi[gq];
-        rescale(rowmax4(__builtin_fmaf(tile_max(), c2, bc)));
-        const float cb = bc - m[gq];
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[gq][t][r], c2, cb));
+          for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_fmaf(s[gq][t][r], c2, bc);
       } else {
-        if (!band) {
-          const float bc = all_lo ? blo[gq] : bhi[gq];
+        const float* qrow = reinterpret_cast<const float*>(sm + qe_off) + (w * WQ + 16 * gq + li) * QS + PADL;
+        const int d0 = kb + 4 * g - myq + left;
 #pragma unroll
-          for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t) {
+          const float* qp = qrow + med3i(d0 + 16 * t, -PADL, nrel);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_fmaf(s[gq][t][r], c2, bc);
-        } else {
-          const float* qrow = reinterpret_cast<const float*>(sm + qe_off) + (w * WQ + 16 * gq + li) * QS + PADL;
-          const int d0 = kb + 4 * g - myq + left;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const float* qp = qrow + med3i(d0 + 16 * t, -PADL, nrel);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_fmaf(s[gq][t][r], c2, qp[r]);
-          }
+          for (int r = 0; r < 4; ++r) s[gq][t][r] = __builtin_fmaf(s[gq][t][r], c2, qp[r]);
         }
-        if constexpr (MASKED) {   // key kb+16t+4g+r: past T -> -inf, masked -> finfo.min (as rel2)
-          const uint64_t okb = okw_of(kt);
-          const uint32_t wlo = (uint32_t)(okb >> (4 * g)), whi = (uint32_t)(okb >> (32 + 4 * g));
-          const int lim = T - kb - 4 * g;
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const uint32_t wd = t < 2 ? wlo : whi;
-              const bool ok = (wd >> (16 * (t & 1) + r)) & 1u;
-              const float fill = 16 * t + r < lim ? NEG_MASK : -INFINITY;
-              s[gq][t][r] = ok ? s[gq][t][r] : fill;
-            }
-        }
-        rescale(rowmax4(tile_max()));
-        const float mg = m[gq];
+      }
+      if constexpr (MASKED) {   // key kb+16t+4g+r: past T -> -inf, masked -> finfo.min (as rel2)
+        const uint64_t okb = okw_of(kt);
+        const uint32_t wlo = (uint32_t)(okb >> (4 * g)), whi = (uint32_t)(okb >> (32 + 4 * g));
+        const int lim = T - kb - 4 * g;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            s[gq][t][r] = (STE_ABLATE & 128) ? s[gq][t][r] - mg : __builtin_amdgcn_exp2f(s[gq][t][r] - mg);
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t wd = t < 2 ? wlo : whi;
+            const bool ok = (wd >> (16 * (t & 1) + r)) & 1u;
+            const float fill = 16 * t + r < lim ? NEG_MASK : -INFINITY;
+            s[gq][t][r] = ok ? s[gq][t][r] : fill;
+          }
       }
+      // row max as a depth-3 tree (a sequential max3 chain serialises 8 dependent VALU ops)
+      const float t0 = max3f(s[gq][0][0], s[gq][0][1], s[gq][0][2]);
+      const float t1 = max3f(s[gq][0][3], s[gq][1][0], s[gq][1][1]);
+      const float t2 = max3f(s[gq][1][2], s[gq][1][3], s[gq][2][0]);
+      const float t3 = max3f(s[gq][2][1], s[gq][2][2], s[gq][2][3]);
+      const float t4 = max3f(s[gq][3][0], s[gq][3][1], s[gq][3][2]);
+      const float u0 = max3f(t0, t1, t2), u1 = max3f(t3, t4, s[gq][3][3]);
+      const float tmax = rowmax4(max3f(u0, u1, u1));
+      // deferred rescale: raise the running max only when a row grew past m + THRESH
+      if (__builtin_amdgcn_ballot_w64(tmax > m[gq] + THRESH) != 0ull) {
+        const float mnew = fmaxf(m[gq], tmax);
+        const float alpha = __builtin_amdgcn_exp2f(m[gq] - mnew);
+        if (SPLIT) lp[gq] *= alpha;
+        else lsum[gq] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
+        m[gq] = mnew;
+      }
+      const float mg = m[gq];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          s[gq][t][r] = (STE_ABLATE & 128) ? s[gq][t][r] - mg : __builtin_amdgcn_exp2f(s[gq][t][r] - mg);
       if (SPLIT) {   // the row sum of p itself (hi + lo P sums to p within 2^-16): fp32 adds, not 2 MFMAs per u
         f32x4 t01 = (s[gq][0] + s[gq][1]) + (s[gq][2] + s[gq][3]);
         lp[gq] += (t01[0] + t01[1]) + (t01[2] + t01[3]);
