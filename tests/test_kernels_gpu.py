@@ -87,6 +87,7 @@ def test_dx_through_cached_transpose():
                                          (1024, 1024, 31936, 80),   # c2 O-proj dW: S=16, Kc=31, 3 leftover K-tiles
                                          (1024, 1024, 15968, 80),   # c3 (b=32) O-proj dW: S=16, ragged 32-row tail
                                          (3072, 768, 8192, 80),     # text QKV dW over 2bL rows
+                                         (768, 768, 31936, 80),     # 9 tiles: S=28 > 16, the reduce's loop tail
                                          (1032, 520, 4160, 8),      # ragged M/N tiles; workspace caps S at 3
                                          (2048, 1024, 960, 80)])    # K < 16 tiles: no split
 def test_gemm_dw_splitk(ops, M, N, K, ws_mb):
