@@ -88,8 +88,8 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // low halves of the same accumulator pair: (bf16)(x - hi) for the hi/lo split of P
 STE_DEV bf16x8 pack_acc_lo(f32x4 a, f32x4 b, bf16x8 hi) {
-  // hi back to fp32 straight from the packed words (low half << 16, high half masked), one
-  // v_pk_add_f32 per pair
+  // hi back to fp32 straight from the packed words (low half << 16, high half masked), then one
+  // subtraction per value (the library is built without packed fp32: _build.py)
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const u32x4 hu = __builtin_bit_cast(u32x4, hi);
   const f32x4 x[2] = {a, b};
@@ -806,7 +806,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
       const int q0g = qw + 16 * gq, myq = q0g + li;
       const bool all_lo = (kb + TK - 1) - q0g <= -left;
       const bool all_hi = kb - (q0g + 15) >= right;
-      // packed fp32 (v_pk_fma_f32) on the accumulator register pairs
+      // two-wide fma on the accumulator register pairs (single-issue: no packed fp32, _build.py)
       const f32x2 c22 = {c2, c2};
       if (all_lo || all_hi) {
         const float bc = all_lo ? blo[gq] : bhi[gq];
