@@ -232,12 +232,14 @@ def cpu_baseline(args):
     return out
 
 
-def hbm_traffic(kernel):
-    """Per-launch HBM bytes of `kernel` from the latest committed PMC reduction
-    (profiles/rNN_hbm_traffic.json, made by profiles/profile_bench.sh: separate rocprofv3
-    FETCH_SIZE / WRITE_SIZE passes of this bench; gfx950 FETCH_SIZE x2 correction applied)."""
+def hbm_traffic(kernel, c5=False):
+    """Per-launch HBM bytes of `kernel` from the latest committed PMC reduction of the same
+    workload family (profiles/rNN*_hbm_traffic.json, made by profiles/profile_bench.sh: separate
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench; gfx950 FETCH_SIZE x2 correction
+    applied).  c5: the config-5 files (tag containing "c5"); otherwise the others."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json")))
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json"))
+                   if ("c5" in os.path.basename(f)) == c5)
     if not files:
         return None, None
     # rocprofv3 names the 8-phase GEMM with its MX template argument (", false>"); the library's
@@ -427,7 +429,7 @@ def main(argv=None):
     else:
         cname = "custom"
     peak = FP8_PEAK_TFLOPS if dom == "gemm_mx8_kernel" else BF16_PEAK_TFLOPS
-    traffic, traffic_src = hbm_traffic(dom)
+    traffic, traffic_src = hbm_traffic(dom, c5=c5)
     out = {
         "metric": ("evaluated audio–text pairs/sec, forward only (whole node), 10s@16kHz + 64-tok" if args.eval else
                    "audio–text pairs/sec (whole node), 10s@16kHz + 64-tok, 1/2/4/8 MI355X"),
