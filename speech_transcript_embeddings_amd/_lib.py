@@ -116,6 +116,7 @@ _SIGS = {
     "ste_gemm_f32": (c_int, [C.POINTER(GemmArgs), c_void_p]),
     "ste_gemm_kernel": (c_int, [C.POINTER(GemmArgs)]),
     "ste_gemm_colsum_ws_floats": (c_int64, [C.POINTER(GemmArgs)]),
+    "ste_gemm_tile_map": (c_int, [c_int, c_int, c_int, C.POINTER(c_int), C.POINTER(c_int)]),
     "ste_gemm_kernel_name": (c_int, [C.POINTER(GemmArgs), c_char_p, c_int]),
     "ste_rows_extract": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                  c_void_p, c_void_p]),

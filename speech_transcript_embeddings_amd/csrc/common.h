@@ -19,6 +19,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define STE_WAVE 64
 #define STE_DEV __device__ __forceinline__
+#define STE_HD __host__ __device__ __forceinline__
 
 // ---------------------------------------------------------------- conversions
 STE_DEV float bf2f(bf16 x) { return (float)x; }

@@ -574,17 +574,45 @@ STE_DEV void epilogue_bf16s(const ste_gemm_args& p, const f32x4 (&acc)[8][4], ch
   }
 }
 
-// block id -> (batch, tile_m, tile_n): bijective XCD remap, then groups of 8 m-tiles
+// tile id (after the XCD remap, which hands each XCD's CUs 32 consecutive ids at a time) ->
+// (tile_m, tile_n).  Outputs >= 8 tiles wide: groups of 4 m-tiles walked in 8-wide n-blocks, so an
+// XCD's 32 concurrent tiles are 4 A row panels x 8 W column panels (the round-3 order gave 8 x 4 only
+// at num_n = 4 and read A panels 7-9x per launch at N = 4,096, profiles/r4c2_hbm_traffic.json).
+// Narrower outputs: groups of 8 m-tiles, n-major within the group.  STE_RASTER_R3: the round-3
+// order for every shape (A/B builds).  Bijective on [0, num_m * num_n).
+STE_HD void tile_of(int t, int num_m, int num_n, int& tm, int& tn) {
+#ifndef STE_RASTER_R3
+  if (num_n >= 8) {
+    constexpr int GM = 4, GN = 8;
+    const int gsz = GM * num_n;
+    const int group = t / gsz, first_m = group * GM;
+    const int gm = num_m - first_m < GM ? num_m - first_m : GM;
+    const int j = t - group * gsz;
+    const int nfull = num_n / GN, full = nfull * gm * GN;
+    if (j < full) {
+      const int nb = j / (gm * GN), r = j - nb * (gm * GN);
+      tm = first_m + r % gm;
+      tn = nb * GN + r / gm;
+    } else {
+      const int r = j - full;
+      tm = first_m + r % gm;
+      tn = nfull * GN + r / gm;
+    }
+    return;
+  }
+#endif
+  constexpr int GROUP = 8;
+  const int group = t / (GROUP * num_n);
+  const int first_m = group * GROUP;
+  const int gsize = num_m - first_m < GROUP ? num_m - first_m : GROUP;
+  tm = first_m + (t % (GROUP * num_n)) % gsize;
+  tn = (t % (GROUP * num_n)) / gsize;
+}
+// block id -> (batch, tile_m, tile_n)
 STE_DEV void map_tile_bid(int bid, int num_m, int num_n, int& batch, int& tm, int& tn) {
   const int tiles = num_m * num_n;
   batch = bid / tiles;
-  int t = bid - batch * tiles;
-  constexpr int GROUP = 8;
-  int group = t / (GROUP * num_n);
-  int first_m = group * GROUP;
-  int gsize = min(num_m - first_m, GROUP);
-  tm = first_m + (t % (GROUP * num_n)) % gsize;
-  tn = (t % (GROUP * num_n)) / gsize;
+  tile_of(bid - batch * tiles, num_m, num_n, tm, tn);
 }
 STE_DEV void map_tile(int nwg, int num_m, int num_n, int& batch, int& tm, int& tn) {
   map_tile_bid(xcd_remap(blockIdx.x, nwg), num_m, num_n, batch, tm, tn);
@@ -1784,6 +1812,12 @@ extern "C" int ste_gemm(const ste_gemm_args* args, void* stream) {
   }
   if (e == 0 && cs_rows) e = ste_rowsum_ordered(a.ws, cs_rows, a.N, a.batch, a.colsum, stream);
   return e;
+}
+
+extern "C" int ste_gemm_tile_map(int t, int num_m, int num_n, int* tm, int* tn) {
+  if (!tm || !tn || num_m <= 0 || num_n <= 0 || t < 0 || t >= num_m * num_n) return STE_ERR_ARG;
+  tile_of(t, num_m, num_n, *tm, *tn);
+  return 0;
 }
 
 extern "C" int64_t ste_gemm_colsum_ws_floats(const ste_gemm_args* args) {
