@@ -98,8 +98,8 @@ int ste_gemm(const ste_gemm_args* args, void* stream);
  * bound over ste_gemm and ste_gemm_f32's tile shapes. */
 int64_t ste_gemm_colsum_ws_floats(const ste_gemm_args* args);
 /* Host-only (never touches the GPU): the output tile (tm, tn) that the GEMM kernels give tile id
- * t (after their XCD remap) of a num_m x num_n tile grid — the L2-aware raster (4 m-tiles x 8-wide
- * n-blocks for outputs >= 8 tiles wide, groups of 8 m-tiles otherwise).  For tests of the order. */
+ * t (after their XCD remap) of a num_m x num_n tile grid — groups of 8 m-tiles, m fastest within a
+ * group.  For tests of the order. */
 int ste_gemm_tile_map(int t, int num_m, int num_n, int* tm, int* tn);
 
 /* The same contract with fp32 A, B (and fp32 C2 / Z) on the exact-f32 matrix core

@@ -575,32 +575,11 @@ STE_DEV void epilogue_bf16s(const ste_gemm_args& p, const f32x4 (&acc)[8][4], ch
 }
 
 // tile id (after the XCD remap, which hands each XCD's CUs 32 consecutive ids at a time) ->
-// (tile_m, tile_n).  Outputs >= 8 tiles wide: groups of 4 m-tiles walked in 8-wide n-blocks, so an
-// XCD's 32 concurrent tiles are 4 A row panels x 8 W column panels (the round-3 order gave 8 x 4 only
-// at num_n = 4 and read A panels 7-9x per launch at N = 4,096, profiles/r4c2_hbm_traffic.json).
-// Narrower outputs: groups of 8 m-tiles, n-major within the group.  STE_RASTER_R3: the round-3
-// order for every shape (A/B builds).  Bijective on [0, num_m * num_n).
+// (tile_m, tile_n): groups of 8 m-tiles, m fastest within the group, so the 32 concurrent tiles
+// of an XCD at N = 1,024 (4 tiles wide) are 8 A row panels x 4 W column panels.  (Round 4 tried
+// 4 m-tiles x 8-wide n-blocks for outputs >= 8 tiles wide, fewer A panels per XCD wave: the
+// N = 4,096 GEMMs ran 3-8 % slower, profiles/r4n_raster_ab.txt.)  Bijective on [0, num_m * num_n).
 STE_HD void tile_of(int t, int num_m, int num_n, int& tm, int& tn) {
-#ifndef STE_RASTER_R3
-  if (num_n >= 8) {
-    constexpr int GM = 4, GN = 8;
-    const int gsz = GM * num_n;
-    const int group = t / gsz, first_m = group * GM;
-    const int gm = num_m - first_m < GM ? num_m - first_m : GM;
-    const int j = t - group * gsz;
-    const int nfull = num_n / GN, full = nfull * gm * GN;
-    if (j < full) {
-      const int nb = j / (gm * GN), r = j - nb * (gm * GN);
-      tm = first_m + r % gm;
-      tn = nb * GN + r / gm;
-    } else {
-      const int r = j - full;
-      tm = first_m + r % gm;
-      tn = nfull * GN + r / gm;
-    }
-    return;
-  }
-#endif
   constexpr int GROUP = 8;
   const int group = t / (GROUP * num_n);
   const int first_m = group * GROUP;

@@ -69,8 +69,8 @@ def test_gemm_kernel_selection(lib):
 @pytest.mark.parametrize("num_m,num_n", [(125, 16), (125, 12), (125, 4), (32, 9), (1, 16), (7, 8), (3, 3), (125, 8)])
 def test_gemm_tile_raster(lib, num_m, num_n):
     """The GEMM kernels' tile order (ste_gemm_tile_map, the same function the device code calls) is
-    a bijection onto the tile grid, and for outputs >= 8 tiles wide every aligned run of 32 ids (one
-    XCD's CUs at a time) covers at most 4 A row panels and 8 W column panels."""
+    a bijection onto the tile grid that walks groups of 8 m-tiles, m fastest: 32 consecutive ids
+    (one XCD's CUs at a time) at N = 1,024 (4 tiles wide) are 8 A row panels x 4 W column panels."""
     f = lib.fn("ste_gemm_tile_map")
     tm, tn = C.c_int(), C.c_int()
     seen = []
@@ -80,13 +80,14 @@ def test_gemm_tile_raster(lib, num_m, num_n):
         seen.append((tm.value, tn.value))
     assert len(set(seen)) == num_m * num_n
     assert f(num_m * num_n, num_m, num_n, C.byref(tm), C.byref(tn)) != 0
-    if num_n >= 8:
-        gsz = 4 * num_n
-        for g0 in range(0, len(seen), gsz):   # whole 4-row groups: 32-id runs stay inside one group
-            grp = seen[g0:g0 + gsz]
-            for w0 in range(0, len(grp) - 31, 32):
-                w = grp[w0:w0 + 32]
-                assert len({m for m, _ in w}) <= 4 and len({n for _, n in w}) <= 8, (g0, w0)
+    for t, (m, n) in enumerate(seen):
+        g0 = (t // (8 * num_n)) * 8
+        gsize = min(8, num_m - g0)
+        j = t % (8 * num_n)
+        assert (m, n) == (g0 + j % gsize, j // gsize)
+    if num_n == 4 and num_m >= 8:
+        w = seen[:32]
+        assert len({m for m, _ in w}) == 8 and len({n for _, n in w}) == 4
 
 
 def test_gemm_split_policies(lib):
