@@ -579,8 +579,11 @@ STE_DEV void epilogue_bf16s(const ste_gemm_args& p, const f32x4 (&acc)[8][4], ch
 // of an XCD at N = 1,024 (4 tiles wide) are 8 A row panels x 4 W column panels.  (Round 4 tried
 // 4 m-tiles x 8-wide n-blocks for outputs >= 8 tiles wide, fewer A panels per XCD wave: the
 // N = 4,096 GEMMs ran 3-8 % slower, profiles/r4n_raster_ab.txt.)  Bijective on [0, num_m * num_n).
+#ifndef STE_TILE_GROUP
+#define STE_TILE_GROUP 8   // A/B builds: -DSTE_TILE_GROUP=16
+#endif
 STE_HD void tile_of(int t, int num_m, int num_n, int& tm, int& tn) {
-  constexpr int GROUP = 8;
+  constexpr int GROUP = STE_TILE_GROUP;
   const int group = t / (GROUP * num_n);
   const int first_m = group * GROUP;
   const int gsize = num_m - first_m < GROUP ? num_m - first_m : GROUP;
