@@ -121,23 +121,51 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(ste_ln_fwd_args a) {
 // Two chained LayerNorms over the same rows, y2 = LN_b(LN_a(x)) (a Conformer layer's final LN
 // and the next layer's FFN1 LN): LN_a's output stays in registers for LN_b, saving LN_b's read
 // of it and a launch.  b.x is not read.
-template <int MAXC>
+// LEAN (A/B, STE_LN_FWD_PAIR=lean): no next-row prefetch and both LayerNorms' gamma / beta re-read
+// per row (L1-resident) instead of held in registers: fewer VGPRs, more waves per SIMD.
+template <int MAXC, bool LEAN = false>
 __global__ __launch_bounds__(NT) void ln_fwd_pair_kernel(ste_ln_fwd_args a, ste_ln_fwd_args b) {
   const int lane = threadIdx.x & 63;
   const int wave = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * (NT / 64);
-  LnParams<MAXC> pa, pb;
-  pa.load(a.gamma, a.beta, a.cols, lane);
-  pb.load(b.gamma, b.beta, b.cols, lane);
-  float v[MAXC * 4], nx[MAXC * 4];
-  if (wave < a.rows) load_row<MAXC>(a.x, a.x_bf16, a.ldx, wave, a.cols, lane, v);
-  for (int row = wave; row < a.rows; row += nwaves) {
-    if (row + nwaves < a.rows) load_row<MAXC>(a.x, a.x_bf16, a.ldx, row + nwaves, a.cols, lane, nx);
-    ln_fwd_row<MAXC>(a, pa, row, lane, v);
-    ln_fwd_row<MAXC>(b, pb, row, lane, v);
+  if constexpr (LEAN) {
+    for (int row = wave; row < a.rows; row += nwaves) {
+      float v[MAXC * 4];
+      load_row<MAXC>(a.x, a.x_bf16, a.ldx, row, a.cols, lane, v);
+      const float *ga = a.gamma, *ba = a.beta, *gb = b.gamma, *bb = b.beta;
+      asm volatile("" : "+s"(ga), "+s"(ba), "+s"(gb), "+s"(bb));   // parameter loads stay in the loop
+      {
+        LnParams<MAXC> pa;
+        pa.load(ga, ba, a.cols, lane);
+        ln_fwd_row<MAXC>(a, pa, row, lane, v);
+      }
+      LnParams<MAXC> pb;
+      pb.load(gb, bb, b.cols, lane);
+      ln_fwd_row<MAXC>(b, pb, row, lane, v);
+    }
+  } else {
+    LnParams<MAXC> pa;
+    pa.load(a.gamma, a.beta, a.cols, lane);
+    LnParams<MAXC> pb;
+    pb.load(b.gamma, b.beta, b.cols, lane);
+    float v[MAXC * 4], nx[MAXC * 4];
+    if (wave < a.rows) load_row<MAXC>(a.x, a.x_bf16, a.ldx, wave, a.cols, lane, v);
+    for (int row = wave; row < a.rows; row += nwaves) {
+      if (row + nwaves < a.rows) load_row<MAXC>(a.x, a.x_bf16, a.ldx, row + nwaves, a.cols, lane, nx);
+      ln_fwd_row<MAXC>(a, pa, row, lane, v);
+      ln_fwd_row<MAXC>(b, pb, row, lane, v);
 #pragma unroll
-    for (int i = 0; i < MAXC * 4; ++i) v[i] = nx[i];
+      for (int i = 0; i < MAXC * 4; ++i) v[i] = nx[i];
+    }
   }
+}
+bool ln_fwd_pair_lean() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("STE_LN_FWD_PAIR");
+    v = (e && e[0] == 'l') ? 1 : 0;
+  }
+  return v == 1;
 }
 
 // Column-sum accumulators of one backward (gamma, beta, and the dxb copy's column sums).
@@ -394,6 +422,7 @@ extern "C" int ste_layernorm_fwd_pair(const ste_ln_fwd_args* a, const ste_ln_fwd
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(grid_for(a->rows));
   if (a->cols <= 256) hipLaunchKernelGGL(ln_fwd_pair_kernel<1>, grid, dim3(NT), 0, s, *a, *b);
+  else if (ln_fwd_pair_lean()) hipLaunchKernelGGL((ln_fwd_pair_kernel<4, true>), grid, dim3(NT), 0, s, *a, *b);
   else hipLaunchKernelGGL(ln_fwd_pair_kernel<4>, grid, dim3(NT), 0, s, *a, *b);
   STE_CHECK_LAUNCH();
   return 0;
