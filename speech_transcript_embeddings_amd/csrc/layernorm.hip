@@ -121,8 +121,10 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(ste_ln_fwd_args a) {
 // Two chained LayerNorms over the same rows, y2 = LN_b(LN_a(x)) (a Conformer layer's final LN
 // and the next layer's FFN1 LN): LN_a's output stays in registers for LN_b, saving LN_b's read
 // of it and a launch.  b.x is not read.
-// LEAN (A/B, STE_LN_FWD_PAIR=lean): no next-row prefetch and both LayerNorms' gamma / beta re-read
-// per row (L1-resident) instead of held in registers: fewer VGPRs, more waves per SIMD.
+// LEAN (default): no next-row prefetch and both LayerNorms' gamma / beta re-read per row
+// (L1-resident) instead of held in registers: 127 VGPRs and 4 waves per SIMD instead of 172 and 2;
+// 98.6 -> 85.8 us at c2 rows in isolation, +0.3 % c2 step (profiles/r4p_ln_pair_ab.txt).
+// STE_LN_FWD_PAIR=prefetch: the round-3 form (A/B).
 template <int MAXC, bool LEAN = false>
 __global__ __launch_bounds__(NT) void ln_fwd_pair_kernel(ste_ln_fwd_args a, ste_ln_fwd_args b) {
   const int lane = threadIdx.x & 63;
@@ -163,7 +165,7 @@ bool ln_fwd_pair_lean() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("STE_LN_FWD_PAIR");
-    v = (e && e[0] == 'l') ? 1 : 0;
+    v = (e && e[0] == 'p') ? 0 : 1;
   }
   return v == 1;
 }
