@@ -79,5 +79,19 @@ def layernorm():
     print(f"ln bwd pair + column sums (both LNs): {us:.1f} us", flush=True)
 
 
+def fbank():
+    """c2 batch: 64 clips of 10 s at 16 kHz -> [64, 499, 160] features (three launches)."""
+    B, N = 64, 160000
+    wav = torch.randn(B, N, device="cuda") * 0.1
+    lens = torch.full((B,), N, device="cuda", dtype=torch.int32)
+    T = ((1 + (N - 400) // 160) + 1) // 2
+    feats = torch.empty(B, T, 160, device="cuda")
+    mask = torch.empty(B, T, device="cuda", dtype=torch.int64)
+    work = torch.empty(B * 2 * T * 80 + B * 160, device="cuda")
+    us = timeit(lambda: ops.fbank(wav, lens, T, feats=feats, mask=mask, work=work))
+    nbytes = 4 * B * N + feats.numel() * 4 + mask.numel() * 8
+    print(f"fbank (3 launches): {us:.1f} us, {nbytes / us / 1e3:.0f} GB/s algorithmic", flush=True)
+
+
 if __name__ == "__main__":
     globals()[sys.argv[1]]()

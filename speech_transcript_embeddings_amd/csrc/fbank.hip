@@ -25,6 +25,7 @@ namespace {
 
 constexpr int FRAME = 400, HOP = 160, NFFT = 512, NBIN = 257, NMEL = 80;
 constexpr int MAXNZ = 640;  // non-zero filter taps (501 for these parameters)
+constexpr int MAXTAP = 16;  // taps of the widest filter (gen_fbank_tables.py asserts it)
 
 // Constant tables, compile-time data (fbank_tables.h, made by gen_fbank_tables.py from the
 // extractor's float64 formulas, rounded to float32 once), read by every frame block:
@@ -122,8 +123,11 @@ __global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restri
     const int n = lane + 64 * i;
     float val = 0.f;
     if (i < 7) {
-      const float up = __shfl(c[i], (lane + 63) & 63, 64);
-      const float wrap = i > 0 ? __shfl(c[i - 1], 63, 64) : 0.f;
+      // lane - 1's value by DPP wave_shr:1 and lane 63's by v_readlane (no ds_bpermute round trips)
+      const float up = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, c[i]), 0x138,
+                                                                               0xF, 0xF, false));
+      const float wrap = i > 0 ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, c[i - 1]), 63))
+                               : 0.f;
       const float prev = lane > 0 ? up : wrap;
       if (n < FRAME) {
         val = (n == 0) ? c[i] * (1.0f - 0.97f) : c[i] - 0.97f * prev;
