@@ -25,7 +25,6 @@ namespace {
 
 constexpr int FRAME = 400, HOP = 160, NFFT = 512, NBIN = 257, NMEL = 80;
 constexpr int MAXNZ = 640;  // non-zero filter taps (501 for these parameters)
-constexpr int MAXTAP = 16;  // taps of the widest filter (gen_fbank_tables.py asserts it)
 
 // Constant tables, compile-time data (fbank_tables.h, made by gen_fbank_tables.py from the
 // extractor's float64 formulas, rounded to float32 once), read by every frame block:
