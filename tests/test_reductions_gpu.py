@@ -87,7 +87,8 @@ def test_sumsq(ops, busy):
         return [acc]
     acc = _twice(fn, busy)[0]
     ref = (g.double() ** 2).sum()
-    assert abs(float(acc[0]) - float(ref)) / float(ref) < 1e-12
+    # fp32 squares (2^-24 relative each) summed in fp64: measured 9e-11
+    assert abs(float(acc[0]) - float(ref)) / float(ref) < 1e-7
 
 
 def test_text_embedding_rows(ops, busy):
