@@ -241,7 +241,7 @@ typedef struct {
   void* dk; int64_t lddk;
   void* dv; int64_t lddv;
   float* delta;       /* workspace [B*H*T] */
-  float* dE;          /* fp32 [left+right+1, 64], accumulated (may be NULL) */
+  float* dE;          /* fp32 [left+right+1, 64], accumulated in a fixed order (may be NULL) */
   float* gwork;       /* workspace [B*H*T*80] fp32, required when dE != NULL */
   /* optional low half of O (bf16, row stride ldolo): the forward (whose PV product runs on
    * P split into bf16 hi + lo halves, so O is ~fp32-accurate) writes bf16(O - bf16(O)), and
