@@ -975,7 +975,12 @@ STE_DEV s16x4 ds_read_tr16_off(uint32_t addr) {
   return r;
 }
 
-template <bool SPLIT>
+// SPLIT: o_lo is written (the fp32 O as bf16 hi + lo, for the backward's delta) and the row sums
+// are fp32 sums of the exact p.  PLO: the PV product also runs on the low half of P (hi + lo P
+// within 2^-16 of p); without it P is bf16 in PV as in the plain forward and O carries P's
+// rounding (about 2^-9 / sqrt(keys) relative) while o_lo still keeps O's fp32 value (A/B:
+// STE_ATTN_PLO=0).
+template <bool SPLIT, bool PLO = SPLIT>
 __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
   using namespace rel4;
   extern __shared__ __attribute__((aligned(16))) char sm[];
@@ -1189,9 +1194,11 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pb, o[gq][dt]);
         if (SPLIT) {
-          const bf16x8 pl = pack_acc_lo(s[gq][2 * u], s[gq][2 * u + 1], pb);
+          if constexpr (PLO) {
+            const bf16x8 pl = pack_acc_lo(s[gq][2 * u], s[gq][2 * u + 1], pb);
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pl, o[gq][dt]);
+            for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pl, o[gq][dt]);
+          }
         } else {
           lsum[gq] = mfma16(ones, pb, lsum[gq]);   // row sum of the same (rounded) P, on the MFMA
         }
@@ -2388,6 +2395,16 @@ bool rel_fwd_v4() {
   return v == 1;
 }
 
+// STE_ATTN_PLO=0: the forward's PV product on bf16 P only (o_lo still written), see rel4
+bool rel_fwd_plo() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("STE_ATTN_PLO");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 // STE_ATTN_DQ=2: the v2 relative-key dQ kernel (A/B comparisons in one process)
 bool rel_dq_v3() {
   static int v = -1;
@@ -2445,7 +2462,8 @@ extern "C" int ste_attention_fwd(const ste_attn_args* a, void* stream) {
     // the hi/lo split of P only when a backward follows (o_lo given); a forward-only call (no_grad
     // evaluation) saves the second PV product
     if (rel_fwd_v4() && a->rel_left + a->rel_right + 1 <= rel4::max_nrel() && a->T <= rel4::MAXT * TK) {
-      if (a->o_lo) hipLaunchKernelGGL(attn_fwd_rel4_kernel<true>, g2, dim3(NT), rel4::FWD_LDS, s, *a);
+      if (a->o_lo && !rel_fwd_plo()) hipLaunchKernelGGL((attn_fwd_rel4_kernel<true, false>), g2, dim3(NT), rel4::FWD_LDS, s, *a);
+      else if (a->o_lo) hipLaunchKernelGGL(attn_fwd_rel4_kernel<true>, g2, dim3(NT), rel4::FWD_LDS, s, *a);
       else hipLaunchKernelGGL(attn_fwd_rel4_kernel<false>, g2, dim3(NT), rel4::FWD_LDS, s, *a);
     } else if (a->o_lo)
       hipLaunchKernelGGL(attn_fwd_rel2_kernel<true>, g2, dim3(NT), rel2::FWD_LDS, s, *a);
