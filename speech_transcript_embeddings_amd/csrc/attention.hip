@@ -975,13 +975,47 @@ STE_DEV s16x4 ds_read_tr16_off(uint32_t addr) {
   return r;
 }
 
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+STE_DEV f32x4 mfma16h(bf16x8 a, f16x8 b, f32x4 c) {   // a: fp16 bits carried in a bf16x8
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), b, c, 0, 0, 0);
+}
+STE_DEV f16x8 pack_acc_h(f32x4 a, f32x4 b) {   // as pack_acc, to fp16 (round to nearest even)
+  f16x8 v;
+  v[0] = (_Float16)a[0]; v[1] = (_Float16)a[1]; v[2] = (_Float16)a[2]; v[3] = (_Float16)a[3];
+  v[4] = (_Float16)b[0]; v[5] = (_Float16)b[1]; v[6] = (_Float16)b[2]; v[7] = (_Float16)b[3];
+  return v;
+}
+// the wave's two V pieces (16 bytes per lane each, see glds_tile_piece) bf16 -> fp16 in place; the
+// caller has waited for their DMA and waits for these LDS writes before the block barrier
+STE_DEV void v_tile_to_f16(char* vtile, int w, int lane) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp) {
+    u32x4* p = reinterpret_cast<u32x4*>(vtile + (2 * w + pp) * 1024 + lane * 16);
+    const u32x4 x = *p;
+    u32x4 y;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // bf16 -> f32 is exact; f32 -> f16 exact in range (round toward zero saturates at 65504)
+      const auto h = __builtin_amdgcn_cvt_pkrtz(__builtin_bit_cast(float, x[i] << 16),
+                                                __builtin_bit_cast(float, x[i] & 0xffff0000u));
+      y[i] = __builtin_bit_cast(unsigned, h);
+    }
+    *p = y;
+  }
+}
+
 // SPLIT: o_lo is written (the fp32 O as bf16 hi + lo, for the backward's delta) and the row sums
 // are fp32 sums of the exact p.  PLO: the PV product also runs on the low half of P (hi + lo P
 // within 2^-16 of p); without it P is bf16 in PV as in the plain forward and O carries P's
 // rounding (about 2^-9 / sqrt(keys) relative) while o_lo still keeps O's fp32 value (A/B:
 // STE_ATTN_PLO=0).
-template <bool SPLIT, bool PLO = SPLIT>
+// F16 (with SPLIT): the PV product in fp16 on P rounded to nearest fp16 (2^-11 relative, 8x finer
+// than bf16) and one MFMA per u, V converted bf16 -> fp16 in LDS once per tile (exact for
+// |v| < 65504, larger magnitudes saturate) by the wave that staged it (v_tile_to_f16).
+template <bool SPLIT, bool PLO = SPLIT, bool F16 = false>
 __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
+  static_assert(!F16 || (SPLIT && !PLO), "F16 replaces the hi/lo split of P");
   using namespace rel4;
   extern __shared__ __attribute__((aligned(16))) char sm[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
@@ -1035,6 +1069,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
   // entries 0..PADL-1 replicate bin 0 and PADL+nrel.. replicate bin nrel-1
   float* qe = reinterpret_cast<float*>(sm + QE_OFF) + w * WQ * QS;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's tile-0 and E pieces, Q
+  if constexpr (F16) v_tile_to_f16(sm + TILE, w, lane);
   __syncthreads();                                    // every wave's E pieces and validity words
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq)
@@ -1190,6 +1225,12 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
+        if constexpr (F16) {
+          const f16x8 ph = pack_acc_h(s[gq][2 * u], s[gq][2 * u + 1]);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16h(vf[dt][u], ph, o[gq][dt]);
+          continue;
+        }
         const bf16x8 pb = pack_acc(s[gq][2 * u], s[gq][2 * u + 1]);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pb, o[gq][dt]);
@@ -1206,6 +1247,10 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
     }
     if (kt + 1 < nkt) {
       if (!(STE_ABLATE & 32)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (this wave's pieces)
+      if constexpr (F16) {
+        v_tile_to_f16(sm + (slot ^ 1) * KV + TILE, w, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
       if (!(STE_ABLATE & 256)) __builtin_amdgcn_s_barrier();                     // ... every wave's, and tile kt fully read
       if (kt + 2 < nkt) issue(kt + 2);
     }
@@ -2405,6 +2450,16 @@ bool rel_fwd_plo() {
   return v == 1;
 }
 
+// STE_ATTN_PV16=1: the forward's PV product in fp16 on fp16-rounded P (rel4 F16)
+bool rel_fwd_pv16() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("STE_ATTN_PV16");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 // STE_ATTN_DQ=2: the v2 relative-key dQ kernel (A/B comparisons in one process)
 bool rel_dq_v3() {
   static int v = -1;
@@ -2462,7 +2517,8 @@ extern "C" int ste_attention_fwd(const ste_attn_args* a, void* stream) {
     // the hi/lo split of P only when a backward follows (o_lo given); a forward-only call (no_grad
     // evaluation) saves the second PV product
     if (rel_fwd_v4() && a->rel_left + a->rel_right + 1 <= rel4::max_nrel() && a->T <= rel4::MAXT * TK) {
-      if (a->o_lo && !rel_fwd_plo()) hipLaunchKernelGGL((attn_fwd_rel4_kernel<true, false>), g2, dim3(NT), rel4::FWD_LDS, s, *a);
+      if (a->o_lo && rel_fwd_pv16()) hipLaunchKernelGGL((attn_fwd_rel4_kernel<true, false, true>), g2, dim3(NT), rel4::FWD_LDS, s, *a);
+      else if (a->o_lo && !rel_fwd_plo()) hipLaunchKernelGGL((attn_fwd_rel4_kernel<true, false>), g2, dim3(NT), rel4::FWD_LDS, s, *a);
       else if (a->o_lo) hipLaunchKernelGGL(attn_fwd_rel4_kernel<true>, g2, dim3(NT), rel4::FWD_LDS, s, *a);
       else hipLaunchKernelGGL(attn_fwd_rel4_kernel<false>, g2, dim3(NT), rel4::FWD_LDS, s, *a);
     } else if (a->o_lo)
