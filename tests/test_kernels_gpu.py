@@ -734,6 +734,13 @@ def test_attention_relkey_o_lo(ops, T):
     _attn_case(ops, B=2, T=T, H=2, rel=True, masked=True, drop_p=0.0, o_lo=True, tol=1e-2)
 
 
+@pytest.mark.parametrize("o_lo", [False, True])
+def test_attention_relkey_past_v4_limit(ops, o_lo):
+    """T = 4,200 frames (84 s of audio) is past the v4 forward's 64 key tiles (rel4::MAXT): the v2
+    forward runs (with and without the hi/lo split), then the v3 backward, masked."""
+    _attn_case(ops, B=1, T=4200, H=1, rel=True, masked=True, drop_p=0.0, o_lo=o_lo)
+
+
 @pytest.mark.parametrize("drop_p", [0.0, 0.1])
 def test_attention_text_o_lo(ops, drop_p):
     _attn_case(ops, B=3, T=64, H=3, rel=False, masked=True, drop_p=drop_p, o_lo=True, qk_scale=0.3, v_common=1.0,
