@@ -633,7 +633,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(ste_attn_args a) {
 // Q·E[nrel-1]; inside, an LDS gather from the wave's Q·Eᵀ table.
 namespace rel2 {
 constexpr int WQ = 32, BQ = 128;
-constexpr int QEW = 76;                    // Q·Eᵀ row stride (>= left+right+1 = 73 bins)
+constexpr int QEW = NREL + 4;              // Q·Eᵀ row stride: every bin the C ABI admits (nrel <= NREL = 80)
 constexpr int KV = 2 * TILE;               // K | V of one tile
 constexpr int MASK_OFF = 2 * KV;           // 2 x 64 int32 key-mask words
 constexpr int QE_OFF = MASK_OFF + 512;

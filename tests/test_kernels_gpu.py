@@ -611,8 +611,10 @@ def test_layernorm_pair_matches_single_calls(ops, case):
 
 
 # -------------------------------------------------------------- attention
-def _attn_case(ops, B, T, H, rel, masked, drop_p, seed=7, qk_scale=0.7, v_common=0.0, o_lo=False, tol=1e-2):
-    """v_common > 0: every value row is a shared per-(batch, head) vector plus 0.05 noise, and
+def _attn_case(ops, B, T, H, rel, masked, drop_p, seed=7, qk_scale=0.7, v_common=0.0, o_lo=False, tol=1e-2, left=64,
+               right=8):
+    """left/right: the relative-distance window (w2v-bert: 64 / 8; nrel = left + right + 1 bins).
+    v_common > 0: every value row is a shared per-(batch, head) vector plus 0.05 noise, and
     qk_scale small makes the attention near-uniform (the random-init encoder regime): O ≈ mean(V)
     and dS = P(dP - delta) is a small difference of large terms."""
     torch.manual_seed(T * 7 + H)
@@ -633,22 +635,24 @@ def _attn_case(ops, B, T, H, rel, masked, drop_p, seed=7, qk_scale=0.7, v_common
         if masked == "all" and B > 2:
             m[2, :] = 0          # every key masked: uniform attention, like the reference's finfo.min fill
         mask = m.reshape(-1).contiguous()
-    E = (torch.randn(73, D, device=DEV) * 0.5).bfloat16() if rel else None
+    nrel = left + right + 1
+    E = (torch.randn(nrel, D, device=DEV) * 0.5).bfloat16() if rel else None
     o = torch.empty(B * T, W, device=DEV, dtype=torch.bfloat16)
     olo = torch.empty_like(o) if o_lo else None
     lse = torch.empty(B * H * T, device=DEV)
-    ops.attention_fwd(q, k, v, B=B, T=T, H=H, o=o, lse=lse, key_mask=mask, rel_E=E, drop_p=drop_p, seed=seed,
-                      o_lo=olo)
+    ops.attention_fwd(q, k, v, B=B, T=T, H=H, o=o, lse=lse, key_mask=mask, rel_E=E, rel_left=left, rel_right=right,
+                      drop_p=drop_p, seed=seed, o_lo=olo)
     qf, kf, vf = (t.float().view(B, T, H, D).clone().requires_grad_() for t in (q, k, v))
     Ef = E.float().clone().requires_grad_() if rel else None
-    ref = attention_ref(qf, kf, vf, mask.view(B, T) if masked else None, Ef, drop_p=drop_p, seed=seed)
+    ref = attention_ref(qf, kf, vf, mask.view(B, T) if masked else None, Ef, left=left, right=right, drop_p=drop_p,
+                        seed=seed)
     assert rel_err(o.view(B, T, H, D), ref) < 1e-2
     with torch.no_grad():  # saved log-sum-exp of the scaled, biased, masked scores
         qh, kh = qf.permute(0, 2, 1, 3), kf.permute(0, 2, 1, 3)
         sc = qh @ kh.transpose(-1, -2)
         if rel:
             pos = torch.arange(T, device=DEV)
-            dist = (pos.view(1, -1) - pos.view(-1, 1)).clamp(-64, 8) + 64
+            dist = (pos.view(1, -1) - pos.view(-1, 1)).clamp(-left, right) + left
             sc = sc + torch.gather(qh @ Ef.t(), 3, dist.view(1, 1, T, T).expand(B, H, T, T))
         sc = sc / math.sqrt(D)
         if masked:
@@ -660,10 +664,11 @@ def _attn_case(ops, B, T, H, rel, masked, drop_p, seed=7, qk_scale=0.7, v_common
     ref.backward(do.float().view(B, T, H, D))
     dqkv = torch.zeros(B * T, 3 * W, device=DEV, dtype=torch.bfloat16)
     delta = torch.empty(B * H * T, device=DEV)
-    dE = torch.zeros(73, D, device=DEV) if rel else None
+    dE = torch.zeros(nrel, D, device=DEV) if rel else None
     gw = torch.empty(B * H * T * 80, device=DEV) if rel else None
     ops.attention_bwd(q, k, v, o, lse, do, dqkv[:, :W], dqkv[:, W:2 * W], dqkv[:, 2 * W:], B=B, T=T, H=H, delta=delta,
-                      key_mask=mask, rel_E=E, drop_p=drop_p, seed=seed, dE=dE, gwork=gw, o_lo=olo)
+                      key_mask=mask, rel_E=E, rel_left=left, rel_right=right, drop_p=drop_p, seed=seed, dE=dE,
+                      gwork=gw, o_lo=olo)
     errs = {"dq": rel_err(dqkv[:, :W].view(B, T, H, D), qf.grad), "dk": rel_err(dqkv[:, W:2 * W].view(B, T, H, D), kf.grad),
             "dv": rel_err(dqkv[:, 2 * W:].view(B, T, H, D), vf.grad)}
     if rel:
@@ -732,6 +737,23 @@ def test_attention_relkey_near_uniform_delta_precision(ops):
 def test_attention_relkey_o_lo(ops, T):
     """The o_lo path at the c2 and c5 (30 s) frame counts, masked."""
     _attn_case(ops, B=2, T=T, H=2, rel=True, masked=True, drop_p=0.0, o_lo=True, tol=1e-2)
+
+
+@pytest.mark.parametrize("left,right", [(16, 16), (74, 0), (68, 8), (71, 8)])
+def test_attention_relkey_window(ops, left, right):
+    """Other relative windows through the C ABI (nrel = 33, 75, 77, 80): 33 and 75 on the v4 forward
+    (at most 75 bins), 77 and 80 (the table capacity) on the v2 forward; all on the v3 backward, with
+    and without the hi/lo split."""
+    for o_lo in (False, True):
+        _attn_case(ops, B=2, T=300, H=2, rel=True, masked=True, drop_p=0.0, o_lo=o_lo, left=left, right=right)
+
+
+@pytest.mark.parametrize("T", [99, 300])
+def test_attention_relkey_dropout(ops, T):
+    """Relative keys with attention dropout (the generic forward / dQ / dK-dV kernels; the
+    w2v-bert configs run the audio attention without dropout), standard and widest window."""
+    _attn_case(ops, B=2, T=T, H=2, rel=True, masked=True, drop_p=0.1)
+    _attn_case(ops, B=2, T=T, H=2, rel=True, masked=True, drop_p=0.1, left=71, right=8)
 
 
 @pytest.mark.parametrize("o_lo", [False, True])
