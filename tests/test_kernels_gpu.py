@@ -452,6 +452,51 @@ def test_attention_f32_fwd(ops, B, T, H, drop_p, masked):
         assert rel_err(got.view(B, T, H, D), want) < 1e-2
 
 
+@pytest.mark.parametrize("T,drop_p,f32", [(70, 0.0, False), (130, 0.1, False), (70, 0.0, True), (130, 0.1, True)])
+def test_attention_zero_masked_rows(ops, T, drop_p, f32):
+    """zero_masked_rows = 1 (the XLM-R SDPA rule): a sample whose every key is masked gets zero
+    output, LSE +inf and zero gradients; the other samples are unaffected.  bf16 forward or the
+    fp32 text forward, then the bf16 backward."""
+    torch.manual_seed(T)
+    B, H, D = 3, 2, 64
+    W = H * D
+    qkv = torch.randn(B * T, 3 * W, device=DEV) * 0.7
+    if not f32:
+        qkv = qkv.bfloat16()
+    q, k, v = qkv[:, :W], qkv[:, W:2 * W], qkv[:, 2 * W:]
+    m = torch.ones(B, T, dtype=torch.int32, device=DEV)
+    m[0, T - T // 3:] = 0
+    m[1, :] = 0                      # every key of sample 1 masked
+    mask = m.reshape(-1).contiguous()
+    o = torch.empty(B * T, W, device=DEV, dtype=torch.bfloat16)
+    olo = torch.empty_like(o)
+    lse = torch.empty(B * H * T, device=DEV)
+    if f32:
+        o32 = torch.empty(B * T, W, device=DEV)
+        ops.attention_fwd_f32(q, k, v, B=B, T=T, H=H, o32=o32, lse=lse, o=o, o_lo=olo, key_mask=mask, drop_p=drop_p,
+                              seed=5, zero_masked_rows=True)
+        assert torch.count_nonzero(o32.view(B, T, W)[1]) == 0
+    else:
+        ops.attention_fwd(q, k, v, B=B, T=T, H=H, o=o, lse=lse, key_mask=mask, drop_p=drop_p, seed=5, o_lo=olo,
+                          zero_masked_rows=True)
+    assert torch.count_nonzero(o.view(B, T, W)[1]) == 0 and torch.count_nonzero(olo.view(B, T, W)[1]) == 0
+    assert torch.isposinf(lse.view(B, H, T)[1]).all() and torch.isfinite(lse.view(B, H, T)[[0, 2]]).all()
+    qb, kb, vb = (t.bfloat16() for t in (q, k, v))
+    do = torch.randn(B * T, W, device=DEV).bfloat16()
+    dq, dk, dv = (torch.full((B * T, W), 7.0, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    ops.attention_bwd(qb, kb, vb, o, lse, do, dq, dk, dv, B=B, T=T, H=H, delta=torch.empty(B * H * T, device=DEV),
+                      key_mask=mask, drop_p=drop_p, seed=5, o_lo=olo)
+    # reference: the uniform-fill reference with sample 1 multiplied out (zero output, zero gradients)
+    qf, kf, vf = (t.float().view(B, T, H, D).clone().requires_grad_() for t in (qb, kb, vb))
+    keep = torch.tensor([1.0, 0.0, 1.0], device=DEV).view(B, 1, 1, 1)
+    rf = attention_ref(qf, kf, vf, m, drop_p=drop_p, seed=5) * keep
+    assert rel_err(o.float().view(B, T, H, D), rf) < 1e-2
+    rf.backward(do.float().view(B, T, H, D))
+    for got, want in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+        assert torch.count_nonzero(got.view(B, T, W)[1]) == 0
+        assert rel_err(got.view(B, T, H, D), want) < 1e-2
+
+
 # -------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("cols", [160, 768, 1024])
 def test_layernorm_fwd_bwd(ops, cols):
