@@ -40,6 +40,20 @@ def test_gemm_layouts(ops, M, N, K):
     assert rel_err(ops.linear_dw(dy, x), dy.float().t() @ x.float()) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 1, 8), (7, 3, 72), (100, 5, 1024), (333, 1, 768), (2, 24, 8)])
+def test_gemm_tiny_shapes(ops, M, N, K):
+    """The edges of the GEMM contract: one row, one to five output columns (N < 8: the element-wise
+    epilogue tail; e.g. the attention-pooling scorer's single logit), the minimum K of 8; fp32 and
+    bf16 outputs, with and without bias."""
+    torch.manual_seed(M * 31 + N)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = torch.randn(N, K, device=DEV).bfloat16()
+    b = torch.randn(N, device=DEV)
+    ref = x.double() @ w.double().t()
+    assert rel_err(ops.linear(x, w, b), ref + b.double()) < 1e-6
+    assert rel_err(ops.linear(x, w, None, out_bf16=True), ref) < 4e-3
+
+
 @pytest.mark.parametrize("rows,cols", [(1024, 4096), (3072, 1024), (130, 77), (64, 1), (1000, 4100)])
 def test_transpose16(ops, rows, cols):
     x = torch.randn(rows, cols, device=DEV).bfloat16()
