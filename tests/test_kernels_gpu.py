@@ -512,7 +512,7 @@ def test_attention_zero_masked_rows(ops, T, drop_p, f32):
 
 
 # -------------------------------------------------------------- LayerNorm
-@pytest.mark.parametrize("cols", [160, 768, 1024])
+@pytest.mark.parametrize("cols", [4, 160, 260, 768, 1024])   # 4 / 260: partial column groups of a wave
 def test_layernorm_fwd_bwd(ops, cols):
     from speech_transcript_embeddings_amd import _lib
     torch.manual_seed(cols)
@@ -544,6 +544,21 @@ def test_layernorm_fwd_bwd(ops, cols):
         assert rel_err(dxb, 0.5 * (xr.grad + dres)) < 5e-3
         assert rel_err(dg, gr.grad) < 1e-5
         assert rel_err(db, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("cols", [1028, 2048])
+def test_layernorm_fwd_wide_rows(ops, cols):
+    """The forward's widest form (ste_layernorm_fwd admits up to 2,048 columns; the backward 1,024)."""
+    torch.manual_seed(cols)
+    rows = 129
+    x = (torch.randn(rows, cols, device=DEV) * 3 - 1).bfloat16()
+    g, b = torch.randn(cols, device=DEV), torch.randn(cols, device=DEV)
+    y = torch.empty(rows, cols, device=DEV)
+    mean, rstd = ops.layernorm_fwd(x, g, b, 1e-5, y=y)
+    xd = x.double()
+    assert rel_err(y, F.layer_norm(xd, (cols,), g.double(), b.double(), 1e-5)) < 1e-5
+    assert rel_err(mean, xd.mean(1)) < 1e-6
+    assert rel_err(rstd, (xd.var(1, unbiased=False) + 1e-5).rsqrt()) < 1e-5
 
 
 @pytest.mark.parametrize("reduce", [False, True])
