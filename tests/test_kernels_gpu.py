@@ -756,7 +756,7 @@ def _attn_case(ops, B, T, H, rel, masked, drop_p, seed=7, qk_scale=0.7, v_common
     return errs
 
 
-@pytest.mark.parametrize("T", [40, 99, 150, 499])   # T < 64: the small-T dE kernel; else the MFMA one
+@pytest.mark.parametrize("T", [17, 40, 99, 150, 499])   # T < 64: the small-T dE kernel; else the MFMA one
 def test_attention_relkey(ops, T):
     _attn_case(ops, B=2, T=T, H=2, rel=True, masked=True, drop_p=0.0)
 
@@ -841,6 +841,12 @@ def test_attention_relkey_past_v4_limit(ops, o_lo):
 def test_attention_text_o_lo(ops, drop_p):
     _attn_case(ops, B=3, T=64, H=3, rel=False, masked=True, drop_p=drop_p, o_lo=True, qk_scale=0.3, v_common=1.0,
                tol=1e-2)
+
+
+@pytest.mark.parametrize("T", [37, 130])
+def test_attention_text_ragged(ops, T):
+    """Text attention at a partial key tile and past two tiles, with dropout."""
+    _attn_case(ops, B=3, T=T, H=3, rel=False, masked=True, drop_p=0.1)
 
 
 @pytest.mark.parametrize("drop_p", [0.0, 0.1])
