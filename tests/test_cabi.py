@@ -157,3 +157,21 @@ def test_argument_errors_return_status_without_launch(lib):
     with pytest.raises(lib.SteError):
         lib.call("ste_copy2d", None, 1, None, 1, 4, 4, 3, None)  # elem_bytes must be 2 or 4
     assert lib.fn("ste_scale_rows")(None, None, 4, 0, 1, None) != 0
+
+
+def test_attention_contract_errors(lib):
+    """The attention entry points reject a relative window past the 80-bin table, unaligned row
+    strides and a dropout rate outside [0, 1) with a status, before any launch."""
+    ERR_ARG, ERR_SHAPE = 1001, 1002                       # include/ste.h STE_ERR_ARG / STE_ERR_SHAPE
+    a = lib.AttnArgs()
+    a.B, a.T, a.H = 2, 100, 2
+    a.ldq = a.ldk = a.ldv = a.ldo = 384
+    a.rel_E, a.rel_left, a.rel_right = 16, 72, 8          # 81 bins (pointer never dereferenced)
+    assert lib.fn("ste_attention_fwd")(C.byref(a), None) == ERR_SHAPE
+    assert lib.fn("ste_attention_bwd")(C.byref(a), None) == ERR_SHAPE
+    a.rel_left = 71                                       # 80 bins, but no o / lse given
+    assert lib.fn("ste_attention_fwd")(C.byref(a), None) == ERR_ARG
+    a.ldk = 388                                           # row stride not a multiple of 8 elements
+    assert lib.fn("ste_attention_fwd")(C.byref(a), None) == ERR_SHAPE
+    a.ldk, a.drop_p = 384, 1.0
+    assert lib.fn("ste_attention_fwd")(C.byref(a), None) == ERR_ARG
