@@ -221,7 +221,8 @@ int ste_layernorm_bwd_pair(const ste_ln_bwd_args* a, const ste_ln_bwd_args* b, v
  *          tf:…xlm_roberta…:186-250.
  * q/k/v/o are bf16 [B*T, *] with row strides ldq/ldk/ldv/ldo; head h uses
  * columns h*64..h*64+63 (head_dim fixed at 64).  key_mask [B*T] (nonzero = valid)
- * may be NULL.  rel_E [left+right+1, 64] bf16 may be NULL (no relative bias).
+ * may be NULL.  rel_E [left+right+1, 64] bf16 may be NULL (no relative bias); windows of up to
+ * 80 bins (left + right + 1 <= 80; STE_ERR_SHAPE beyond).
  * lse [B*H*T] fp32 is saved for backward.
  */
 typedef struct {
