@@ -44,18 +44,30 @@ def stats(db):
         w.writerow([n, k, int(s), round(mu, 3), round(100 * s / total, 2), int(min(v)), int(max(v)), round(sd, 3)])
 
 
-def counter(db, name):
+def _grid_col(c):
+    cols = [r[1] for r in c.execute("pragma table_info(counters_collection)").fetchall()]
+    for n in ("grid_size", "grid_size_x", "grid_x"):
+        if n in cols:
+            return n
+    return None
+
+
+def counter(db, name, with_grid=False):
+    """[(kernel, value)] (or [(kernel, grid, value)]) per dispatch of the last step."""
     c = sqlite3.connect(db)
-    rows = c.execute("select dispatch_id, kernel_name, value from counters_collection where counter_name = ?",
-                     (name,)).fetchall()
-    agg = defaultdict(lambda: [None, 0.0])
-    for d, k, v in rows:
+    gc = _grid_col(c) if with_grid else None
+    sel = f"dispatch_id, kernel_name, {gc if gc else '0'}, value"
+    rows = c.execute(f"select {sel} from counters_collection where counter_name = ?", (name,)).fetchall()
+    agg = defaultdict(lambda: [None, 0, 0.0])
+    for d, k, gr, v in rows:
         a = agg[d]
-        a[0] = k
-        a[1] += float(v)
+        a[0], a[1] = k, gr
+        a[2] += float(v)
     out = sorted(agg.items())
-    start = max(i for i, (_, (k, _)) in enumerate(out) if "fbank_logmel_kernel" in k)
-    return [(k, v) for _, (k, v) in out[start:]]
+    start = max(i for i, (_, (k, _, _)) in enumerate(out) if "fbank_logmel_kernel" in k)
+    if with_grid:
+        return [(k, gr, v) for _, (k, gr, v) in out[start:]]
+    return [(k, v) for _, (k, _, v) in out[start:]]
 
 
 def traffic(fdb, wdb):
@@ -68,8 +80,21 @@ def traffic(fdb, wdb):
         acc[short(k)][2] += v * 1024
     out = {k: {"launches": n, "fetch_bytes_per_launch": round(f / n), "write_bytes_per_launch": round(w / n),
                "hbm_bytes_per_launch": round((f + w) / n)} for k, (n, f, w) in acc.items() if n}
-    print(json.dumps(dict(sorted(out.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * kv[1]["launches"])),
-                     indent=1))
+    res = dict(sorted(out.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * kv[1]["launches"]))
+    # the same per launch population: kernel name + grid size (work-items), so that one kernel's
+    # launches at different shapes (audio vs text rows, main vs side stream) can be compared with
+    # bench.py's per-shape algorithmic bytes
+    byg = defaultdict(lambda: [0, 0.0, 0.0])
+    for k, gr, v in counter(fdb, "FETCH_SIZE", True):
+        a = byg[f"{short(k)}@{gr}"]
+        a[0] += 1
+        a[1] += 2.0 * v * 1024
+    for k, gr, v in counter(wdb, "WRITE_SIZE", True):
+        byg[f"{short(k)}@{gr}"][2] += v * 1024
+    res["by_grid"] = {k: {"launches": n, "fetch_bytes_per_launch": round(f / n), "write_bytes_per_launch": round(w / n),
+                          "hbm_bytes_per_launch": round((f + w) / n)}
+                      for k, (n, f, w) in sorted(byg.items(), key=lambda kv: -(kv[1][1] + kv[1][2])) if n}
+    print(json.dumps(res, indent=1))
 
 
 def pmc(*dbs):

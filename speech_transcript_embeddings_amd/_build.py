@@ -16,6 +16,11 @@ CSRC = PKG / "csrc"
 INCLUDE = PKG.parent / "include"
 OBJ = PKG / "_obj"
 LIB = PKG / "libste.so"
+# -DSTE_AB: the A/B build (libste_ab.so, objects in _obj_ab) whose switches read STE_* environment
+# variables (csrc/common.h STE_AB_ENV); the shipped libste.so reads none.  Select it at run time with
+# STE_LIB=.../libste_ab.so (_lib.py).
+OBJ_AB = PKG / "_obj_ab"
+LIB_AB = PKG / "libste_ab.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # No packed-fp32 VALU code (v_pk_add/mul/fma_f32): on the MI355X, with another stream's MFMA
@@ -35,11 +40,11 @@ def _headers_mtime() -> float:
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
-def _compile(src: Path, hdr_mtime: float, verbose: bool) -> Path:
-    obj = OBJ / (src.stem + ".o")
+def _compile(src: Path, hdr_mtime: float, verbose: bool, ab: bool = False) -> Path:
+    obj = (OBJ_AB if ab else OBJ) / (src.stem + ".o")
     if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, hdr_mtime):
         return obj
-    cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *FLAGS, *(["-DSTE_AB"] if ab else []), "-c", str(src), "-o", str(obj)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -48,22 +53,23 @@ def _compile(src: Path, hdr_mtime: float, verbose: bool) -> Path:
     return obj
 
 
-def build(verbose: bool = False, jobs: int = 8) -> Path:
-    OBJ.mkdir(exist_ok=True)
+def build(verbose: bool = False, jobs: int = 8, ab: bool = False) -> Path:
+    obj_dir, lib = (OBJ_AB, LIB_AB) if ab else (OBJ, LIB)
+    obj_dir.mkdir(exist_ok=True)
     srcs = sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp"))
     hm = _headers_mtime()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hm, verbose), srcs))
+        objs = list(ex.map(lambda s: _compile(s, hm, verbose, ab), srcs))
     newest = max(o.stat().st_mtime for o in objs)
-    if not LIB.exists() or LIB.stat().st_mtime < newest:
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs)]
+    if not lib.exists() or lib.stat().st_mtime < newest:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib), *map(str, objs)]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    print(build(verbose="-v" in sys.argv, ab="--ab" in sys.argv))

@@ -19,6 +19,14 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("STE_LIB", _PKG / "libste.so"))
+# the A/B build (_build.py --ab: libste_ab.so) is the only configuration whose STE_* switches read
+# the environment, on both sides of the ABI; with the shipped libste.so every switch is its default
+AB_BUILD = LIB_PATH.name == "libste_ab.so"
+
+
+def ab_env(name: str, default: str) -> str:
+    """An A/B switch's value: the environment's under the A/B build, else `default`."""
+    return os.environ.get(name, default) if AB_BUILD else default
 
 c_void_p, c_int, c_int64, c_float, c_uint64, c_char_p = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_uint64, C.c_char_p
 c_i32p = C.POINTER(C.c_int32)

@@ -19,7 +19,6 @@
 // read both row-wise (ds_read_b128) and transposed (ds_read_b64_tr_b16).  The
 // "swapped" products (Sᵀ = K·Qᵀ) keep the softmax row on the lane, and accumulator
 // tiles feed the next MFMA directly as B operands (no LDS round trip for P or dS).
-#include <cstdlib>
 #include <type_traits>
 #include "common.h"
 #include "../../include/ste.h"
@@ -975,47 +974,16 @@ STE_DEV s16x4 ds_read_tr16_off(uint32_t addr) {
   return r;
 }
 
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-STE_DEV f32x4 mfma16h(bf16x8 a, f16x8 b, f32x4 c) {   // a: fp16 bits carried in a bf16x8
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), b, c, 0, 0, 0);
-}
-STE_DEV f16x8 pack_acc_h(f32x4 a, f32x4 b) {   // as pack_acc, to fp16 (round to nearest even)
-  f16x8 v;
-  v[0] = (_Float16)a[0]; v[1] = (_Float16)a[1]; v[2] = (_Float16)a[2]; v[3] = (_Float16)a[3];
-  v[4] = (_Float16)b[0]; v[5] = (_Float16)b[1]; v[6] = (_Float16)b[2]; v[7] = (_Float16)b[3];
-  return v;
-}
-// the wave's two V pieces (16 bytes per lane each, see glds_tile_piece) bf16 -> fp16 in place; the
-// caller has waited for their DMA and waits for these LDS writes before the block barrier
-STE_DEV void v_tile_to_f16(char* vtile, int w, int lane) {
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-  for (int pp = 0; pp < 2; ++pp) {
-    u32x4* p = reinterpret_cast<u32x4*>(vtile + (2 * w + pp) * 1024 + lane * 16);
-    const u32x4 x = *p;
-    u32x4 y;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      // bf16 -> f32 is exact; f32 -> f16 exact in range (round toward zero saturates at 65504)
-      const auto h = __builtin_amdgcn_cvt_pkrtz(__builtin_bit_cast(float, x[i] << 16),
-                                                __builtin_bit_cast(float, x[i] & 0xffff0000u));
-      y[i] = __builtin_bit_cast(unsigned, h);
-    }
-    *p = y;
-  }
-}
-
-// SPLIT: o_lo is written (the fp32 O as bf16 hi + lo, for the backward's delta) and the row sums
-// are fp32 sums of the exact p.  PLO: the PV product also runs on the low half of P (hi + lo P
-// within 2^-16 of p); without it P is bf16 in PV as in the plain forward and O carries P's
-// rounding (about 2^-9 / sqrt(keys) relative) while o_lo still keeps O's fp32 value (A/B:
-// STE_ATTN_PLO=0).
-// F16 (with SPLIT): the PV product in fp16 on P rounded to nearest fp16 (2^-11 relative, 8x finer
-// than bf16) and one MFMA per u, V converted bf16 -> fp16 in LDS once per tile (exact for
-// |v| < 65504, larger magnitudes saturate) by the wave that staged it (v_tile_to_f16).
-template <bool SPLIT, bool PLO = SPLIT, bool F16 = false>
+// SPLIT: o_lo is written (O as bf16 hi + lo, for the backward's delta = dO·O).
+// PLO: the PV product runs on P = bf16(P) + bf16(P - bf16(P)) (hi + lo within 2^-16 of p) and the
+// row sum is the fp32 sum of the exact p.  Without PLO the PV product runs on bf16 P and the row
+// sum is the MFMA sum of the SAME rounded P, so O = Σ P̃ V / Σ P̃ is a weighted mean whose weights
+// sum to 1 up to fp32 accumulation: a component common to every V row passes into O exactly, and
+// delta = dO·O cancels it in the backward's dP - delta as the exact-P delta does (the near-uniform
+// regime of tests/test_kernels_gpu.py).  Forward-only calls (no o_lo) use the same product.
+template <bool SPLIT, bool PLO>
 __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
-  static_assert(!F16 || (SPLIT && !PLO), "F16 replaces the hi/lo split of P");
+  static_assert(SPLIT || !PLO, "the hi/lo split of P only serves the backward's delta");
   using namespace rel4;
   extern __shared__ __attribute__((aligned(16))) char sm[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
@@ -1069,7 +1037,6 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
   // entries 0..PADL-1 replicate bin 0 and PADL+nrel.. replicate bin nrel-1
   float* qe = reinterpret_cast<float*>(sm + QE_OFF) + w * WQ * QS;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's tile-0 and E pieces, Q
-  if constexpr (F16) v_tile_to_f16(sm + TILE, w, lane);
   __syncthreads();                                    // every wave's E pieces and validity words
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq)
@@ -1122,7 +1089,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
   };
   float m[2] = {-INFINITY, -INFINITY};
   f32x4 o[2][4], lsum[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  float lp[2] = {0.f, 0.f};   // SPLIT: per-lane fp32 partial row sums of the exact p (reduced at the end)
+  float lp[2] = {0.f, 0.f};   // PLO: per-lane fp32 partial row sums of the exact p (reduced at the end)
   bf16x8 ones;
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
@@ -1205,7 +1172,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
       if (__builtin_amdgcn_ballot_w64(tmax > m[gq] + THRESH) != 0ull) {
         const float mnew = fmaxf(m[gq], tmax);
         const float alpha = __builtin_amdgcn_exp2f(m[gq] - mnew);
-        if (SPLIT) lp[gq] *= alpha;
+        if (PLO) lp[gq] *= alpha;
         else lsum[gq] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
@@ -1217,7 +1184,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           s[gq][t][r] = (STE_ABLATE & 128) ? s[gq][t][r] - mg : __builtin_amdgcn_exp2f(s[gq][t][r] - mg);
-      if (SPLIT) {   // the row sum of p itself (hi + lo P sums to p within 2^-16): fp32 adds, not 2 MFMAs per u
+      if (PLO) {   // the row sum of p itself (hi + lo P sums to p within 2^-16): fp32 adds, not 2 MFMAs per u
         f32x4 t01 = (s[gq][0] + s[gq][1]) + (s[gq][2] + s[gq][3]);
         lp[gq] += (t01[0] + t01[1]) + (t01[2] + t01[3]);
       }
@@ -1225,21 +1192,13 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        if constexpr (F16) {
-          const f16x8 ph = pack_acc_h(s[gq][2 * u], s[gq][2 * u + 1]);
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16h(vf[dt][u], ph, o[gq][dt]);
-          continue;
-        }
         const bf16x8 pb = pack_acc(s[gq][2 * u], s[gq][2 * u + 1]);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pb, o[gq][dt]);
-        if (SPLIT) {
-          if constexpr (PLO) {
-            const bf16x8 pl = pack_acc_lo(s[gq][2 * u], s[gq][2 * u + 1], pb);
+        if constexpr (PLO) {
+          const bf16x8 pl = pack_acc_lo(s[gq][2 * u], s[gq][2 * u + 1], pb);
 #pragma unroll
-            for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pl, o[gq][dt]);
-          }
+          for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pl, o[gq][dt]);
         } else {
           lsum[gq] = mfma16(ones, pb, lsum[gq]);   // row sum of the same (rounded) P, on the MFMA
         }
@@ -1247,10 +1206,6 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
     }
     if (kt + 1 < nkt) {
       if (!(STE_ABLATE & 32)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (this wave's pieces)
-      if constexpr (F16) {
-        v_tile_to_f16(sm + (slot ^ 1) * KV + TILE, w, lane);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
       if (!(STE_ABLATE & 256)) __builtin_amdgcn_s_barrier();                     // ... every wave's, and tile kt fully read
       if (kt + 2 < nkt) issue(kt + 2);
     }
@@ -1262,7 +1217,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq) {
     // every accumulator row holds the full row sum (MFMA form) / the 4 lanes of a row hold partials
-    const float lt = SPLIT ? rowsum4(lp[gq]) : lsum[gq][0];
+    const float lt = PLO ? rowsum4(lp[gq]) : lsum[gq][0];
     const int myq = qw + 16 * gq + li;
     if (myq < T) {
       const float inv_l = 1.0f / lt;
@@ -1282,240 +1237,9 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
     }
   }
 }
-// ====================================== relative-key backward, v2: dQ (+ delta, + bins G)
-// 4 waves x 16 queries, K/V ring as in the forward.  delta = rowsum(dO*O) is computed here
-// from the wave's own dO/O fragments (no separate pass) and written for the dK/dV kernel.
-// Probabilities in the exp2 domain: p = exp2((s + bias)*c2 - lse*log2e); a masked key gets
-// exp(NEG_MASK - lse) (0, or 1/l for a row whose every key is masked).  Distance bins:
-// outside the band a whole tile falls into bin 0 or nrel-1 (register sums); inside, the
-// unique interior bin of each (query, key) is stored to the wave's G table.
-namespace rel2 {
-constexpr int DQ_Q = 64;                         // queries per block
-constexpr int GW = 96;                           // G row stride (3 k-steps of 32 for G·E)
-constexpr int DQ_QE_OFF = MASK_OFF + 512;
-constexpr int DQ_G_OFF = DQ_QE_OFF + 4 * 16 * QEW * 4;
-constexpr int DQ_LDS = DQ_G_OFF + 4 * 16 * GW * 4;
-}  // namespace rel2
-
-__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel2_kernel(ste_attn_args a) {
-  using namespace rel2;
-  extern __shared__ __attribute__((aligned(16))) char sm[];
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int T = a.T, H = a.H;
-  const int ntile = (T + DQ_Q - 1) / DQ_Q;
-  const int id = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = id % ntile, bh = id / ntile, h = bh % H, b = bh / H, bT = b * T;
-  const int left = a.rel_left, right = a.rel_right, nrel = left + right + 1;
-  const bf16* Qb = (const bf16*)a.q + h * HD;
-  const bf16* Kb = (const bf16*)a.k + h * HD;
-  const bf16* Vb = (const bf16*)a.v + h * HD;
-  const bf16* dOb = (const bf16*)a.dout + h * HD;
-  const bf16* Ob = (const bf16*)a.o + h * HD;
-  const bf16* Olb = a.o_lo ? (const bf16*)a.o_lo + h * HD : nullptr;
-  const int q0 = tile * DQ_Q + w * 16, myq = q0 + li;
-  const bool qvalid = myq < T;
-  const int64_t rowid = (int64_t)(b * H + h) * T + myq;
-  const float c2 = a.scale * LOG2E;
-
-  bf16x8 qf[2], df[2];
-  float dpart = 0.f;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int64_t off = (int64_t)(bT + myq);
-    qf[s] = qvalid ? *reinterpret_cast<const bf16x8*>(Qb + off * a.ldq + 32 * s + 8 * g) : bf16x8{};
-    df[s] = qvalid ? *reinterpret_cast<const bf16x8*>(dOb + off * a.lddo + 32 * s + 8 * g) : bf16x8{};
-    const bf16x8 of = qvalid ? *reinterpret_cast<const bf16x8*>(Ob + off * a.ldo + 32 * s + 8 * g) : bf16x8{};
-    const bf16x8 ol = (qvalid && Olb) ? *reinterpret_cast<const bf16x8*>(Olb + off * a.ldolo + 32 * s + 8 * g)
-                                      : bf16x8{};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) dpart += (float)df[s][e] * ((float)of[e] + (float)ol[e]);
-  }
-  dpart += __shfl_xor(dpart, 16, 64);
-  dpart += __shfl_xor(dpart, 32, 64);
-  const float dl = dpart;
-  if (qvalid && g == 0) a.delta[rowid] = dl;
-  const float lse = qvalid ? a.lse[rowid] : 0.f;
-  const float nl2 = -lse * LOG2E;
-  const float pm = lse == -INFINITY ? 1.0f / T : 0.f;   // probability of a masked key in this row
-
-  float* qe = reinterpret_cast<float*>(sm + DQ_QE_OFF) + w * 16 * QEW;
-  float* gt = reinterpret_cast<float*>(sm + DQ_G_OFF) + w * 16 * GW;
-  stage_E(sm, (const bf16*)a.rel_E, nrel, GW, tid);
-  for (int i = lane; i < 16 * GW; i += 64) gt[i] = 0.f;
-  __syncthreads();
-#pragma unroll
-  for (int jt = 0; jt < NREL / 16; ++jt) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sm, jt * 16, s, lane), qf[s], acc);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = jt * 16 + 4 * g + r;
-      if (j < QEW) qe[li * QEW + j] = acc[r];
-    }
-  }
-  __syncthreads();
-  const float blo = qe[li * QEW] * c2 + nl2, bhi = qe[li * QEW + nrel - 1] * c2 + nl2;
-  const float* qrow = qe + li * QEW + left;
-  float* grow = gt + li * GW + left;
-
-  char* sMask = sm + MASK_OFF;
-  const int nkt = (T + TK - 1) / TK;
-  const bool has_mask = a.key_mask != nullptr;
-  auto issue = [&](int kt) {
-    char* buf = sm + (kt & 1) * KV;
-    const int kb = kt * TK;
-    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w, lane);
-    glds_tile_piece(Kb, a.ldk, bT, kb, T, buf, 2 * w + 1, lane);
-    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w, lane);
-    glds_tile_piece(Vb, a.ldv, bT, kb, T, buf + TILE, 2 * w + 1, lane);
-    if (w == 0 && has_mask) glds_mask(a.key_mask, bT, kb, T, sMask + (kt & 1) * 256, lane);
-  };
-  issue(0);
-  if (nkt > 1) issue(1);
-  if (nkt > 1) {
-    if (w == 0 && has_mask) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-
-  f32x4 dq[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float glo = 0.f, ghi = 0.f;
-
-  for (int kt = 0; kt < nkt; ++kt) {
-    const char* tK = sm + (kt & 1) * KV;
-    const char* tV = tK + TILE;
-    const int* mk = reinterpret_cast<const int*>(sMask + (kt & 1) * 256);
-    const int kb = kt * TK;
-    f32x4 sc[4], dp[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[t] = sc[t];
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        sc[t] = mfma16(frag_kc(tK, t * 16, ss, lane), qf[ss], sc[t]);
-        dp[t] = mfma16(frag_kc(tV, t * 16, ss, lane), df[ss], dp[t]);
-      }
-    }
-    bf16x8 ktr[4][2];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) ktr[dt][u] = frag_tr_asm(tK, dt * 16, u, lane);
-    const bool lane_in = kb + lane < T;
-    const uint64_t in_bits = __ballot(lane_in);
-    const uint64_t ok_bits = __ballot(lane_in && (!has_mask || mk[lane] != 0));
-    const bool all_valid = ok_bits == ~0ull;
-    const bool all_lo = (kb + TK - 1) - q0 <= -left;
-    const bool all_hi = kb - (q0 + 15) >= right;
-    const bool band = !(all_lo || all_hi);
-    if (!band) {
-      const float cb = all_lo ? blo : bhi;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sc[t][r] = __builtin_amdgcn_exp2f(fmaf(sc[t][r], c2, cb));
-    } else {
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int d = kb + 16 * t + 4 * g + r - myq;
-          d = med3i(d, -left, right);
-          sc[t][r] = __builtin_amdgcn_exp2f(fmaf(sc[t][r] + qrow[d], c2, nl2));
-        }
-    }
-    if (!all_valid) {
-      const uint64_t inl = in_bits >> (4 * g), okl = ok_bits >> (4 * g);
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int bit = 16 * t + r;
-          const float fill = ((inl >> bit) & 1) ? pm : 0.f;
-          sc[t][r] = ((okl >> bit) & 1) ? sc[t][r] : fill;
-        }
-    }
-    // dS = P (dP - delta); bins
-    float bsum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float ds = sc[t][r] * (dp[t][r] - dl);
-        sc[t][r] = ds;
-        bsum += ds;
-      }
-    if (!band) {
-      if (all_lo) glo += bsum; else ghi += bsum;
-    } else {
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int d = kb + 16 * t + 4 * g + r - myq;
-          if (d <= -left) glo += sc[t][r];
-          else if (d >= right) ghi += sc[t][r];
-          else grow[d] = sc[t][r];
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const bf16x8 pb = pack_acc(sc[2 * u], sc[2 * u + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(ktr[dt][u], pb, dq[dt]);
-    }
-    if (kt + 1 < nkt) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (kt + 2 < nkt) issue(kt + 2);
-    }
-  }
-  glo += __shfl_xor(glo, 16, 64);
-  glo += __shfl_xor(glo, 32, 64);
-  ghi += __shfl_xor(ghi, 16, 64);
-  ghi += __shfl_xor(ghi, 32, 64);
-  if (g == 0) {
-    gt[li * GW] = glo;
-    gt[li * GW + nrel - 1] = ghi;
-  }
-  __syncthreads();                       // ring free: restage E (96 rows) for dQ += G·E
-  stage_E(sm, (const bf16*)a.rel_E, nrel, GW, tid);
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const f32x4 g0 = *reinterpret_cast<const f32x4*>(gt + li * GW + 32 * u + 4 * g);
-    const f32x4 g1 = *reinterpret_cast<const f32x4*>(gt + li * GW + 32 * u + 16 + 4 * g);
-    const bf16x8 pb = pack_acc(g0, g1);
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(frag_tr(sm, dt * 16, u, lane), pb, dq[dt]);
-  }
-  if (a.dE && qvalid) {
-    float* G = a.gwork + rowid * NREL;
-#pragma unroll
-    for (int c = 0; c < NREL / 16; ++c) {
-      const int j = c * 16 + 4 * g;
-      *reinterpret_cast<f32x4*>(G + j) = *reinterpret_cast<const f32x4*>(gt + li * GW + j);
-    }
-  }
-  if (qvalid) {
-    bf16* dQ = (bf16*)a.dq + (int64_t)(bT + myq) * a.lddq + h * HD;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) store_bf16x4(dQ + 16 * dt + 4 * g, dq[dt] * a.scale);
-  }
-}
-
-// ====================================== relative-key backward, v3: dQ (+ delta, + bins G)
-// v2's schedule with 32 queries per wave: two 16-row groups share every K, V and transposed-K
-// fragment read (half the LDS traffic per MFMA, as in the forward), 128 queries per block.
+// ====================================== relative-key backward: dQ (+ delta, + bins G)
+// 4 waves x 32 queries: two 16-row groups share every K, V and transposed-K fragment read (half
+// the LDS traffic per MFMA, as in the forward), 128 queries per block, K/V in a 2-deep DMA ring.
 // The per-row Q·Eᵀ table and the G (distance-bin) table share one LDS row: an interior bin
 // d (-left < d < right) of a query is read for exactly one key (k = q + d), right before that
 // key's dS is written to the same slot; the clamped bins 0 and nrel-1 stay intact for the other
@@ -1821,7 +1545,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
   }
 }
 
-// ================================================= relative-key backward, v2: dK and dV
+// ================================================= relative-key backward: dK and dV
 // 4 waves x 32 keys (two 16-key groups sharing every Q/dO fragment read), 128 keys per
 // block, iterating over query tiles of 64 whose Q, dO, lse and delta are staged by
 // global_load_lds into a 2-deep ring.  Per query tile the four waves rebuild that tile's
@@ -1832,216 +1556,15 @@ constexpr int KB = 128;                          // keys per block
 constexpr int QD = 2 * TILE + 512;               // Q | dO | lse[64] | delta[64]
 constexpr int KV_E_OFF = 2 * QD;
 constexpr int KV_QE_OFF = KV_E_OFF + NREL * 128;
-constexpr int KV_EDGE_OFF = KV_QE_OFF + 64 * QEW * 4;   // elo[64], ehi[64]
-constexpr int DKV_LDS = KV_EDGE_OFF + 512;
 constexpr int QE3 = NREL + 4;                               // v3: Q·Eᵀ rows padded to 84 floats
 constexpr int KV_EDGE3_OFF = KV_QE_OFF + 64 * QE3 * 4;     // (the band reads: <= 2-way bank conflicts)
 constexpr int DKV3_LDS = KV_EDGE3_OFF + 512;
 }  // namespace rel2
 
-__global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel2_kernel(ste_attn_args a) {
-  using namespace rel2;
-  extern __shared__ __attribute__((aligned(16))) char sm[];
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int T = a.T, H = a.H;
-  const int ntile = (T + KB - 1) / KB;
-  const int id = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = id % ntile, bh = id / ntile, h = bh % H, b = bh / H, bT = b * T;
-  const int left = a.rel_left, right = a.rel_right, nrel = left + right + 1;
-  const bf16* Qb = (const bf16*)a.q + h * HD;
-  const bf16* Kb = (const bf16*)a.k + h * HD;
-  const bf16* Vb = (const bf16*)a.v + h * HD;
-  const bf16* dOb = (const bf16*)a.dout + h * HD;
-  const int kb0 = tile * KB, k0w = kb0 + w * 32;
-  const int64_t rowbase = (int64_t)(b * H + h) * T;
-  const float c2 = a.scale * LOG2E;
-
-  bf16x8 kf[2][2], vf[2][2];
-  bool kmask[2];
-#pragma unroll
-  for (int gk = 0; gk < 2; ++gk) {
-    const int key = k0w + 16 * gk + li;
-    const bool kv = key < T;
-    kmask[gk] = kv && a.key_mask != nullptr && a.key_mask[bT + key] == 0;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      kf[gk][s] = kv ? *reinterpret_cast<const bf16x8*>(Kb + (int64_t)(bT + key) * a.ldk + 32 * s + 8 * g) : bf16x8{};
-      vf[gk][s] = kv ? *reinterpret_cast<const bf16x8*>(Vb + (int64_t)(bT + key) * a.ldv + 32 * s + 8 * g) : bf16x8{};
-    }
-  }
-  const bool any_masked = __ballot(kmask[0] || kmask[1]) != 0;
-  char* sE = sm + KV_E_OFF;
-  float* qet = reinterpret_cast<float*>(sm + KV_QE_OFF);
-  float* elo = reinterpret_cast<float*>(sm + KV_EDGE_OFF);
-  float* ehi = elo + 64;
-  stage_E(sE, (const bf16*)a.rel_E, nrel, NREL, tid);
-
-  const int nqt = (T + TQ - 1) / TQ;
-  // wave w stages Q pieces 2w,2w+1 and dO pieces 2w,2w+1; wave 0 the lse words, wave 1 delta
-  auto issue = [&](int qt) {
-    char* buf = sm + (qt & 1) * QD;
-    const int qb = qt * TQ;
-    glds_tile_piece(Qb, a.ldq, bT, qb, T, buf, 2 * w, lane);
-    glds_tile_piece(Qb, a.ldq, bT, qb, T, buf, 2 * w + 1, lane);
-    glds_tile_piece(dOb, a.lddo, bT, qb, T, buf + TILE, 2 * w, lane);
-    glds_tile_piece(dOb, a.lddo, bT, qb, T, buf + TILE, 2 * w + 1, lane);
-    if (w < 2) {   // wave-uniform base + 32-bit lane offset (saddr DMA; no 64-bit address to keep live)
-      const char* base = (const char*)(w == 0 ? a.lse : a.delta);
-      const uint32_t off = (uint32_t)(rowbase + min(qb + lane_now(), T - 1)) * 4u;
-      __builtin_amdgcn_global_load_lds((const void*)(base + off), (lds_void*)(buf + 2 * TILE + w * 256), 4, 0, 0);
-    }
-  };
-  issue(0);
-  if (nqt > 1) issue(1);
-  if (nqt > 1) {
-    if (w < 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();   // also publishes sE (plain stores)
-
-  f32x4 dk[2][4], dv[2][4];
-#pragma unroll
-  for (int gk = 0; gk < 2; ++gk)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      dk[gk][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dv[gk][i] = dk[gk][i];
-    }
-
-  for (int qt = 0; qt < nqt; ++qt) {
-    const char* tQ = sm + (qt & 1) * QD;
-    const char* tD = tQ + TILE;
-    const float* sL = reinterpret_cast<const float*>(tQ + 2 * TILE);   // lse[64] | delta[64]
-    const int qb = qt * TQ;
-    // Q·Eᵀ of this query tile: wave w builds rows 16w..16w+15
-    const bool blk_lo = (kb0 + KB - 1) - qb <= -left;
-    const bool blk_hi = kb0 - (qb + TQ - 1) >= right;
-    const bool blk_band = !(blk_lo || blk_hi);
-    if (!(STE_ABLATE & 1)) {
-      bf16x8 qfr[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) qfr[s] = frag_kc(tQ, 16 * w, s, lane);
-#pragma unroll
-      for (int jt = 0; jt < NREL / 16; ++jt) {
-        if (!blk_band && jt != 0 && jt != (nrel - 1) / 16) continue;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 2; ++s) acc = mfma16(frag_kc(sE, jt * 16, s, lane), qfr[s], acc);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = jt * 16 + 4 * g + r;
-          if (j < QEW) qet[(16 * w + li) * QEW + j] = acc[r];
-          if (j == 0) elo[16 * w + li] = acc[r] * c2;
-          if (j == nrel - 1) ehi[16 * w + li] = acc[r] * c2;
-        }
-      }
-    }
-    if (!(STE_ABLATE & 1)) __syncthreads();
-    // per-lane query vectors (queries 16n + 4g + r): -lse*log2e, delta, edge biases
-    f32x4 nl2[4], dlt[4], lsev[4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      lsev[n] = *reinterpret_cast<const f32x4*>(sL + 16 * n + 4 * g);
-      dlt[n] = *reinterpret_cast<const f32x4*>(sL + 64 + 16 * n + 4 * g);
-      nl2[n] = lsev[n] * -LOG2E;
-    }
-#pragma unroll
-    for (int gk = 0; gk < 2; ++gk) {
-      const int k0g = k0w + 16 * gk, mykey = k0g + li;
-      f32x4 sc[4], dp[4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        sc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[n] = sc[n];
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          if (STE_ABLATE & 8) continue;
-          sc[n] = mfma16(frag_kc(tQ, 16 * n, ss, lane), kf[gk][ss], sc[n]);
-          dp[n] = mfma16(frag_kc(tD, 16 * n, ss, lane), vf[gk][ss], dp[n]);
-        }
-      }
-      const bool all_lo = (k0g + 15) - qb <= -left;
-      const bool all_hi = k0g - (qb + TQ - 1) >= right;
-      if (all_lo || all_hi) {
-        const float* ev = all_lo ? elo : ehi;
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          const f32x4 eb = *reinterpret_cast<const f32x4*>(ev + 16 * n + 4 * g);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) sc[n][r] = (STE_ABLATE & 2) ? fmaf(sc[n][r], c2, eb[r] + nl2[n][r])
-                                                                  : __builtin_amdgcn_exp2f(fmaf(sc[n][r], c2, eb[r] + nl2[n][r]));
-        }
-      } else {
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int ql = 16 * n + 4 * g + r;
-            int d = mykey - (qb + ql);
-            d = med3i(d, -left, right);
-            sc[n][r] = __builtin_amdgcn_exp2f(fmaf(sc[n][r] + qet[ql * QEW + d + left], c2, nl2[n][r]));
-          }
-      }
-      if (any_masked && kmask[gk]) {
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) sc[n][r] = lsev[n][r] == -INFINITY ? 1.0f / T : 0.f;
-      }
-      if (qb + TQ > T) {  // last query tile: rows past T (staged as copies of row T-1) add nothing
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (qb + 16 * n + 4 * g + r >= T) sc[n][r] = 0.f;
-      }
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        dp[n] = sc[n] * (dp[n] - dlt[n]) * a.scale;   // dS * scale (for dK)
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const bf16x8 pv = pack_acc(sc[2 * u], sc[2 * u + 1]);
-        const bf16x8 pk = pack_acc(dp[2 * u], dp[2 * u + 1]);
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          if (STE_ABLATE & 4) continue;
-          dv[gk][dt] = mfma16(frag_tr(tD, dt * 16, u, lane), pv, dv[gk][dt]);
-          dk[gk][dt] = mfma16(frag_tr(tQ, dt * 16, u, lane), pk, dk[gk][dt]);
-        }
-        if (STE_ABLATE & 4) { dv[gk][0] += pv[0]; dk[gk][0] += pk[0]; }
-      }
-    }
-    if (qt + 1 < nqt) {
-      if (!(STE_ABLATE & 16)) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-      }
-      if (qt + 2 < nqt) issue(qt + 2);
-    }
-  }
-#pragma unroll
-  for (int gk = 0; gk < 2; ++gk) {
-    const int key = k0w + 16 * gk + li;
-    if (key < T) {
-      bf16* dK = (bf16*)a.dk + (int64_t)(bT + key) * a.lddk + h * HD;
-      bf16* dV = (bf16*)a.dv + (int64_t)(bT + key) * a.lddv + h * HD;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        store_bf16x4(dK + 16 * dt + 4 * g, dk[gk][dt]);
-        store_bf16x4(dV + 16 * dt + 4 * g, dv[gk][dt]);
-      }
-    }
-  }
-}
-
-// v3 of the dK/dV kernel: the same algorithm as v2 with each Q/dO fragment (row and transposed)
-// read from LDS once per 32-query half and used for both key groups (v2 re-read them per key
-// group: LDS traffic equal to the MFMA time), transposed reads through the asm form (the
-// builtin makes hipcc drain the in-flight tile DMA at every read).
+// Each Q/dO fragment (row and transposed) is read from LDS once per 32-query half and used for
+// both key groups (reading them per key group made the LDS traffic equal to the MFMA time);
+// transposed reads go through the asm form (the builtin makes hipcc drain the in-flight tile DMA
+// at every read).
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_rel3_kernel(ste_attn_args a) {
   using namespace rel2;
   extern __shared__ __attribute__((aligned(16))) char sm[];
@@ -2408,76 +1931,26 @@ constexpr int FWD_LDS = 4 * TILE + NREL * 128 + 4 * 16 * NREL * 4 + 2 * 64 * 4;
 constexpr int DQ_LDS = 2 * TILE + 96 * 128 + 4 * 16 * NREL * 4 + 4 * 16 * 96 * 4 + 64 * 4;
 constexpr int DKV_LDS = 4 * TILE + NREL * 128 + 64 * NREL * 4 + 2 * 128 * 4;
 
-template <template <bool, bool> class K>
-struct Dispatch;
-
-// STE_ATTN_DE=2: the small-T VALU dE kernel instead of the MFMA one at every T (A/B runs)
+// A/B switches, read only by -DSTE_AB builds (libste_ab.so, _build.py --ab); the shipped library
+// reads no environment and always takes the defaults below.
+//   STE_ATTN_DE=2   the small-T VALU dE kernel at every T
+//   STE_ATTN_FWD=2  the rel2 forward instead of rel4
+//   STE_ATTN_PLO=1  the rel4 forward's hi/lo P split (exact-p row sums) when o_lo is requested
+bool ab_is(const char* name, char v) {
+  const char* e = STE_AB_ENV(name);
+  return e && e[0] == v;
+}
 bool rel_de3() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("STE_ATTN_DE");
-    v = (e && e[0] == '2') ? 0 : 1;
-  }
-  return v == 1;
+  static const bool v = !ab_is("STE_ATTN_DE", '2');
+  return v;
 }
-// STE_ATTN_V1=1: the original relative-key kernels (A/B comparisons in one process)
-bool rel_v2() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("STE_ATTN_V1");
-    v = (e && e[0] == '1') ? 0 : 1;
-  }
-  return v == 1;
-}
-
-// STE_ATTN_FWD=2: the v2 relative-key forward instead of v4 (A/B comparisons in one process)
 bool rel_fwd_v4() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("STE_ATTN_FWD");   // "2": the rel2 forward
-    v = (e && e[0] == '2') ? 0 : 1;
-  }
-  return v == 1;
+  static const bool v = !ab_is("STE_ATTN_FWD", '2');
+  return v;
 }
-
-// STE_ATTN_PLO=0: the forward's PV product on bf16 P only (o_lo still written), see rel4
 bool rel_fwd_plo() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("STE_ATTN_PLO");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
-// STE_ATTN_PV16=1: the forward's PV product in fp16 on fp16-rounded P (rel4 F16)
-bool rel_fwd_pv16() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("STE_ATTN_PV16");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v == 1;
-}
-
-// STE_ATTN_DQ=2: the v2 relative-key dQ kernel (A/B comparisons in one process)
-bool rel_dq_v3() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("STE_ATTN_DQ");
-    v = (e && e[0] == '2') ? 0 : 1;
-  }
-  return v == 1;
-}
-
-// STE_ATTN_BWD=2: the v2 relative-key dK/dV kernel (A/B comparisons in one process)
-bool rel_bwd_v3() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("STE_ATTN_BWD");
-    v = (e && e[0] == '2') ? 0 : 1;
-  }
-  return v == 1;
+  static const bool v = ab_is("STE_ATTN_PLO", '1');
+  return v;
 }
 
 int check(const ste_attn_args* a) {
@@ -2512,15 +1985,12 @@ extern "C" int ste_attention_fwd(const ste_attn_args* a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)(((a->T + TQ - 1) / TQ) * a->H * a->B));
   const bool rel = a->rel_E != nullptr, drop = a->drop_p > 0.f;
-  if (rel && !drop && rel_v2()) {
+  if (rel && !drop) {
     dim3 g2((unsigned)(((a->T + rel2::BQ - 1) / rel2::BQ) * a->H * a->B));
-    // the hi/lo split of P only when a backward follows (o_lo given); a forward-only call (no_grad
-    // evaluation) saves the second PV product
     if (rel_fwd_v4() && a->rel_left + a->rel_right + 1 <= rel4::max_nrel() && a->T <= rel4::MAXT * TK) {
-      if (a->o_lo && rel_fwd_pv16()) hipLaunchKernelGGL((attn_fwd_rel4_kernel<true, false, true>), g2, dim3(NT), rel4::FWD_LDS, s, *a);
-      else if (a->o_lo && !rel_fwd_plo()) hipLaunchKernelGGL((attn_fwd_rel4_kernel<true, false>), g2, dim3(NT), rel4::FWD_LDS, s, *a);
-      else if (a->o_lo) hipLaunchKernelGGL(attn_fwd_rel4_kernel<true>, g2, dim3(NT), rel4::FWD_LDS, s, *a);
-      else hipLaunchKernelGGL(attn_fwd_rel4_kernel<false>, g2, dim3(NT), rel4::FWD_LDS, s, *a);
+      if (a->o_lo && rel_fwd_plo()) hipLaunchKernelGGL((attn_fwd_rel4_kernel<true, true>), g2, dim3(NT), rel4::FWD_LDS, s, *a);
+      else if (a->o_lo) hipLaunchKernelGGL((attn_fwd_rel4_kernel<true, false>), g2, dim3(NT), rel4::FWD_LDS, s, *a);
+      else hipLaunchKernelGGL((attn_fwd_rel4_kernel<false, false>), g2, dim3(NT), rel4::FWD_LDS, s, *a);
     } else if (a->o_lo)
       hipLaunchKernelGGL(attn_fwd_rel2_kernel<true>, g2, dim3(NT), rel2::FWD_LDS, s, *a);
     else
@@ -2542,18 +2012,13 @@ extern "C" int ste_attention_bwd(const ste_attn_args* a, void* stream) {
   if ((a->lddo & 7) || (a->lddq & 3) || (a->lddk & 3) || (a->lddv & 3)) return STE_ERR_SHAPE;
   if (a->dE && (!a->gwork || !a->rel_E)) return STE_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  if (a->rel_E && a->drop_p == 0.f && rel_v2()) {
-    if (rel_dq_v3() && a->rel_left + a->rel_right + 1 < rel2::GT3) {   // bin GT3-1 is the spare slot
-      dim3 gq((unsigned)(((a->T + rel2::DQ3_Q - 1) / rel2::DQ3_Q) * a->H * a->B));
-      hipLaunchKernelGGL(attn_bwd_dq_rel3_kernel, gq, dim3(NT), rel2::DQ3_LDS, s, *a);
-    } else {
-      dim3 gq((unsigned)(((a->T + rel2::DQ_Q - 1) / rel2::DQ_Q) * a->H * a->B));
-      hipLaunchKernelGGL(attn_bwd_dq_rel2_kernel, gq, dim3(NT), rel2::DQ_LDS, s, *a);
-    }
+  if (a->rel_E && a->drop_p == 0.f) {
+    static_assert(NREL < rel2::GT3, "bin GT3-1 is the dQ kernel's spare slot");
+    dim3 gq((unsigned)(((a->T + rel2::DQ3_Q - 1) / rel2::DQ3_Q) * a->H * a->B));
+    hipLaunchKernelGGL(attn_bwd_dq_rel3_kernel, gq, dim3(NT), rel2::DQ3_LDS, s, *a);
     STE_CHECK_LAUNCH();
     dim3 gk((unsigned)(((a->T + rel2::KB - 1) / rel2::KB) * a->H * a->B));
-    if (rel_bwd_v3()) hipLaunchKernelGGL(attn_bwd_dkv_rel3_kernel, gk, dim3(NT), rel2::DKV3_LDS, s, *a);
-    else hipLaunchKernelGGL(attn_bwd_dkv_rel2_kernel, gk, dim3(NT), rel2::DKV_LDS, s, *a);
+    hipLaunchKernelGGL(attn_bwd_dkv_rel3_kernel, gk, dim3(NT), rel2::DKV3_LDS, s, *a);
     STE_CHECK_LAUNCH();
     if (a->dE) return launch_dE(a, s);
     return 0;

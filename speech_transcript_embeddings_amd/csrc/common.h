@@ -170,4 +170,14 @@ STE_DEV s16x4 ds_read_tr16_asm(const char* p) {
   return r;
 }
 
+// A/B switches.  The shipped library reads no environment: STE_AB_ENV(name) is a null pointer
+// there, so every switch takes its default.  Builds with -DSTE_AB (_build.py --ab -> libste_ab.so,
+// for same-box A/B runs only) read the named variable.
+#ifdef STE_AB
+#include <cstdlib>
+#define STE_AB_ENV(name) getenv(name)
+#else
+#define STE_AB_ENV(name) ((const char*)nullptr)
+#endif
+
 #define STE_CHECK_LAUNCH() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)

@@ -1533,7 +1533,7 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(ste_gemm_args p, const 
 int few_split(const ste_gemm_args& a) {
   static int on = -1;
   if (on < 0) {
-    const char* e = getenv("STE_GEMM_FEW_SPLIT");
+    const char* e = STE_AB_ENV("STE_GEMM_FEW_SPLIT");
     on = (e && e[0] == '0') ? 0 : 1;
   }
   if (!on || !a.a_kc || !a.b_kc || !a.ws || a.batch != 1 || a.colsum) return 0;
@@ -1551,7 +1551,7 @@ int few_split(const ste_gemm_args& a) {
 bool batched_dw_ok(const ste_gemm_args& a) {
   static int on = -1;   // STE_GEMM_BATCHED_DW=0: the small kernel (A/B)
   if (on < 0) {
-    const char* e = getenv("STE_GEMM_BATCHED_DW");
+    const char* e = STE_AB_ENV("STE_GEMM_BATCHED_DW");
     on = (e && e[0] == '0') ? 0 : 1;
   }
   if (!on || a.a_kc || a.b_kc || a.batch < 2) return false;
@@ -1616,7 +1616,7 @@ bool big_ok(const ste_gemm_args& a) {
   const long tiles = (long)((a.M + 255) / 256) * ((a.N + 255) / 256) * a.batch;
   static int min_tiles = -1;   // STE_GEMM_MIN_TILES: A/B of the small-kernel threshold
   if (min_tiles < 0) {
-    const char* e = getenv("STE_GEMM_MIN_TILES");
+    const char* e = STE_AB_ENV("STE_GEMM_MIN_TILES");
     min_tiles = e ? atoi(e) : 240;
   }
   return tiles >= min_tiles;
@@ -1625,7 +1625,7 @@ bool big_ok(const ste_gemm_args& a) {
 }  // namespace
 
 static int env_flag(const char* name) {
-  const char* e = getenv(name);
+  const char* e = STE_AB_ENV(name);
   return (e && e[0] == '1') ? 1 : 0;
 }
 // STE_GEMM_SMALL_ONLY=1: every shape on the 128x128 kernel; STE_GEMM_2PH=1: the 2-buffer
@@ -1977,7 +1977,7 @@ namespace {
 bool mx8_8ph_on() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("STE_MX8_8PH");
+    const char* e = STE_AB_ENV("STE_MX8_8PH");
     v = (e && e[0] == '0') ? 0 : 1;
   }
   return v == 1;

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(NT) void ln_fwd_pair_kernel(ste_ln_fwd_args a, ste_
 bool ln_fwd_pair_lean() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("STE_LN_FWD_PAIR");
+    const char* e = STE_AB_ENV("STE_LN_FWD_PAIR");
     v = (e && e[0] == 'p') ? 0 : 1;
   }
   return v == 1;

@@ -19,7 +19,6 @@ store.py (beta=1 accumulation), so micro-batch accumulation needs no extra pass.
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 
@@ -61,18 +60,18 @@ class Engine:
         # the text encoder (forward and backward) runs on a second HIP stream, concurrently with
         # the audio encoder: its GEMMs are too small to fill 256 CUs (8,192 rows) and overlap the
         # audio side's bandwidth-bound kernels.  STE_TEXT_STREAM=0: one stream (A/B runs).
-        self.overlap = os.environ.get("STE_TEXT_STREAM", "1") != "0"
+        self.overlap = _lib.ab_env("STE_TEXT_STREAM", "1") != "0"
         # layerdrop draws (tf:…wav2vec2_bert…:519-522): the global torch RNG unless a trainer sets a
         # generator (TrainStep broadcasts one seed so every data-parallel rank drops the same layers)
         self.layerdrop_gen = None
         # a Conformer layer's final LN and the next layer's FFN1 LN as one fused pass (forward and
         # backward, ste_layernorm_*_pair); STE_LN_PAIR=0: separate launches (A/B runs)
-        self.ln_pair = os.environ.get("STE_LN_PAIR", "1") != "0"
+        self.ln_pair = _lib.ab_env("STE_LN_PAIR", "1") != "0"
         # the text encoder's forward to ~fp32 accuracy (split-bf16 GEMMs, fp32 attention): the loss
         # gradient differences the positive and corrupted transcripts' embeddings, so their bf16
         # forward rounding reappeared in every gradient downstream.  STE_TEXT_PRECISE=0:
         # the plain bf16 forward (A/B runs only)
-        self.precise_text = os.environ.get("STE_TEXT_PRECISE", "1") != "0"
+        self.precise_text = _lib.ab_env("STE_TEXT_PRECISE", "1") != "0"
 
     @property
     def fp8(self):

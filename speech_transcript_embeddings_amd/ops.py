@@ -29,9 +29,9 @@ def _ld(t: torch.Tensor) -> int:
 
 
 # True: column / table-row reductions through the library's fp32 atomics (its workspace-free path;
-# A/B runs and tests; STE_ATOMIC_SUMS=1 sets it for a whole run).  Default: ordered partial sums,
+# A/B runs and tests; STE_ATOMIC_SUMS=1 sets it for a whole run under the A/B build).  Default: ordered partial sums,
 # run-to-run deterministic gradients.
-ATOMIC_SUMS = os.environ.get("STE_ATOMIC_SUMS") == "1"
+ATOMIC_SUMS = _lib.ab_env("STE_ATOMIC_SUMS", "0") == "1"
 _RED_WS = {}
 
 
@@ -286,26 +286,29 @@ def layernorm_fwd_pair(first: dict, second: dict):
     ((mean1, rstd1), (mean2, rstd2))."""
     a, m1, r1, nb1 = _ln_fwd_struct(**first)
     b, m2, r2, nb2 = _ln_fwd_struct(None, rows=a.rows, cols=a.cols, **second)
-    _traced("layernorm_fwd", nb1 + nb2, lambda: call("ste_layernorm_fwd_pair", C.byref(a), C.byref(b), _s()))
+    _traced("layernorm_fwd_pair", nb1 + nb2, lambda: call("ste_layernorm_fwd_pair", C.byref(a), C.byref(b), _s()))
     return (m1, r1), (m2, r2)
 
 
 # True: LayerNorm column sums through fp32 atomics (the library's workspace-free path; A/B and tests;
-# STE_LN_ATOMIC=1 sets it for a whole run)
-LN_ATOMIC_COLSUMS = os.environ.get("STE_LN_ATOMIC") == "1"
+# STE_LN_ATOMIC=1 sets it for a whole run under the A/B build)
+LN_ATOMIC_COLSUMS = _lib.ab_env("STE_LN_ATOMIC", "0") == "1"
 
 
 _LN_WS_BUF = {}
 
 
 def _ln_ws(dev, rows, cols, slot):
-    """Column-partial workspace of a LayerNorm backward, cached per (stream, shape, slot): the
-    launches of one stream run in order, so consecutive backwards reuse one buffer (a pair
-    kernel's two LayerNorms take slots 0 and 1); concurrent streams get their own."""
-    key = (torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0, rows, cols, slot)
+    """Column-partial workspace of a LayerNorm backward, one per (stream, slot), grown on demand:
+    the launches of one stream run in order, so consecutive backwards reuse one buffer (a pair
+    kernel's two LayerNorms take slots 0 and 1); concurrent streams get their own.  Its size
+    (ste_layernorm_bwd_ws_floats) stops growing once rows reach the kernel's block count, so
+    batches padded to different lengths share one buffer instead of one each."""
+    key = (torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0, slot)
+    need = _ln_ws_floats(rows, cols)
     w = _LN_WS_BUF.get(key)
-    if w is None:
-        w = _LN_WS_BUF[key] = torch.empty(_ln_ws_floats(rows, cols), device=dev, dtype=F32)
+    if w is None or w.numel() < need:
+        w = _LN_WS_BUF[key] = torch.empty(need, device=dev, dtype=F32)
     return w
 
 
@@ -359,7 +362,7 @@ def layernorm_bwd_pair(first: dict, second: dict):
     no dy; second's dx output is optional).  Keyword sets as layernorm_bwd."""
     a, nb1, _wa = _ln_bwd_struct(None, **first, _slot=1)
     b, nb2, _wb = _ln_bwd_struct(**second)
-    _traced("layernorm_bwd", nb1 + nb2, lambda: call("ste_layernorm_bwd_pair", C.byref(a), C.byref(b), _s()))
+    _traced("layernorm_bwd_pair", nb1 + nb2, lambda: call("ste_layernorm_bwd_pair", C.byref(a), C.byref(b), _s()))
 
 
 # -------------------------------------------------------------- attention
@@ -670,12 +673,17 @@ def sumsq(g, acc, part=None):
     if ATOMIC_SUMS:
         part = None
     assert part is None or (part.dtype == torch.float64 and part.numel() >= SUMSQ_PARTS)
-    call("ste_sumsq", ptr(g), g.numel(), ptr(acc), ptr(part), _s())
+    # algorithmic bytes: one fp32 read per gradient element (SURVEY §8d clip_grad_norm_)
+    _traced("sumsq", 4 * g.numel(), lambda: call("ste_sumsq", ptr(g), g.numel(), ptr(acc), ptr(part), _s()))
 
 
 def adamw(p, g, m, v, p_bf16, *, lr, beta1, beta2, eps, wd, step, sumsq_acc=None, max_norm=1.0):
-    call("ste_adamw", ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), p.numel(), float(lr), float(beta1), float(beta2),
-         float(eps), float(wd), int(step), ptr(sumsq_acc), float(max_norm), _s())
+    # algorithmic bytes (28 B/param): read p, g, m, v and write p, m, v in fp32, plus the
+    # bf16 MFMA shadow of p when one is refreshed (2 B)
+    nbytes = p.numel() * (28 + (2 if p_bf16 is not None else 0))
+    _traced("adamw", nbytes, lambda: call("ste_adamw", ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), p.numel(), float(lr),
+                                          float(beta1), float(beta2), float(eps), float(wd), int(step), ptr(sumsq_acc),
+                                          float(max_norm), _s()))
 
 
 def cast_bf16(x, y):

@@ -205,10 +205,12 @@ class GradSync:
     different token counts (a short last batch, length-bucketed padding).  The capacity is fixed
     per run, never agreed per step: word_capacity = the most token ids one optimizer step can
     carry (TrainStep: 2 x micro-batch x max_text_length x accumulation; the reference pads every
-    transcript to max_text_length, ref :838-851), or, when the caller cannot say, agreed once by
-    ensure_capacity() (a MAX all-reduce on the first step, before its kernels are queued).  A step
-    with more ids than the capacity raises.  So a step's backward holds no collective of its own
-    and no host wait.
+    transcript to max_text_length, ref :838-851); a step with more ids than a configured capacity
+    raises on every rank alike only if every rank's count exceeds it, so the configured value must
+    be a true bound.  When the caller cannot say, the capacity is agreed on EVERY optimizer step by
+    ensure_capacity() (a MAX all-reduce that TrainStep makes before the step's kernels are queued),
+    so ranks with different token counts (length-bucketed padding) always take the same path.  A
+    step's backward therefore holds no collective of its own and no host wait.
     `finish()` waits for every collective (on the current stream) before clip + AdamW.
     """
 
@@ -226,6 +228,8 @@ class GradSync:
         self.works = []
         self.sparse = None
         self.capacity = None if word_capacity is None else int(word_capacity)
+        self.configured = word_capacity is not None
+        self._agreed = False   # unconfigured: the capacity was agreed for the current step
         grad_slots = [sl for sl in store.slots.values() if sl.segment in ("enc", "head")]
 
         ordered = sorted(grad_slots, key=lambda x: x.offset)
@@ -290,19 +294,20 @@ class GradSync:
                 self.works.append(dist.all_reduce(t, op=op, async_op=True))
 
     def ensure_capacity(self, n_ids: int) -> int:
-        """The run's word-table exchange capacity: the configured one, or (first call without one)
-        the MAX of every rank's n_ids, agreed once with a blocking all-reduce — called before a
-        step's kernels are queued, so it never stalls a backward.  Raises when a step carries more
-        ids than the capacity (every rank must use the same capacity)."""
+        """The step's word-table exchange capacity.  Configured: checked (raises when a step
+        carries more ids).  Not configured: the MAX of every rank's n_ids, agreed with a blocking
+        all-reduce on every call — TrainStep makes that call once per optimizer step, before the
+        step's kernels are queued, so it never stalls a backward and never goes stale."""
         if not self.active() or self.words is None:
             return int(n_ids)
-        if self.capacity is None:
+        if not self.configured:
             dev = self.store.device
             t = torch.tensor([int(n_ids)], dtype=torch.int64,
                              device=dev if dist.get_backend() == "nccl" and dev.type == "cuda" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             self.capacity = int(t.item())
-        if n_ids > self.capacity:
+            self._agreed = True
+        elif n_ids > self.capacity:
             raise RuntimeError(f"{n_ids} token ids in one step exceed the word-table exchange capacity "
                                f"{self.capacity} (TrainStep(micro_batch=, max_text_length=) sets it)")
         return self.capacity
@@ -338,7 +343,11 @@ class GradSync:
             return
         self._reduce(self.ranges[stage])
         if stage == "text" and self.words is not None:
-            n = self.ensure_capacity(ids.numel() if ids is not None else 0)
+            if self.configured or not self._agreed:
+                n = self.ensure_capacity(ids.numel() if ids is not None else 0)
+            else:   # agreed for this step before its kernels were queued
+                n = self.capacity
+            self._agreed = False
             if ids is not None and self.sparse_pays(n):   # n, hence the choice, equal on every rank
                 self._sparse_words(ids, n)
             else:
@@ -509,7 +518,7 @@ class TrainStep:
         Data parallel: rank 0's layerdrop seed is broadcast so every rank drops the same Conformer
         layers (tf:…wav2vec2_bert…:519-522 draws one number per layer per batch).  micro_batch and
         max_text_length (the reference pads transcripts to it, ref :838-851) fix the word-table
-        exchange capacity (GradSync) up front; without them it is agreed once, on the first step."""
+        exchange capacity (GradSync) up front; without them it is agreed on every optimizer step."""
         self.model = model
         self.acc = max(1, int(accumulation_steps))
         self._micro = 0
@@ -573,7 +582,7 @@ class TrainStep:
         st.sync_shadow()
         eng = m.engine
         if self._micro + 1 == self.acc:   # the window's last micro-batch: check the word-table exchange
-            # capacity (agreed once on the first step if not configured) before any kernel is queued
+            # capacity (agreed across ranks here if not configured) before any kernel is queued
             n_ids = batch["input_ids_pos"].numel() + batch["input_ids_neg"].numel()
             self.gradsync.ensure_capacity(n_ids + sum(int(t.numel()) for t in (self._ids if self._micro else [])))
         tf_p, tf_n, af, align, ctx = eng.forward(batch, True)

@@ -54,3 +54,19 @@ def test_layernorm_reductions_without_bpermute(tmp_path):
     text = _disasm(objs[0], tmp_path)
     assert "ds_bpermute" not in text
     assert "row_mirror" in text and "permlane32_swap" in text
+
+
+def test_shipped_library_reads_no_environment():
+    """no switch in the shipped libste.so may change numerics from the environment.
+    The A/B switches compile to their defaults unless -DSTE_AB (libste_ab.so, _build.py --ab), so
+    the default build imports no getenv and carries none of the switch names."""
+    lib = ROOT / "speech_transcript_embeddings_amd" / "libste.so"
+    if not lib.exists() or shutil.which("nm") is None:
+        pytest.skip("libste.so or binutils not present")
+    und = subprocess.run(["nm", "-D", "--undefined-only", str(lib)], check=True, capture_output=True,
+                         text=True).stdout
+    assert not re.search(r"\b(secure_)?getenv\b", und), "libste.so imports getenv"
+    data = lib.read_bytes()
+    names = set(re.findall(rb"STE_[A-Z0-9_]{3,}", data))
+    # the only STE_ strings allowed are none at all: every switch name lives in #ifdef STE_AB code
+    assert not names, f"switch names in the shipped library: {sorted(names)}"

@@ -85,7 +85,7 @@ def _sync_case(rank, world):
     """Dense blocks + sparse word table; returns (max err vs the all-rank average, untouched tail ok,
     every collective async).  The ranks hold DIFFERENT token counts (the sparse
     capacity and the sparse-vs-dense choice must still agree): first with the capacity agreed
-    once by ensure_capacity (MAX over ranks), then with a configured one."""
+    for the step by ensure_capacity (MAX over ranks), then with a configured one."""
     from speech_transcript_embeddings_amd import ops
     from speech_transcript_embeddings_amd.train import GradSync
     ops.rows_extract, ops.rows_accumulate = rows_extract_ref, rows_accumulate_ref
@@ -116,7 +116,7 @@ def _sync_case(rank, world):
     assert all(gs.ranges[k] for k in GradSync.STAGES), gs.ranges   # every stage has a non-empty block
     gs.bucket = 29  # several buckets + ragged ones
     g0 = g.clone()
-    assert gs.ensure_capacity(ids.numel()) == 10 + 2 * (world - 1)   # agreed once: the MAX over ranks
+    assert gs.ensure_capacity(ids.numel()) == 10 + 2 * (world - 1)   # agreed for the step: the MAX over ranks
     with _Recorder() as rec:
         for stage in GradSync.STAGES:
             gs.stage_done(stage, ids)
@@ -515,7 +515,7 @@ def _nosync_worker(rank, world, port, q):
         _head_stand_ins()
         B, L = 3, 4
         out = {}
-        for mode in ("configured", "agreed_once"):
+        for mode in ("configured", "agreed_per_step"):
             for acc in (1, 2):
                 model = _fake_model(B, L)
                 kw = dict(micro_batch=B, max_text_length=L) if mode == "configured" else {}
@@ -529,10 +529,11 @@ def _nosync_worker(rank, world, port, q):
                              "input_ids_neg": neg, "attention_mask_neg": torch.ones(B, L, dtype=torch.long)}
                     with _SyncSpy() as spy:
                         step.step_batch(batch)
-                    # the unconfigured capacity is agreed once, on the first optimizer step's
-                    # final micro-batch (before any of its work is queued); nothing after that
-                    first = mode == "agreed_once" and it == acc - 1
-                    if not first:
+                    # the unconfigured capacity is agreed on every optimizer step's final
+                    # micro-batch, before any of its work is queued (a capacity agreed
+                    # once goes stale when a later step carries more ids); nothing else blocks
+                    agree = mode == "agreed_per_step" and it % acc == acc - 1
+                    if not agree:
                         hits += spy.blocking()
                 out[f"{mode}/acc{acc}"] = hits
                 out[f"{mode}/acc{acc}/steps"] = step.opt.t
@@ -562,7 +563,7 @@ def test_step_batch_no_host_sync_gloo_world2():
         assert p.exitcode == 0
     for r, out in res.items():
         assert "error" not in out, out.get("error")
-        for mode in ("configured", "agreed_once"):
+        for mode in ("configured", "agreed_per_step"):
             for acc in (1, 2):
                 k = f"{mode}/acc{acc}"
                 assert out[k] == [], (r, k, out[k])      # no host read, no sync, no blocking collective
