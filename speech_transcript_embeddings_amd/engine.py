@@ -1033,9 +1033,10 @@ class Engine:
 
     def backward(self, ctx, d_tp, d_tn, d_af, d_align, stage_done=None):
         """Backward of the whole step.  stage_done(name) is called once the gradients of a
-        parameter block are final (GradSync.STAGES order: "heads", "audio_layers", "audio",
-        "text"), so a data-parallel
-        caller can start their collective while the rest of the backward runs."""
+        parameter block are final, so a data-parallel caller can start their collective while the
+        rest of the backward runs: "heads", then (text on its side stream) "text" with the current
+        stream set to that side stream, "audio_layers", "audio"; on one stream the GradSync.STAGES
+        order "heads", "audio_layers", "audio", "text"."""
         nb = ctx["t_nb"]
         d_tf = self._e(nb, self.m.projection_dim)
         _copy_f32(d_tp, d_tf[: nb // 2])
@@ -1052,12 +1053,17 @@ class Engine:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 self.text_backward(dth, ctx)
+                if stage_done:
+                    # the text block is final once the side stream has run its backward: its
+                    # collectives (dense all-reduce, word-table row exchange) are queued behind it on
+                    # the side stream and overlap the audio backward's frozen layers, instead of
+                    # waiting for the join
+                    stage_done("text")
             self.audio_backward(dah, ctx, (lambda: stage_done("audio_layers")) if stage_done else None)
             main.wait_stream(side)
             del dah
             if stage_done:
                 stage_done("audio")
-                stage_done("text")
         else:
             self.audio_backward(dah, ctx, (lambda: stage_done("audio_layers")) if stage_done else None)
             del dah

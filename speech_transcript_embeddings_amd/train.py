@@ -191,7 +191,10 @@ class GradSync:
                       them (the frozen layers' input-gradient passes still run behind it);
       "audio"         the rest of the audio encoder (feature projection, SpecAugment embedding),
                       at the end of the audio backward;
-      "text"          the text encoder (its backward runs on the side stream; joined at the end).
+      "text"          the text encoder, as soon as its backward has run on the side stream: the
+                      call is made with that stream current, so this block's collectives queue
+                      behind the text backward alone and overlap the audio backward (on one
+                      stream: after the audio backward).
     Each block's dense ranges are all-reduced asynchronously (RCCL ring over xGMI, <= bucket_mb
     per call, average) while the remaining backward kernels run.  The 250,002 x 768
     word-embedding gradient is exchanged row-sparse: each rank extracts the rows of its own token
@@ -358,9 +361,13 @@ class GradSync:
             w.wait()
         self.works = []
         if self.sparse is not None:
-            g2, all_ids, all_rows, cap, ws, waits, _keep = self.sparse
+            g2, all_ids, all_rows, cap, ws, waits, keep = self.sparse
             for w in waits:
                 w.wait()
+            if all_ids.is_cuda:   # made on the stream that ran the text backward, read here
+                cur = torch.cuda.current_stream(all_ids.device)
+                for t in (all_ids, all_rows, *keep):
+                    t.record_stream(cur)
             for r in range(ws):  # rank order: identical summation on every rank
                 ops.rows_accumulate(g2, all_ids[r * cap:(r + 1) * cap], all_rows[r * cap:(r + 1) * cap], 1.0 / ws)
             self.sparse = None
