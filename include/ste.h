@@ -264,6 +264,13 @@ int ste_attention_fwd(const ste_attn_args* a, void* stream);
  * conventions of ste_attention_fwd, so ste_attention_bwd runs on bf16 copies of q/k/v. */
 int ste_attention_fwd_f32(const ste_attn_args* a, float* o32, int64_t ldo32, void* stream);
 int ste_attention_bwd(const ste_attn_args* a, void* stream);
+/* fp32 backward of ste_attention_fwd_f32 (the precise text backward; replaces the autograd of
+ * tf:…xlm_roberta…:186-250 as trainer_unfreeze.py:1093 `loss.backward()` runs it): q/k/v and dout fp32,
+ * o / o_lo the forward's bf16 hi / lo halves of O (delta = dout·(o + o_lo)), lse as saved, the
+ * forward's key_mask / drop_p / seed / zero_masked_rows; writes dq / dk / dv fp32 (row strides
+ * lddq / lddk / lddv; head h at columns h*64..).  rel_E must be NULL; delta, dE, gwork unused.
+ * Run-to-run deterministic (no atomics). */
+int ste_attention_bwd_f32(const ste_attn_args* a, void* stream);
 
 /* ----------------------------------------------- Conformer conv module core --
  * GLU over channels then causal depthwise conv (left pad K-1), no bias.

@@ -137,6 +137,7 @@ _SIGS = {
     "ste_attention_fwd": (c_int, [C.POINTER(AttnArgs), c_void_p]),
     "ste_attention_bwd": (c_int, [C.POINTER(AttnArgs), c_void_p]),
     "ste_attention_fwd_f32": (c_int, [C.POINTER(AttnArgs), c_void_p, c_int64, c_void_p]),
+    "ste_attention_bwd_f32": (c_int, [C.POINTER(AttnArgs), c_void_p]),
     "ste_split_bf16": (c_int, [c_void_p, c_int64, c_int64, c_int, c_void_p, c_int, c_int, c_void_p]),
     "ste_glu_dwconv_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "ste_glu_dwconv_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

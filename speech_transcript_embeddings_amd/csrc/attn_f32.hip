@@ -6,10 +6,11 @@
 // (80 % shared tokens), so bf16 rounding of the text encoder's forward activations reappeared
 // as 1-2.5 % errors in every gradient downstream of the transcript embeddings.  The
 // text side is 3.4 % of the step's FLOPs and runs on the side stream, so its forward is
-// computed to fp32 accuracy (split-bf16 GEMMs + this kernel); its backward keeps the bf16
-// kernels, fed by the bf16 copies (q/k/v, O + O_lo) and the LSE this kernel saves in the same
-// convention as attention.hip (natural log, masked keys at the finfo.min score, dropout index
-// ((b·H + h)·T + q)·T + key), so ste_attention_bwd runs on them unchanged.
+// computed to fp32 accuracy (split-bf16 GEMMs + this kernel), and so is its backward
+// (attn_f32_bwd_kernel below: the loss-derived gradients of the clean and corrupted transcripts
+// cancel in every text weight and bias, tests/precision_probe_text.py).  The LSE is saved in the
+// convention of attention.hip (natural log, masked keys at the finfo.min score, dropout index
+// ((b·H + h)·T + q)·T + key), so ste_attention_bwd also runs on bf16 copies of its inputs.
 //
 // One block per (sample, head, 64-query tile), 4 waves x 16 query rows, keys in chunks of 64.
 // Register-blocked VALU fp32 with the softmax row lane-local: lane (r, g) = (l & 15, l >> 4)
@@ -146,6 +147,176 @@ __global__ __launch_bounds__(NT) void attn_f32_fwd_kernel(ste_attn_args a, float
   }
 }
 
+
+// ------------------------------------------------------------------------------- backward
+// fp32 backward of the kernel above: dV = Pdᵀ·dO, dS = P ∘ (m·dO·Vᵀ − δ), dQ = scale·dS·K,
+// dK = scale·dSᵀ·Q, with P recomputed from fp32 q / k and the saved LSE, m the dropout scale of
+// the forward's mask (the same counter-based hash and index), Pd = P·m, and δ = dO·O from the
+// forward's O hi + lo halves (~16 mantissa bits).  One block per (sample, head) walks the key
+// chunks of 64 (dK, dV of the chunk in registers, written once) and, inside, the query tiles of 64
+// (dQ of a tile summed over the chunks in order by the same threads: deterministic, no atomics).
+// 256 threads; thread (ty, tx) = (t >> 4, t & 15) owns query rows ty + 16i and keys tx + 16j of a
+// score tile, and rows ty + 16i x columns 4tx..4tx+3 of the dQ / dK / dV tiles.
+constexpr int BLD = HD + 4;   // fp32 row stride of the Q / dO / K / V images
+constexpr int SLD = KC + 1;   // row stride of the Pd / dS images
+
+template <bool DROP>
+__global__ __launch_bounds__(NT) void attn_f32_bwd_kernel(ste_attn_args a) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  float* sQ = smf;                       // [64][BLD]
+  float* sD = sQ + QT * BLD;             // dO
+  float* sK = sD + QT * BLD;
+  float* sV = sK + KC * BLD;
+  float* sP = sV + KC * BLD;             // Pd [q][key]
+  float* sS = sP + QT * SLD;             // dS [q][key]
+  float* sL = sS + QT * SLD;             // lse[64]
+  float* sDl = sL + QT;                  // delta[64]
+  float* sF = sDl + QT;                  // key flags[64]
+  const int T = a.T, H = a.H;
+  const int bh = blockIdx.x, h = bh % H, b = bh / H, bT = b * T;
+  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  const float* Qg = (const float*)a.q + h * HD;
+  const float* Kg = (const float*)a.k + h * HD;
+  const float* Vg = (const float*)a.v + h * HD;
+  const float* dOg = (const float*)a.dout + h * HD;
+  const bf16* Og = (const bf16*)a.o + h * HD;
+  const bf16* Olg = (const bf16*)a.o_lo + h * HD;
+  float* dQg = (float*)a.dq + h * HD;
+  float* dKg = (float*)a.dk + h * HD;
+  float* dVg = (float*)a.dv + h * HD;
+  const uint32_t thresh = (uint32_t)(a.drop_p * 4294967296.0);
+  const float inv_keep = DROP ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  const float inv_T = 1.0f / (float)T;
+  const int nkc = (T + KC - 1) / KC, nqt = (T + QT - 1) / QT;
+  // stage rows [r0, r0 + 64) of a [B*T, *] fp32 operand (head h) into an image; rows >= T are 0
+  auto stage = [&](float* img, const float* src, int64_t ld, int r0) {
+    for (int i = tid; i < 64 * HD / 4; i += NT) {
+      const int r = i >> 4, c = (i & 15) * 4;
+      *reinterpret_cast<f32x4*>(img + r * BLD + c) =
+          r0 + r < T ? *reinterpret_cast<const f32x4*>(src + (int64_t)(bT + r0 + r) * ld + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  for (int kc = 0; kc < nkc; ++kc) {
+    const int k0 = kc * KC;
+    __syncthreads();   // the previous chunk's images are consumed
+    stage(sK, Kg, a.ldk, k0);
+    stage(sV, Vg, a.ldv, k0);
+    if (tid < KC) sF[tid] = key_flag32(a.key_mask, bT, k0 + tid, T);
+    f32x4 dk[4], dv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int qt = 0; qt < nqt; ++qt) {
+      const int q0 = qt * QT;
+      __syncthreads();   // the previous tile's Q / dO / Pd / dS images are consumed
+      stage(sQ, Qg, a.ldq, q0);
+      stage(sD, dOg, a.lddo, q0);
+      // delta = dO·(O_hi + O_lo) per query row: 16 lanes per row, 4 columns each, DPP-free shuffles
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = ty + 16 * i, q = q0 + r;
+        float part = 0.f;
+        if (q < T) {
+          const int64_t row = bT + q;
+          const f32x4 dov = *reinterpret_cast<const f32x4*>(dOg + row * a.lddo + 4 * tx);
+          const f32x4 oh = load_bf16x4(Og + row * a.ldo + 4 * tx);
+          const f32x4 ol = load_bf16x4(Olg + row * a.ldolo + 4 * tx);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) part = fmaf(dov[e], oh[e] + ol[e], part);
+        }
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) part += __shfl_xor(part, o, 16);
+        if (tx == 0) {
+          sDl[r] = part;
+          sL[r] = q < T ? a.lse[(int64_t)bh * T + q] : INFINITY;   // rows past T: p = 0
+        }
+      }
+      __syncthreads();
+      // scores and dP for rows ty + 16i, keys tx + 16j
+      float sc[4][4], dp[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sc[i][j] = dp[i][j] = 0.f;
+#pragma unroll 4
+      for (int d = 0; d < HD; d += 4) {
+        f32x4 qv[4], dov[4], kv[4], vv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          qv[i] = *reinterpret_cast<const f32x4*>(sQ + (ty + 16 * i) * BLD + d);
+          dov[i] = *reinterpret_cast<const f32x4*>(sD + (ty + 16 * i) * BLD + d);
+          kv[i] = *reinterpret_cast<const f32x4*>(sK + (tx + 16 * i) * BLD + d);
+          vv[i] = *reinterpret_cast<const f32x4*>(sV + (tx + 16 * i) * BLD + d);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              sc[i][j] = fmaf(qv[i][e], kv[j][e], sc[i][j]);
+              dp[i][j] = fmaf(dov[i][e], vv[j][e], dp[i][j]);
+            }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = ty + 16 * i, q = q0 + r;
+        const float lse = sL[r], dl = sDl[r];
+        const uint64_t drow = ((uint64_t)bh * T + (uint64_t)(q < T ? q : 0)) * (uint64_t)T;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int kl = tx + 16 * j, key = k0 + kl;
+          const float f = sF[kl];
+          float p;
+          if (lse == INFINITY || f < -0.5f) p = 0.f;                 // zero-weight row / key past T
+          else if (lse == -INFINITY) p = inv_T;                       // uniform row (every key masked)
+          else p = __expf((f > 0.5f ? sc[i][j] * a.scale : NEG_MASK) - lse);
+          const float m = DROP ? drop_scale(a.seed, drow + (uint64_t)key, thresh, inv_keep) : 1.0f;
+          sP[r * SLD + kl] = p * m;
+          sS[r * SLD + kl] = p * (m * dp[i][j] - dl);
+        }
+      }
+      __syncthreads();
+      // dV += Pdᵀ·dO, dK += dSᵀ·Q (keys ty + 16i, columns 4tx..), dQ tile = dS·K (rows ty + 16i)
+      f32x4 dq[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int nq = min(QT, T - q0), nk = min(KC, T - k0);
+      for (int r = 0; r < nq; ++r) {
+        const f32x4 dov = *reinterpret_cast<const f32x4*>(sD + r * BLD + 4 * tx);
+        const f32x4 qv = *reinterpret_cast<const f32x4*>(sQ + r * BLD + 4 * tx);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int kl = ty + 16 * i;
+          dv[i] += sP[r * SLD + kl] * dov;
+          dk[i] += sS[r * SLD + kl] * qv;
+        }
+      }
+      for (int kl = 0; kl < nk; ++kl) {
+        const f32x4 kv = *reinterpret_cast<const f32x4*>(sK + kl * BLD + 4 * tx);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dq[i] += sS[(ty + 16 * i) * SLD + kl] * kv;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = q0 + ty + 16 * i;
+        if (q >= T) continue;
+        float* dst = dQg + (int64_t)(bT + q) * a.lddq + 4 * tx;
+        f32x4 v = dq[i] * a.scale;
+        if (kc > 0) v += *reinterpret_cast<const f32x4*>(dst);   // this thread's own earlier chunk
+        *reinterpret_cast<f32x4*>(dst) = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = k0 + ty + 16 * i;
+      if (key >= T) continue;
+      *reinterpret_cast<f32x4*>(dKg + (int64_t)(bT + key) * a.lddk + 4 * tx) = dk[i] * a.scale;
+      *reinterpret_cast<f32x4*>(dVg + (int64_t)(bT + key) * a.lddv + 4 * tx) = dv[i];
+    }
+  }
+}
+constexpr int BWD_F32_LDS = (4 * 64 * BLD + 2 * 64 * SLD + 3 * 64) * 4;
+
 }  // namespace
 
 extern "C" int ste_attention_fwd_f32(const ste_attn_args* args, float* o32, int64_t ldo32, void* stream) {
@@ -162,6 +333,28 @@ extern "C" int ste_attention_fwd_f32(const ste_attn_args* args, float* o32, int6
     hipLaunchKernelGGL(attn_f32_fwd_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, a, o32, ldo32);
   else
     hipLaunchKernelGGL(attn_f32_fwd_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, a, o32, ldo32);
+  STE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ste_attention_bwd_f32(const ste_attn_args* args, void* stream) {
+  if (!args) return STE_ERR_ARG;
+  const ste_attn_args& a = *args;
+  if (!a.q || !a.k || !a.v || !a.lse || !a.dout || !a.o || !a.o_lo || !a.dq || !a.dk || !a.dv || a.rel_E)
+    return STE_ERR_ARG;
+  if (a.B <= 0 || a.T <= 0 || a.H <= 0) return STE_ERR_SHAPE;
+  if ((a.ldq & 3) || (a.ldk & 3) || (a.ldv & 3) || (a.lddo & 3) || (a.lddq & 3) || (a.lddk & 3) || (a.lddv & 3) ||
+      (a.ldo & 3) || (a.ldolo & 3) ||
+      (((uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v | (uintptr_t)a.dout | (uintptr_t)a.dq | (uintptr_t)a.dk |
+        (uintptr_t)a.dv) & 15) ||
+      (((uintptr_t)a.o | (uintptr_t)a.o_lo) & 7))
+    return STE_ERR_SHAPE;
+  if (a.drop_p < 0.f || a.drop_p >= 1.f) return STE_ERR_ARG;
+  const dim3 grid((unsigned)((int64_t)a.B * a.H));
+  if (a.drop_p > 0.f)
+    hipLaunchKernelGGL(attn_f32_bwd_kernel<true>, grid, dim3(NT), BWD_F32_LDS, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(attn_f32_bwd_kernel<false>, grid, dim3(NT), BWD_F32_LDS, (hipStream_t)stream, a);
   STE_CHECK_LAUNCH();
   return 0;
 }

@@ -501,6 +501,8 @@ class Engine:
         return self._postln_fwd(self.tcfg, XLMR_NAMES, i, x, xb, nb, L, mask32, hp, ap, seed, save)
 
     def _xlmr_bwd(self, i, sv, dx2, nb, L, mask32, hp, ap):
+        if self.precise_text:
+            return self._postln_bwd_x2(self.tcfg, XLMR_NAMES, i, sv, dx2, nb, L, mask32, hp, ap)
         return self._postln_bwd(self.tcfg, XLMR_NAMES, i, sv, dx2, nb, L, mask32, hp, ap)
 
     def _postln_fwd(self, c, nm, i, x, xb, nb, L, mask32, hp, ap, seed, save=True, act_p=0.0):
@@ -559,15 +561,12 @@ class Engine:
         eps = c.layer_norm_eps
         tr = s.trainable_layer(pre + nm["q"] + ".weight")
         sv = {"tr": tr, "seed": seed, "act_p": act_p}
-        qkvb = self._e(M, 3 * D, dtype=BF16) if save else None
-        qkv = ops.linear(xs, s.w2(pre + nm["q"] + ".weight", 3), s.fused(pre + nm["q"] + ".bias", 3, "p"),
-                         out_bf16_copy=qkvb)
+        qkv = ops.linear(xs, s.w2(pre + nm["q"] + ".weight", 3), s.fused(pre + nm["q"] + ".bias", 3, "p"))
         os_ = self._e(M, 2 * D, dtype=BF16)   # [O | O_lo]: the O-proj input and the backward's O, O_lo
         lse = self._e(nb * H * L)
         ops.attention_fwd_f32(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B=nb, T=L, H=H, o32=None, lse=lse,
                               o=os_[:, :D], o_lo=os_[:, D:], key_mask=mask32, scale=1.0 / math.sqrt(D // H),
                               drop_p=ap, seed=_site_seed(seed, 1), zero_masked_rows=True)
-        del qkv
         y1 = ops.linear(os_, s.w2(pre + nm["o"] + ".weight"), s.p(pre + nm["o"] + ".bias"), residual=x, drop_p=hp,
                         seed=_site_seed(seed, 2))
         x1 = self._e(M, D)
@@ -582,11 +581,80 @@ class Engine:
         x2 = self._e(M, D)
         x2s = self._e(M, 2 * D, dtype=BF16)
         sv["st2"] = self._ln(y2, pre + nm["ln2"], eps, y=x2, yb=x2s[:, :D], ylo=x2s[:, D:])
-        if save:
-            sv.update(qkv=qkvb, o=os_[:, :D], o_lo=os_[:, D:], lse=lse, y1=y1, zt=zt, y2=y2)
-        if tr:
-            sv.update(xb=xs[:, :D], x1b=x1s[:, :D], h=hs_[:, :F_])
+        if save:   # what _postln_bwd_x2 reads: fp32 q/k/v, the O image, LSE, LN inputs, GELU input
+            sv.update(qkv=qkv, os=os_, lse=lse, y1=y1, zt=zt, y2=y2)
+        if tr:     # the trained layers' dW operands as [hi | lo] images
+            sv.update(xs=xs, x1s=x1s, hs=hs_)
         return x2, x2s, sv
+
+    def _dw2(self, dys, xs, wname, fused=1):
+        """dW += dYᵀ·X of a text Linear from [hi | lo] split images of both operands, to ~fp32:
+        dY_hiᵀX_hi + dY_loᵀX_hi + dY_hiᵀX_lo (the lo·lo term is below fp32 rounding), three
+        k-major GEMMs accumulating into the flat gradient buffer."""
+        g = self.s.fused(wname, fused, "g") if fused > 1 else self.s.g(wname)
+        if g is None:
+            return
+        g2 = g.view(g.shape[0], -1)
+        n, k = dys.shape[1] // 2, xs.shape[1] // 2
+        for dy, x in ((dys[:, :n], xs[:, :k]), (dys[:, n:], xs[:, :k]), (dys[:, :n], xs[:, k:])):
+            ops.linear_dw(dy, x, out=g2, beta=1.0, ws=self.ws)
+
+    def _postln_bwd_x2(self, c, nm, i, sv, dx2, nb, L, mask32, hp, ap):
+        """Backward of _postln_fwd_x2 to ~fp32 accuracy.  The loss gradient reaching the text
+        encoder is the difference of the clean and the corrupted transcript's nearly equal
+        backward passes (80 % shared tokens), which every text weight and bias gradient sums over
+        rows: bf16 rounding of the backward's dY operands, of dO and of the attention backward
+        reappeared there as 1.2-2 % errors (tests/precision_probe_text.py).  So every dX GEMM reads
+        its dY as a [hi | lo] split image against [Wᵀ | Wᵀ] (ParamStore.wt2, K' = 2·out), the
+        GELU-backward GEMM writes its output as a split image, the O-proj input gradient dO stays
+        fp32, the attention backward runs in fp32 on the fp32 q/k/v (ste_attention_bwd_f32), the
+        bias gradients are column sums of fp32 values, and the trained layers' dW read split
+        images of both operands (_dw2)."""
+        s = self.s
+        pre = nm["layer"].format(i=i)
+        M, D, F_ = dx2.shape[0], c.hidden_size, c.intermediate_size
+        H = c.num_attention_heads
+        tr = sv["tr"]
+        seed = sv["seed"]
+        dy2 = self._e(M, D)
+        self._ln_bwd(dx2, sv["y2"], sv["st2"], pre + nm["ln2"], dx=dy2, drop_p=hp, seed=_site_seed(seed, 3),
+                     dsum=s.g(pre + nm["fo"] + ".bias"))
+        dy2s = ops.split_bf16(dy2, 2, 2)
+        dzs = self._e(M, 2 * F_, dtype=BF16)     # [dz | dz_lo]
+        ops.linear(dy2s, s.wt2(pre + nm["fo"] + ".weight"), act=ACT_GELU_BWD, z=sv["zt"], out=dzs[:, :F_],
+                   out_bf16_copy=dzs[:, F_:], copy_lo=True, colsum=s.g(pre + nm["fi"] + ".bias"),
+                   drop_p=sv["act_p"], seed=_site_seed(seed, 4), ws=self.ws)
+        if tr:
+            self._dw2(dy2s, sv["hs"], pre + nm["fo"] + ".weight")
+        del dy2s
+        dx1 = ops.linear(dzs, s.wt2(pre + nm["fi"] + ".weight"), residual=dy2, ws=self.ws)
+        if tr:
+            self._dw2(dzs, sv["x1s"], pre + nm["fi"] + ".weight")
+        del dzs, dy2
+        dy1 = self._e(M, D)
+        self._ln_bwd(dx1, sv["y1"], sv["st1"], pre + nm["ln1"], dx=dy1, drop_p=hp, seed=_site_seed(seed, 2),
+                     dsum=s.g(pre + nm["o"] + ".bias"))
+        del dx1
+        dy1s = ops.split_bf16(dy1, 2, 2)
+        do = ops.linear(dy1s, s.wt2(pre + nm["o"] + ".weight"), ws=self.ws)   # fp32 dO
+        if tr:
+            self._dw2(dy1s, sv["os"], pre + nm["o"] + ".weight")
+        del dy1s
+        qkv, os_ = sv["qkv"], sv["os"]
+        dqkv = self._e(M, 3 * D)
+        ops.attention_bwd_f32(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], os_[:, :D], os_[:, D:], sv["lse"], do,
+                              dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], B=nb, T=L, H=H, key_mask=mask32,
+                              scale=1.0 / math.sqrt(D // H), drop_p=ap, seed=_site_seed(seed, 1),
+                              zero_masked_rows=True)
+        del do
+        if tr:
+            self._db(dqkv, pre + nm["q"] + ".bias", fused=3)
+        dqkvs = ops.split_bf16(dqkv, 2, 2)
+        del dqkv
+        dx0 = ops.linear(dqkvs, s.wt2(pre + nm["q"] + ".weight", 3), residual=dy1, ws=self.ws)
+        if tr:
+            self._dw2(dqkvs, sv["xs"], pre + nm["q"] + ".weight", fused=3)
+        return dx0
 
     def _postln_bwd(self, c, nm, i, sv, dx2, nb, L, mask32, hp, ap):
         s = self.s

@@ -408,6 +408,31 @@ def attention_fwd_f32(q, k, v, *, B, T, H, o32, lse, o=None, o_lo=None, key_mask
     call("ste_attention_fwd_f32", C.byref(a), ptr(o32), 0 if o32 is None else _ld(o32), _s())
 
 
+def attention_bwd_f32(q, k, v, o, o_lo, lse, dout, dq, dk, dv, *, B, T, H, key_mask=None, scale=0.125, drop_p=0.0,
+                      seed=0, zero_masked_rows=False):
+    """Backward of attention_fwd_f32 in fp32 (ste_attention_bwd_f32): q/k/v/dout fp32 [B*T, *] views,
+    o / o_lo the forward's bf16 hi / lo halves of O, lse as it saved -> dq/dk/dv fp32 views."""
+    for t in (q, k, v, dout, dq, dk, dv):
+        assert t.dtype == F32
+    assert o.dtype == BF16 and o_lo.dtype == BF16
+    a = AttnArgs()
+    a.B, a.T, a.H = B, T, H
+    a.q, a.ldq = ptr(q), _ld(q)
+    a.k, a.ldk = ptr(k), _ld(k)
+    a.v, a.ldv = ptr(v), _ld(v)
+    a.o, a.ldo = ptr(o), _ld(o)
+    a.o_lo, a.ldolo = ptr(o_lo), _ld(o_lo)
+    a.lse = ptr(lse)
+    a.key_mask = ptr(key_mask)
+    a.scale, a.drop_p, a.seed = float(scale), float(drop_p), int(seed) & (2**64 - 1)
+    a.zero_masked_rows = int(bool(zero_masked_rows))
+    a.dout, a.lddo = ptr(dout), _ld(dout)
+    a.dq, a.lddq = ptr(dq), _ld(dq)
+    a.dk, a.lddk = ptr(dk), _ld(dk)
+    a.dv, a.lddv = ptr(dv), _ld(dv)
+    call("ste_attention_bwd_f32", C.byref(a), _s())
+
+
 def split_bf16(x, nblk, lo_mask, out=None):
     """fp32 [rows, K] -> bf16 [rows, nblk·K]: copy i = bf16(x), or its low half bf16(x - bf16(x)) where
     bit i of lo_mask is set (ste_split_bf16)."""

@@ -466,6 +466,47 @@ def test_attention_f32_fwd(ops, B, T, H, drop_p, masked):
         assert rel_err(got.view(B, T, H, D), want) < 1e-2
 
 
+@pytest.mark.parametrize("B,T,H,drop_p,masked,zero_rows", [(3, 64, 12, 0.0, True, True), (2, 100, 4, 0.1, True, True),
+                                                           (64, 64, 12, 0.1, False, True), (3, 16, 2, 0.0, "all", True),
+                                                           (3, 130, 2, 0.1, "all", False), (2, 37, 3, 0.0, True, False)])
+def test_attention_f32_bwd(ops, B, T, H, drop_p, masked, zero_rows):
+    """The precise text backward's attention (ste_attention_bwd_f32) against float64 autograd of the
+    same forward: fp32 q/k/v and dO, P recomputed from the saved LSE, delta from O hi + lo, the
+    forward's dropout mask; one 64-key chunk, ragged and multi-chunk T (dQ summed over chunks in
+    order), an all-masked sample under both conventions (SDPA's zero rows, eager's uniform rows)."""
+    torch.manual_seed(T * 3 + H)
+    D, W = 64, H * 64
+    qkv = torch.randn(B * T, 3 * W, device=DEV) * 0.7
+    q, k, v = qkv[:, :W], qkv[:, W:2 * W], qkv[:, 2 * W:]
+    mask = None
+    if masked:
+        m = torch.ones(B, T, dtype=torch.int32, device=DEV)
+        m[0, T - T // 3:] = 0
+        m[1, :5] = 0
+        if masked == "all":
+            m[2, :] = 0
+        mask = m.reshape(-1).contiguous()
+    o = torch.empty(B * T, W, device=DEV, dtype=torch.bfloat16)
+    olo = torch.empty_like(o)
+    lse = torch.empty(B * H * T, device=DEV)
+    ops.attention_fwd_f32(q, k, v, B=B, T=T, H=H, o32=None, lse=lse, o=o, o_lo=olo, key_mask=mask, drop_p=drop_p,
+                          seed=5, zero_masked_rows=zero_rows)
+    do = torch.randn(B * T, W, device=DEV)
+    dqkv = torch.full((B * T, 3 * W), float("nan"), device=DEV)
+    ops.attention_bwd_f32(q, k, v, o, olo, lse, do, dqkv[:, :W], dqkv[:, W:2 * W], dqkv[:, 2 * W:], B=B, T=T, H=H,
+                          key_mask=mask, drop_p=drop_p, seed=5, zero_masked_rows=zero_rows)
+    qd, kd, vd = (t.double().view(B, T, H, D).clone().requires_grad_() for t in (q, k, v))
+    ref = attention_ref(qd, kd, vd, mask.view(B, T) if masked else None, drop_p=drop_p, seed=5)
+    if zero_rows and masked:   # SDPA: a sample whose every key is masked gets zero weights
+        ref = ref * (mask.view(B, T).sum(1) > 0).double()[:, None, None, None]
+    ref.backward(do.double().view(B, T, H, D))
+    errs = {n: _rel64(dqkv[:, i * W:(i + 1) * W].view(B, T, H, D), g)
+            for i, (n, g) in enumerate((("dq", qd.grad), ("dk", kd.grad), ("dv", vd.grad)))}
+    print(f"attention_bwd_f32 B={B} T={T} H={H} drop={drop_p} masked={masked} zero_rows={zero_rows}: {errs}")
+    for n, e in errs.items():
+XX
+
+
 @pytest.mark.parametrize("T,drop_p,f32", [(70, 0.0, False), (130, 0.1, False), (70, 0.0, True), (130, 0.1, True)])
 def test_attention_zero_masked_rows(ops, T, drop_p, f32):
     """zero_masked_rows = 1 (the XLM-R SDPA rule): a sample whose every key is masked gets zero
