@@ -72,6 +72,9 @@ class Engine:
         # forward rounding reappeared in every gradient downstream.  STE_TEXT_PRECISE=0:
         # the plain bf16 forward (A/B runs only)
         self.precise_text = _lib.ab_env("STE_TEXT_PRECISE", "1") != "0"
+        # with precise_text: the text backward to ~fp32 accuracy as well (_postln_bwd_x2); off, the
+        # backward reads bf16 copies of the precise forward's activations (_postln_bwd)
+        self.precise_text_bwd = _lib.ab_env("STE_TEXT_PRECISE_BWD", "1") != "0"
 
     @property
     def fp8(self):
@@ -501,7 +504,7 @@ class Engine:
         return self._postln_fwd(self.tcfg, XLMR_NAMES, i, x, xb, nb, L, mask32, hp, ap, seed, save)
 
     def _xlmr_bwd(self, i, sv, dx2, nb, L, mask32, hp, ap):
-        if self.precise_text:
+        if self.precise_text and self.precise_text_bwd:
             return self._postln_bwd_x2(self.tcfg, XLMR_NAMES, i, sv, dx2, nb, L, mask32, hp, ap)
         return self._postln_bwd(self.tcfg, XLMR_NAMES, i, sv, dx2, nb, L, mask32, hp, ap)
 
@@ -561,7 +564,9 @@ class Engine:
         eps = c.layer_norm_eps
         tr = s.trainable_layer(pre + nm["q"] + ".weight")
         sv = {"tr": tr, "seed": seed, "act_p": act_p}
-        qkv = ops.linear(xs, s.w2(pre + nm["q"] + ".weight", 3), s.fused(pre + nm["q"] + ".bias", 3, "p"))
+        qkvb = self._e(M, 3 * D, dtype=BF16) if (save and not self.precise_text_bwd) else None
+        qkv = ops.linear(xs, s.w2(pre + nm["q"] + ".weight", 3), s.fused(pre + nm["q"] + ".bias", 3, "p"),
+                         out_bf16_copy=qkvb)
         os_ = self._e(M, 2 * D, dtype=BF16)   # [O | O_lo]: the O-proj input and the backward's O, O_lo
         lse = self._e(nb * H * L)
         ops.attention_fwd_f32(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B=nb, T=L, H=H, o32=None, lse=lse,
@@ -581,10 +586,14 @@ class Engine:
         x2 = self._e(M, D)
         x2s = self._e(M, 2 * D, dtype=BF16)
         sv["st2"] = self._ln(y2, pre + nm["ln2"], eps, y=x2, yb=x2s[:, :D], ylo=x2s[:, D:])
-        if save:   # what _postln_bwd_x2 reads: fp32 q/k/v, the O image, LSE, LN inputs, GELU input
-            sv.update(qkv=qkv, os=os_, lse=lse, y1=y1, zt=zt, y2=y2)
-        if tr:     # the trained layers' dW operands as [hi | lo] images
-            sv.update(xs=xs, x1s=x1s, hs=hs_)
+        if save and self.precise_text_bwd:   # what _postln_bwd_x2 reads: fp32 q/k/v, the O image, LSE,
+            sv.update(qkv=qkv, os=os_, lse=lse, y1=y1, zt=zt, y2=y2)   # LN inputs, GELU input
+            if tr:                             # the trained layers' dW operands as [hi | lo] images
+                sv.update(xs=xs, x1s=x1s, hs=hs_)
+        elif save:                             # what _postln_bwd reads: bf16 copies, the hi halves
+            sv.update(qkv=qkvb, o=os_[:, :D], o_lo=os_[:, D:], lse=lse, y1=y1, zt=zt, y2=y2)
+            if tr:
+                sv.update(xb=xs[:, :D], x1b=x1s[:, :D], h=hs_[:, :F_])
         return x2, x2s, sv
 
     def _dw2(self, dys, xs, wname, fused=1):

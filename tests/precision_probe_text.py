@@ -186,7 +186,8 @@ def main():
     sets = {"hip_text_bwd": ["tdy", "tdo", "tatt", "tdwx"], "tdy": ["tdy"], "tdo": ["tdo"], "tatt": ["tatt"],
             "tdwx": ["tdwx"], "afa": ["afa"], "all": list(FLAGS), "all_but_tdy": ["tdo", "tatt", "tdwx", "afa"],
             "all_but_tatt": ["tdy", "tdo", "tdwx", "afa"], "all_but_tdwx": ["tdy", "tdo", "tatt", "afa"],
-            "tatt_tdwx_afa": ["tatt", "tdwx", "afa"], "tatt_afa": ["tatt", "afa"], "tdwx_afa": ["tdwx", "afa"]}
+            "tatt_tdwx_afa": ["tatt", "tdwx", "afa"], "tatt_afa": ["tatt", "afa"], "tdwx_afa": ["tdwx", "afa"],
+            "tdy_tdwx_afa": ["tdy", "tdwx", "afa"], "tdy_afa": ["tdy", "afa"], "tdo_tatt_tdwx_afa": ["tdo", "tatt", "tdwx", "afa"]}
     if args.sets != "all":
         sets = {k: v for k, v in sets.items() if k in args.sets.split(",")}
     for name, on in sets.items():
