@@ -155,13 +155,16 @@ __global__ __launch_bounds__(NT) void attn_f32_fwd_kernel(ste_attn_args a, float
 // forward's O hi + lo halves (~16 mantissa bits).  One block per (sample, head) walks the key
 // chunks of 64 (dK, dV of the chunk in registers, written once) and, inside, the query tiles of 64
 // (dQ of a tile summed over the chunks in order by the same threads: deterministic, no atomics).
-// 256 threads; thread (ty, tx) = (t >> 4, t & 15) owns query rows ty + 16i and keys tx + 16j of a
-// score tile, and rows ty + 16i x columns 4tx..4tx+3 of the dQ / dK / dV tiles.
+// 1,024 threads (4 waves per SIMD: the images take 104 KB, one block per CU, and a 64 x 64 tile is
+// too little work per (sample, head) for fewer waves to hide the LDS latency — 256 threads ran at
+// 730 us per c2 text layer).  Thread (r, c) = (t >> 4, t & 15): the scores of query row r with keys
+// c + 16j; row / key r x columns 4c..4c+3 of the dQ / dK / dV tiles.
+constexpr int BWD_NT = 1024;
 constexpr int BLD = HD + 4;   // fp32 row stride of the Q / dO / K / V images
 constexpr int SLD = KC + 1;   // row stride of the Pd / dS images
 
 template <bool DROP>
-__global__ __launch_bounds__(NT) void attn_f32_bwd_kernel(ste_attn_args a) {
+__global__ __launch_bounds__(BWD_NT) void attn_f32_bwd_kernel(ste_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   float* sQ = smf;                       // [64][BLD]
   float* sD = sQ + QT * BLD;             // dO
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(NT) void attn_f32_bwd_kernel(ste_attn_args a) {
   float* sF = sDl + QT;                  // key flags[64]
   const int T = a.T, H = a.H;
   const int bh = blockIdx.x, h = bh % H, b = bh / H, bT = b * T;
-  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  const int tid = threadIdx.x, r = tid >> 4, c = tid & 15;
   const float* Qg = (const float*)a.q + h * HD;
   const float* Kg = (const float*)a.k + h * HD;
   const float* Vg = (const float*)a.v + h * HD;
@@ -188,13 +191,10 @@ __global__ __launch_bounds__(NT) void attn_f32_bwd_kernel(ste_attn_args a) {
   const float inv_keep = DROP ? 1.0f / (1.0f - a.drop_p) : 1.0f;
   const float inv_T = 1.0f / (float)T;
   const int nkc = (T + KC - 1) / KC, nqt = (T + QT - 1) / QT;
-  // stage rows [r0, r0 + 64) of a [B*T, *] fp32 operand (head h) into an image; rows >= T are 0
+  // row r0 + r of a [B*T, *] fp32 operand (head h), columns 4c..4c+3, into an image; rows >= T are 0
   auto stage = [&](float* img, const float* src, int64_t ld, int r0) {
-    for (int i = tid; i < 64 * HD / 4; i += NT) {
-      const int r = i >> 4, c = (i & 15) * 4;
-      *reinterpret_cast<f32x4*>(img + r * BLD + c) =
-          r0 + r < T ? *reinterpret_cast<const f32x4*>(src + (int64_t)(bT + r0 + r) * ld + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    *reinterpret_cast<f32x4*>(img + r * BLD + 4 * c) =
+        r0 + r < T ? *reinterpret_cast<const f32x4*>(src + (int64_t)(bT + r0 + r) * ld + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
   };
   for (int kc = 0; kc < nkc; ++kc) {
     const int k0 = kc * KC;
@@ -202,116 +202,83 @@ __global__ __launch_bounds__(NT) void attn_f32_bwd_kernel(ste_attn_args a) {
     stage(sK, Kg, a.ldk, k0);
     stage(sV, Vg, a.ldv, k0);
     if (tid < KC) sF[tid] = key_flag32(a.key_mask, bT, k0 + tid, T);
-    f32x4 dk[4], dv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
     for (int qt = 0; qt < nqt; ++qt) {
-      const int q0 = qt * QT;
+      const int q0 = qt * QT, q = q0 + r;
       __syncthreads();   // the previous tile's Q / dO / Pd / dS images are consumed
       stage(sQ, Qg, a.ldq, q0);
       stage(sD, dOg, a.lddo, q0);
-      // delta = dO·(O_hi + O_lo) per query row: 16 lanes per row, 4 columns each, DPP-free shuffles
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = ty + 16 * i, q = q0 + r;
+      {  // delta = dO·(O_hi + O_lo) of row r: the row's 16 lanes, 4 columns each
         float part = 0.f;
         if (q < T) {
           const int64_t row = bT + q;
-          const f32x4 dov = *reinterpret_cast<const f32x4*>(dOg + row * a.lddo + 4 * tx);
-          const f32x4 oh = load_bf16x4(Og + row * a.ldo + 4 * tx);
-          const f32x4 ol = load_bf16x4(Olg + row * a.ldolo + 4 * tx);
+          const f32x4 dov = *reinterpret_cast<const f32x4*>(dOg + row * a.lddo + 4 * c);
+          const f32x4 oh = load_bf16x4(Og + row * a.ldo + 4 * c);
+          const f32x4 ol = load_bf16x4(Olg + row * a.ldolo + 4 * c);
 #pragma unroll
           for (int e = 0; e < 4; ++e) part = fmaf(dov[e], oh[e] + ol[e], part);
         }
 #pragma unroll
         for (int o = 8; o >= 1; o >>= 1) part += __shfl_xor(part, o, 16);
-        if (tx == 0) {
+        if (c == 0) {
           sDl[r] = part;
           sL[r] = q < T ? a.lse[(int64_t)bh * T + q] : INFINITY;   // rows past T: p = 0
         }
       }
       __syncthreads();
-      // scores and dP for rows ty + 16i, keys tx + 16j
-      float sc[4][4], dp[4][4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) sc[i][j] = dp[i][j] = 0.f;
-#pragma unroll 4
+      // scores and dP of row r with keys c + 16j
+      float sc[4] = {0.f, 0.f, 0.f, 0.f}, dp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
       for (int d = 0; d < HD; d += 4) {
-        f32x4 qv[4], dov[4], kv[4], vv[4];
+        const f32x4 qv = *reinterpret_cast<const f32x4*>(sQ + r * BLD + d);
+        const f32x4 dov = *reinterpret_cast<const f32x4*>(sD + r * BLD + d);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          qv[i] = *reinterpret_cast<const f32x4*>(sQ + (ty + 16 * i) * BLD + d);
-          dov[i] = *reinterpret_cast<const f32x4*>(sD + (ty + 16 * i) * BLD + d);
-          kv[i] = *reinterpret_cast<const f32x4*>(sK + (tx + 16 * i) * BLD + d);
-          vv[i] = *reinterpret_cast<const f32x4*>(sV + (tx + 16 * i) * BLD + d);
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 kv = *reinterpret_cast<const f32x4*>(sK + (c + 16 * j) * BLD + d);
+          const f32x4 vv = *reinterpret_cast<const f32x4*>(sV + (c + 16 * j) * BLD + d);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            sc[j] = fmaf(qv[e], kv[e], sc[j]);
+            dp[j] = fmaf(dov[e], vv[e], dp[j]);
+          }
         }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              sc[i][j] = fmaf(qv[i][e], kv[j][e], sc[i][j]);
-              dp[i][j] = fmaf(dov[i][e], vv[j][e], dp[i][j]);
-            }
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = ty + 16 * i, q = q0 + r;
+      {
         const float lse = sL[r], dl = sDl[r];
         const uint64_t drow = ((uint64_t)bh * T + (uint64_t)(q < T ? q : 0)) * (uint64_t)T;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int kl = tx + 16 * j, key = k0 + kl;
+          const int kl = c + 16 * j, key = k0 + kl;
           const float f = sF[kl];
           float p;
           if (lse == INFINITY || f < -0.5f) p = 0.f;                 // zero-weight row / key past T
           else if (lse == -INFINITY) p = inv_T;                       // uniform row (every key masked)
-          else p = __expf((f > 0.5f ? sc[i][j] * a.scale : NEG_MASK) - lse);
+          else p = __expf((f > 0.5f ? sc[j] * a.scale : NEG_MASK) - lse);
           const float m = DROP ? drop_scale(a.seed, drow + (uint64_t)key, thresh, inv_keep) : 1.0f;
           sP[r * SLD + kl] = p * m;
-          sS[r * SLD + kl] = p * (m * dp[i][j] - dl);
+          sS[r * SLD + kl] = p * (m * dp[j] - dl);
         }
       }
       __syncthreads();
-      // dV += Pdᵀ·dO, dK += dSᵀ·Q (keys ty + 16i, columns 4tx..), dQ tile = dS·K (rows ty + 16i)
-      f32x4 dq[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // dV += Pdᵀ·dO, dK += dSᵀ·Q for key r, columns 4c..; dQ tile row r = dS·K
       const int nq = min(QT, T - q0), nk = min(KC, T - k0);
-      for (int r = 0; r < nq; ++r) {
-        const f32x4 dov = *reinterpret_cast<const f32x4*>(sD + r * BLD + 4 * tx);
-        const f32x4 qv = *reinterpret_cast<const f32x4*>(sQ + r * BLD + 4 * tx);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int kl = ty + 16 * i;
-          dv[i] += sP[r * SLD + kl] * dov;
-          dk[i] += sS[r * SLD + kl] * qv;
-        }
+      for (int i = 0; i < nq; ++i) {
+        dv += sP[i * SLD + r] * *reinterpret_cast<const f32x4*>(sD + i * BLD + 4 * c);
+        dk += sS[i * SLD + r] * *reinterpret_cast<const f32x4*>(sQ + i * BLD + 4 * c);
       }
-      for (int kl = 0; kl < nk; ++kl) {
-        const f32x4 kv = *reinterpret_cast<const f32x4*>(sK + kl * BLD + 4 * tx);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dq[i] += sS[(ty + 16 * i) * SLD + kl] * kv;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = q0 + ty + 16 * i;
-        if (q >= T) continue;
-        float* dst = dQg + (int64_t)(bT + q) * a.lddq + 4 * tx;
-        f32x4 v = dq[i] * a.scale;
+      f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+      for (int kl = 0; kl < nk; ++kl) dq += sS[r * SLD + kl] * *reinterpret_cast<const f32x4*>(sK + kl * BLD + 4 * c);
+      if (q < T) {
+        float* dst = dQg + (int64_t)(bT + q) * a.lddq + 4 * c;
+        f32x4 v = dq * a.scale;
         if (kc > 0) v += *reinterpret_cast<const f32x4*>(dst);   // this thread's own earlier chunk
         *reinterpret_cast<f32x4*>(dst) = v;
       }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int key = k0 + ty + 16 * i;
-      if (key >= T) continue;
-      *reinterpret_cast<f32x4*>(dKg + (int64_t)(bT + key) * a.lddk + 4 * tx) = dk[i] * a.scale;
-      *reinterpret_cast<f32x4*>(dVg + (int64_t)(bT + key) * a.lddv + 4 * tx) = dv[i];
+    const int key = k0 + r;
+    if (key < T) {
+      *reinterpret_cast<f32x4*>(dKg + (int64_t)(bT + key) * a.lddk + 4 * c) = dk * a.scale;
+      *reinterpret_cast<f32x4*>(dVg + (int64_t)(bT + key) * a.lddv + 4 * c) = dv;
     }
   }
 }
@@ -352,9 +319,9 @@ extern "C" int ste_attention_bwd_f32(const ste_attn_args* args, void* stream) {
   if (a.drop_p < 0.f || a.drop_p >= 1.f) return STE_ERR_ARG;
   const dim3 grid((unsigned)((int64_t)a.B * a.H));
   if (a.drop_p > 0.f)
-    hipLaunchKernelGGL(attn_f32_bwd_kernel<true>, grid, dim3(NT), BWD_F32_LDS, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(attn_f32_bwd_kernel<true>, grid, dim3(BWD_NT), BWD_F32_LDS, (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL(attn_f32_bwd_kernel<false>, grid, dim3(NT), BWD_F32_LDS, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(attn_f32_bwd_kernel<false>, grid, dim3(BWD_NT), BWD_F32_LDS, (hipStream_t)stream, a);
   STE_CHECK_LAUNCH();
   return 0;
 }

@@ -1443,6 +1443,8 @@ int num_cus() {
   X(true, false, 0, STE_ACT_NONE)                            /* dX, fp32 out       */ \
   X(true, true, EF_Z | EF_COLSUM | EF_CBF16, STE_ACT_SWISH_BWD) /* dz = dh·W ⊙ act'(z), Wᵀ copy */ \
   X(true, true, EF_Z | EF_COLSUM | EF_CBF16, STE_ACT_GELU_BWD)                        \
+  X(true, true, EF_Z | EF_COLSUM | EF_C3 | EF_CBF16, STE_ACT_GELU_BWD) /* precise text dz: dz, dz_lo */ \
+  X(true, true, EF_Z | EF_C3 | EF_CBF16, STE_ACT_GELU_BWD)            /* ... frozen layer        */ \
   X(true, true, EF_Z | EF_CBF16, STE_ACT_SWISH_BWD)          /* frozen layer: no db */ \
   X(true, true, EF_Z | EF_CBF16, STE_ACT_GELU_BWD)                                    \
   X(true, true, EF_Z | EF_COLSUM | EF_DROP | EF_CBF16, STE_ACT_GELU_BWD) /* wav2vec2 act dropout */ \
