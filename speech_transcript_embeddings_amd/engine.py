@@ -72,9 +72,13 @@ class Engine:
         # forward rounding reappeared in every gradient downstream.  STE_TEXT_PRECISE=0:
         # the plain bf16 forward (A/B runs only)
         self.precise_text = _lib.ab_env("STE_TEXT_PRECISE", "1") != "0"
-        # with precise_text: the text backward to ~fp32 accuracy as well (_postln_bwd_x2); off, the
-        # backward reads bf16 copies of the precise forward's activations (_postln_bwd)
-        self.precise_text_bwd = _lib.ab_env("STE_TEXT_PRECISE_BWD", "1") != "0"
+        # with precise_text: the text backward to ~fp32 accuracy as well (_postln_bwd_x2: fp32 text
+        # attention backward, split-bf16 dY and dW operands).  Opt-in: it halves the loss-derived
+        # error of the text weights (tests/test_model_gpu.py, tests/precision_probe_text.py) for
+        # 2.9 % of the c2 step (its extra side-stream work competes with the audio chain:
+        # profiles/r5e_text_bwd_ab.txt); off, the backward reads bf16 copies of the precise forward's
+        # activations (_postln_bwd).  Set the attribute before the first forward.
+        self.precise_text_bwd = _lib.ab_env("STE_TEXT_PRECISE_BWD", "0") == "1"
 
     @property
     def fp8(self):

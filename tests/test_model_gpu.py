@@ -174,8 +174,9 @@ def test_backward_random_cotangents(tag):
     assert errs[len(errs) // 2][0] < 5e-3
 
 
-@pytest.mark.parametrize("tag", ["noalign", "align", "nopool", "masked"])
-def test_forward_backward_matches_golden_and_oracle(tag):
+@pytest.mark.parametrize("tag,precise_bwd", [("noalign", False), ("align", False), ("nopool", False), ("masked", False),
+                                             ("nopool", True), ("masked", True)])
+def test_forward_backward_matches_golden_and_oracle(tag, precise_bwd):
     """The drop-in autograd path (compute_pos_neg_embeddings -> (aud*txt).sum(1) -> loss_fn ->
     loss.backward(), ref :1068-1094) against the reference's golden outputs and the oracle.
 
@@ -193,6 +194,7 @@ def test_forward_backward_matches_golden_and_oracle(tag):
     meta, z = load(tag)
     model = mini_model(meta)
     model.eval()
+    model.engine.precise_text_bwd = precise_bwd
     from speech_transcript_embeddings_amd.model import AlignmentAwareInfoNCE, EnhancedAudioTextModel
     batch = batch_of(z)
     tpn, tnn, an = EnhancedAudioTextModel.compute_pos_neg_embeddings(model, batch)
@@ -237,6 +239,7 @@ def test_forward_backward_matches_golden_and_oracle(tag):
     lo.backward()
     mx = mini_model(meta, exact=True)
     mx.eval()
+    mx.engine.precise_text_bwd = precise_bwd
     tpx, tnx, anx = EnhancedAudioTextModel.compute_pos_neg_embeddings(mx, batch)
     AlignmentAwareInfoNCE(0.1, 0.5)((anx * tpx).sum(1), (anx * tnx).sum(1),
                                     alignment_scores=mx.last_alignment_scores).backward()
@@ -260,6 +263,13 @@ def test_forward_backward_matches_golden_and_oracle(tag):
     # tokens), and the text backward's bf16 dY operands carry that cancellation
     assert errs[len(errs) // 2][0] < 1e-2 and errs[0][0] < 2e-2, errs[:3]
     assert agree >= 0.99 * total, agree / total
+    if precise_bwd:
+        # the precise text backward (fp32 attention backward, split dY / dW operands): every text
+        # gradient within north_star's 1e-2 bf16 bound (measured 0.5-0.7 %; with the bf16 text
+        # backward 1.1-2.0 %, tests/precision_probe_text.py attributes it to the dY / dO rounding)
+        text = [(e, n) for e, n in errs if n.startswith("text_encoder.")]
+        print(f"[{tag}] precise text backward, text tensors worst {text[:3]}")
+        assert text[0][0] < 1e-2, text[:3]
 
 
 def test_fp8_gemm_matches_oracle():
