@@ -9,7 +9,7 @@
 //   -> 512-point radix-8 Stockham FFT in registers (fp32, twiddles from double sincos) -> |X|^2
 //   -> 80 kaldi-scale triangular mel filters built in mel space (sparse, per-block
 //   table) -> max(1.1920929e-7, .) -> natural log.
-// Kernel 2 (two single-wave blocks per clip, one lane per mel bin): per-mel-bin mean and
+// Kernel 2 (one 1024-thread block per clip, rows staged through LDS): per-mel-bin mean and
 // unbiased variance over the clip's frames exactly as numpy evaluates them on the extractor's
 // float32 log-mel array (tf:…seamless_m4t…:256-261: x.mean(0), x.var(0, ddof=1), (x - mean)/sqrt(var + 1e-7)):
 // float32 sums accumulated frame by frame in order (numpy's reduction over a non-contiguous
@@ -191,52 +191,55 @@ __global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restri
 }
 
 // per-clip CMVN statistics: stats[b][m] = mean, stats[b][NMEL + m] = sqrt(var + 1e-7)
-// The sums must run frame by frame in order (numpy's rounding: the reduction over axis 0 of a
-// C-contiguous [T, 80] array adds whole rows), so one lane per mel bin owns each chain: a wave
-// holds 64 consecutive bins of one clip (two waves per clip), reads its rows straight from the
-// log-mel array (one coalesced 256-B row slice per frame) STATS_PF frames ahead of the chain, and
-// walks the mean pass and then the variance pass; 2 x B single-wave blocks, no LDS, no barriers.
-// (Was: one 1,024-thread block per clip staging 128-frame chunks through LDS, 64 blocks on 256
-// CUs, 31 us for the c2 batch.)
-constexpr int STATS_PF = 16;
-__global__ __launch_bounds__(64) void fbank_stats_kernel(const int32_t* __restrict__ lengths, int Fmax,
-                                                       const float* __restrict__ work, float* __restrict__ stats) {
-  const int b = blockIdx.x >> 1, m = (blockIdx.x & 1) * 64 + threadIdx.x;
+// The sums must run frame by frame in order (numpy's rounding), so one thread per mel bin owns
+// each chain; the block's 1024 threads stage the clip's log-mel rows through LDS in chunks of
+// STATS_CH frames with all of a chunk's loads in flight at once, and the next chunk's loads are
+// issued into registers before the 80 chains walk the current one.
+constexpr int STATS_NT = 1024, STATS_CH = 128, STATS_PER = STATS_CH * NMEL / STATS_NT;   // 10
+__global__ __launch_bounds__(STATS_NT) void fbank_stats_kernel(const int32_t* __restrict__ lengths, int Fmax,
+                                                             const float* __restrict__ work,
+                                                             float* __restrict__ stats) {
+  __shared__ float sx[2][STATS_CH * NMEL];   // 80 KB
+  const int b = blockIdx.x, tid = threadIdx.x;
   const int len = lengths[b];
   const int F = len >= FRAME ? 1 + (len - FRAME) / HOP : 0;
-  if (m >= NMEL) return;
-  const float* x = work + (int64_t)b * Fmax * NMEL + m;
-  auto fetch = [&](float (&r)[STATS_PF], int f0) {
-#pragma unroll
-    for (int i = 0; i < STATS_PF; ++i) r[i] = f0 + i < F ? x[(int64_t)(f0 + i) * NMEL] : 0.f;
-  };
+  const float* x = work + (int64_t)b * Fmax * NMEL;
+  const int nch = (F + STATS_CH - 1) / STATS_CH;
   float s = 0.f, q = 0.f, mean = 0.f;
-  float cur[STATS_PF], nxt[STATS_PF];
+  float r[STATS_PER];
+  auto fetch = [&](int c) {   // chunk c (of the 2 * nch chunk visits) -> registers
+    const int f0 = (c % nch) * STATS_CH, n = min(STATS_CH, F - f0) * NMEL;
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    fetch(cur, 0);
-    for (int f0 = 0; f0 < F; f0 += STATS_PF) {
-      fetch(nxt, f0 + STATS_PF);          // the next batch's loads in flight under this one's chain
-      const int n = min(STATS_PF, F - f0);
+    for (int i = 0; i < STATS_PER; ++i) {
+      const int e = tid + i * STATS_NT;
+      r[i] = e < n ? x[(int64_t)f0 * NMEL + e] : 0.f;
+    }
+  };
+  if (nch > 0) fetch(0);
+  for (int c = 0; c < 2 * nch; ++c) {
+    float* buf = sx[c & 1];
 #pragma unroll
-      for (int i = 0; i < STATS_PF; ++i) {
-        if (i < n) {
-          if (pass == 0) {
-            s = __fadd_rn(s, cur[i]);
-          } else {
-            const float d = __fsub_rn(cur[i], mean);
-            q = __fadd_rn(q, __fmul_rn(d, d));
-          }
+    for (int i = 0; i < STATS_PER; ++i) buf[tid + i * STATS_NT] = r[i];
+    __syncthreads();
+    if (c + 1 < 2 * nch) fetch(c + 1);
+    if (tid < NMEL) {
+      const int f0 = (c % nch) * STATS_CH, nf = min(STATS_CH, F - f0);
+      if (c < nch) {
+        for (int i = 0; i < nf; ++i) s = __fadd_rn(s, buf[i * NMEL + tid]);
+        if (c == nch - 1) mean = __fdiv_rn(s, (float)F);
+      } else {
+        for (int i = 0; i < nf; ++i) {
+          const float d = __fsub_rn(buf[i * NMEL + tid], mean);
+          q = __fadd_rn(q, __fmul_rn(d, d));
         }
       }
-#pragma unroll
-      for (int i = 0; i < STATS_PF; ++i) cur[i] = nxt[i];
     }
-    if (pass == 0) mean = F > 0 ? __fdiv_rn(s, (float)F) : 0.f;
   }
-  const float var = F > 1 ? __fdiv_rn(q, (float)(F - 1)) : 0.f;
-  stats[(int64_t)b * 2 * NMEL + m] = mean;
-  stats[(int64_t)b * 2 * NMEL + NMEL + m] = __fsqrt_rn(__fadd_rn(var, 1e-7f));
+  if (tid < NMEL) {
+    const float var = F > 1 ? __fdiv_rn(q, (float)(F - 1)) : 0.f;
+    stats[(int64_t)b * 2 * NMEL + tid] = mean;
+    stats[(int64_t)b * 2 * NMEL + NMEL + tid] = __fsqrt_rn(__fadd_rn(var, 1e-7f));
+  }
 }
 
 constexpr int NORM_ROWS = 8;   // stacked rows per block of the normalise / stack kernel
@@ -287,7 +290,7 @@ extern "C" int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* length
                      Fmax, logmel);
   STE_CHECK_LAUNCH();
   float* stats = work + (int64_t)B * Fmax * NMEL;
-  hipLaunchKernelGGL(fbank_stats_kernel, dim3(2 * B), dim3(64), 0, s, lengths, Fmax, logmel, stats);
+  hipLaunchKernelGGL(fbank_stats_kernel, dim3(B), dim3(STATS_NT), 0, s, lengths, Fmax, logmel, stats);
   STE_CHECK_LAUNCH();
   hipLaunchKernelGGL(fbank_norm_kernel, dim3((Tmax + NORM_ROWS - 1) / NORM_ROWS, B), dim3(256), 0, s, lengths, Fmax,
                      Tmax, logmel, stats, pad_value, feats, mask, mask_mode);

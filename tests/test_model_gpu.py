@@ -265,7 +265,7 @@ def test_forward_backward_matches_golden_and_oracle(tag, precise_bwd):
     assert agree >= 0.99 * total, agree / total
     if precise_bwd:
         # the precise text backward (fp32 attention backward, split dY / dW operands): every text
-        # gradient within north_star's 1e-2 bf16 bound (measured 0.5-0.7 %; with the bf16 text
+        # gradient within north_star's 1e-2 bf16 bound (measured 0.20 / 0.37 %, masked / nopool; with the bf16 text
         # backward 1.1-2.0 %, tests/precision_probe_text.py attributes it to the dY / dO rounding)
         text = [(e, n) for e, n in errs if n.startswith("text_encoder.")]
         print(f"[{tag}] precise text backward, text tensors worst {text[:3]}")
