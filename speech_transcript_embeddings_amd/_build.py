@@ -44,7 +44,9 @@ def _compile(src: Path, hdr_mtime: float, verbose: bool, ab: bool = False) -> Pa
     obj = (OBJ_AB if ab else OBJ) / (src.stem + ".o")
     if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, hdr_mtime):
         return obj
-    cmd = [HIPCC, *FLAGS, *(["-DSTE_AB"] if ab else []), "-c", str(src), "-o", str(obj)]
+    # STE_BUILD_DEFINES="-DNAME=V ...": extra macros for one-off experiment builds (A/B only)
+    extra = os.environ.get("STE_BUILD_DEFINES", "").split() if ab else []
+    cmd = [HIPCC, *FLAGS, *(["-DSTE_AB"] if ab else []), *extra, "-c", str(src), "-o", str(obj)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

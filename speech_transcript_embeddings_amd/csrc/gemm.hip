@@ -1086,6 +1086,56 @@ STE_DEV void epilogue_8ph(const ste_gemm_args& p, const f32x4 (&acc)[8][4], floa
     colsum_flush(p, csum, c0, c1, batch, lane, ((int64_t)batch * ((p.M + 255) >> 8) + (m0 >> 8)) * 2 + wm);
 }
 
+// The epilogue of an operand-loading (Z or R) compile-time epilogue on a full tile, with the next
+// tile's prologue DMA issued after the first two passes' loads: those loads are older than the DMA
+// (vmcnt counts in issue order), so they land without waiting for it, and every later pass's loads
+// are issued two passes ahead, after the DMA.  All of this tile's stores then follow the
+// prologue, so the next tile's first waits may leave them in flight (epi_stores<EF>(), as the
+// load-free EPI_OVL epilogues do) and they drain under its first K-tiles; the DMA latency hides
+// under the epilogue instead of following it.
+#ifndef STE_EPI_PRE
+#define STE_EPI_PRE 1
+#endif
+template <int EF, int ACT, class Pro>
+STE_DEV void epilogue_8ph_pre(const ste_gemm_args& p, const f32x4 (&acc)[8][4], float* epi, int m0, int n0, int batch,
+                              int wm, int wn, int lane, f32x8 bias, Pro&& prologue) {
+  static_assert(EF >= 0 && (EF & (EF_COLSUM | EF_BETA | EF_RS | EF_Q8)) == 0, "EPI_PRE epilogues");
+  Csum csum = {};
+  const int c0 = n0 + wn * 32, c1 = n0 + 128 + wn * 32;
+#define STE_EPI_STAGE(PS)                                                                       \
+  {                                                                                             \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                             \
+      _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                           \
+        const int row = (lane >> 4) * 4 + r, chunk = (4 * j + ((lane & 15) >> 2)) ^ ((r >> 1) & 1); \
+        epi[row * 64 + chunk * 4 + (lane & 3)] = acc[PS][j][r];                                 \
+      }                                                                                         \
+    }                                                                                           \
+    __builtin_amdgcn_s_waitcnt(0xc07f);                                                         \
+    __builtin_amdgcn_wave_barrier();                                                            \
+  }
+#define STE_EPI_ROW0(PS) (m0 + wm * 128 + (PS) * 16)
+#define STE_EPI_LOAD(PS, L) epi_load16<EF, ACT, true>(p, STE_EPI_ROW0(PS), c0, c1, batch, lane, L);
+#define STE_EPI_STORE(PS, L)                                                                    \
+  epi_store16<EF, ACT, true>(p, epi, STE_EPI_ROW0(PS), c0, c1, batch, lane, bias, L, csum);     \
+  __builtin_amdgcn_s_waitcnt(0xc07f);                                                           \
+  __builtin_amdgcn_wave_barrier();
+  EpiLoads L0, L1;
+  STE_EPI_LOAD(0, L0) STE_EPI_LOAD(1, L1)
+  prologue();
+  STE_EPI_STAGE(0) STE_EPI_STORE(0, L0) STE_EPI_LOAD(2, L0)
+  STE_EPI_STAGE(1) STE_EPI_STORE(1, L1) STE_EPI_LOAD(3, L1)
+  STE_EPI_STAGE(2) STE_EPI_STORE(2, L0) STE_EPI_LOAD(4, L0)
+  STE_EPI_STAGE(3) STE_EPI_STORE(3, L1) STE_EPI_LOAD(5, L1)
+  STE_EPI_STAGE(4) STE_EPI_STORE(4, L0) STE_EPI_LOAD(6, L0)
+  STE_EPI_STAGE(5) STE_EPI_STORE(5, L1) STE_EPI_LOAD(7, L1)
+  STE_EPI_STAGE(6) STE_EPI_STORE(6, L0)
+  STE_EPI_STAGE(7) STE_EPI_STORE(7, L1)
+#undef STE_EPI_STAGE
+#undef STE_EPI_ROW0
+#undef STE_EPI_LOAD
+#undef STE_EPI_STORE
+}
+
 // steady-state operand wait: W pieces stay in flight (4 half-tiles = 8; MX adds the K-tile's scale
 // piece, issued with A-half 0, so 9), plus the previous tile's epilogue stores still draining
 // (capped at the 6-bit vmcnt field: waiting for a few more of those stores is merely early)
@@ -1161,6 +1211,11 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p, M
                             : smem + EPI_OFF + wave * EPI16_FLOATS * 4;
   float* epi = reinterpret_cast<float*>(epi_base);
   constexpr bool EPI_OVL = EF >= 0 && (EF & (EF_Z | EF_R | EF_BETA | EF_COLSUM | EF_RS)) == 0;
+  // operand-loading epilogues (residual adds, activation backward x Z): the prologue DMA goes out
+  // behind the first two passes' loads (epilogue_8ph_pre); A/B builds: -DSTE_EPI_PRE=0
+  constexpr bool EPI_PRE_OK = EF >= 0 && !EPI_OVL && !MX && !SW && (EF & (EF_Z | EF_R)) != 0 &&
+                              (EF & (EF_BETA | EF_COLSUM | EF_RS | EF_Q8 | EF_DROP)) == 0;   // DROP: spills
+  constexpr bool epi_pre = EPI_PRE_OK && STE_EPI_PRE;
   f32x8 bias = f32x8{};
   f32x4 sbias[4] = {};
   // the tile's bias preloaded across the main loop — except MX, whose main loop needs the registers
@@ -1384,19 +1439,31 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p, M
       }
     };
     if (EPI_OVL) next_prologue();
+    bool pro_done = EPI_OVL;
     if constexpr (SW) {
       char* slot = epi_base;
       if (full_tile) epilogue_bf16s<EF, ACT, true>(p, acc, slot, em0, en0, ebatch, wm, wn, lane, sbias);
       else epilogue_bf16s<EF, ACT, false>(p, acc, slot, em0, en0, ebatch, wm, wn, lane, sbias);
     } else {
       const Q8Out* q8 = MX && mx.q8.q ? &mx.q8 : nullptr;
-      if (full_tile) epilogue_8ph<EF, ACT, true>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias, q8);
-      else epilogue_8ph<EF, ACT, false>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias, q8);
+      if constexpr (EPI_PRE_OK) {
+        if (full_tile && epi_pre) {
+          epilogue_8ph_pre<EF, ACT>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias, next_prologue);
+          pro_done = true;
+        } else if (full_tile) {
+          epilogue_8ph<EF, ACT, true>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias, q8);
+        } else {
+          epilogue_8ph<EF, ACT, false>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias, q8);
+        }
+      } else {
+        if (full_tile) epilogue_8ph<EF, ACT, true>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias, q8);
+        else epilogue_8ph<EF, ACT, false>(p, acc, epi, em0, en0, ebatch, wm, wn, lane, bias, q8);
+      }
     }
-    if (!EPI_OVL) next_prologue();
+    if (!pro_done) next_prologue();
     if (!more) break;
     vb = vb_next;
-    extra = (EPI_OVL && full_tile) ? 1 : 0;
+    extra = ((EPI_OVL || (EPI_PRE_OK && epi_pre)) && full_tile) ? 1 : 0;
     if constexpr (EF >= 0 && (EF & EF_BIAS) != 0 && !MX) {
       if constexpr (SW) swap_bias(p, n0, wn, lane, sbias);
       else bias = tile_bias(p, n0, wn, lane);
