@@ -896,10 +896,7 @@ STE_DEV int half_row(int pr, int h) {
 
 // O32: the source as a 32-bit byte offset from the (wave-uniform) base, which the DMA takes as
 // saddr + voffset: one VGPR per piece instead of a 64-bit pointer (operands < 4 GiB; the MX kernel,
-// whose scale staging needs the registers, and every k-major operand: the weight-gradient kernel
-// <false, false> spilled 47 VGPRs with 64-bit sources, and hipcc follows each scratch reload of a
-// spilled source address with vmcnt(0), draining the counted DMA pipeline in every phase that
-// stages; see km_o32_ok for the host-side size guard)
+// whose scale staging needs the registers)
 template <bool KC, int G, bool O32 = false>
 STE_DEV void stage_half(const bf16* base, int64_t ld, int row0, int rows, int k0, int h, char* dst, int wave,
                         int lane) {
@@ -914,18 +911,10 @@ STE_DEV void stage_half(const bf16* base, int64_t ld, int row0, int rows, int k0
       if (O32) src = (const bf16*)((const char*)base + (uint32_t)(((uint32_t)gr * (uint32_t)ld + k0 + ch * 8) * 2u));
       else src = base + (int64_t)gr * ld + k0 + ch * 8;
     } else {   // image [64 k][128 cols], 256-B k-rows, chunk ^ km_xor(k)
-      // O32: the lane id regenerated (mbcnt, behind an opaque copy) instead of kept live across the
-      // K-loop: its derived offsets were what the weight-gradient kernel spilled
-      int ln = lane;
-      if (O32) {
-        ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-        asm volatile("" : "+v"(ln));
-      }
-      const int kk = piece * 4 + (ln >> 4);
-      const int lc = (ln & 15) ^ km_chunk_xor(kk);
+      const int kk = piece * 4 + (lane >> 4);
+      const int lc = (lane & 15) ^ km_chunk_xor(kk);
       const int gc = min(row0 + half_row<G>(lc * 8, h), rows - 8);
-      if (O32) src = (const bf16*)((const char*)base + (uint32_t)(((uint32_t)(k0 + kk) * (uint32_t)ld + gc) * 2u));
-      else src = base + (int64_t)(k0 + kk) * ld + gc;
+      src = base + (int64_t)(k0 + kk) * ld + gc;
     }
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
   }
@@ -1203,9 +1192,9 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p, M
   const bf16* B;
   operand_bases<A_KC, B_KC>(p, batch, A, B, nk);
 #define STAGE_A(t, h) \
-  stage_half<A_KC, 64, MX || !A_KC>(A, p.lda, m0, p.M, (t) * 64, h, smem + ((t) & 1) * BUF + (h) * HALF, wave, lane)
+  stage_half<A_KC, 64, MX>(A, p.lda, m0, p.M, (t) * 64, h, smem + ((t) & 1) * BUF + (h) * HALF, wave, lane)
 #define STAGE_B(t, h) \
-  stage_half<B_KC, 128, MX || !B_KC>(B, p.ldb, n0, p.N, (t) * 64, h, smem + ((t) & 1) * BUF + (2 + (h)) * HALF, wave, lane)
+  stage_half<B_KC, 128, MX>(B, p.ldb, n0, p.N, (t) * 64, h, smem + ((t) & 1) * BUF + (2 + (h)) * HALF, wave, lane)
 #define STAGE_S(t) \
   if constexpr (MX) stage_scales(mx, m0, p.M, n0, p.N, (t), smem, wave, lane)
 #define STAGE_PROLOGUE()                                                    \
@@ -1624,16 +1613,6 @@ int few_split(const ste_gemm_args& a) {
   return 2;
 }
 
-// The 8-phase kernel stages k-major operands from 32-bit byte offsets (stage_half<.., O32>): every
-// k-major operand of one launch entry (batch entry / split-K slab of k_rows rows) must span less
-// than 4 GiB.  Larger ones take the small kernel.
-bool km_o32_ok(const ste_gemm_args& a, int64_t k_rows) {
-  const int64_t lim = (int64_t)1 << 32;
-  if (!a.a_kc && (k_rows * a.lda + a.M) * 2 >= lim) return false;
-  if (!a.b_kc && (k_rows * a.ldb + a.N) * 2 >= lim) return false;
-  return true;
-}
-
 // Batched weight gradients (both operands k-major, batch > 1: the wav2vec2 conv stack's per-clip
 // dW slabs over strided views, K = frames of one clip, usually ragged): the 8-phase kernel over
 // the whole-64 part of K (the batch fills the chip), the K % 64 tail accumulated by the small
@@ -1647,7 +1626,6 @@ bool batched_dw_ok(const ste_gemm_args& a) {
   if (!on || a.a_kc || a.b_kc || a.batch < 2) return false;
   if (a.bias || a.C2 || a.C3 || a.R || a.Z || a.colsum || a.row_scale || a.act || a.drop_p > 0.f) return false;
   if ((a.M & 7) || (a.N & 7) || a.M < 256 || a.N < 256 || a.K < 1024) return false;
-  if (!km_o32_ok(a, a.K)) return false;
   const long tiles = (long)((a.M + 255) / 256) * ((a.N + 255) / 256) * a.batch;
   return tiles >= 240;
 }
@@ -1671,7 +1649,6 @@ SplitPlan splitk_plan(const ste_gemm_args& a) {
   const int64_t slab = (int64_t)a.M * a.N * 4;
   while (S > 1 && S * slab > a.ws_bytes) --S;
   if (S < 1 || S * slab > a.ws_bytes) return pl;
-  if (!km_o32_ok(a, (int64_t)(nk / S + 1) * 64)) return pl;   // a slab: Kc (+1 leftover) K-tiles
   pl.S = S;
   pl.Kc = nk / S;
   return pl;
@@ -1705,7 +1682,6 @@ bool big_ok_shape(const ste_gemm_args& a) {
 }
 bool big_ok(const ste_gemm_args& a) {
   if (!big_ok_shape(a)) return false;
-  if (!km_o32_ok(a, a.K)) return false;
   const long tiles = (long)((a.M + 255) / 256) * ((a.N + 255) / 256) * a.batch;
   static int min_tiles = -1;   // STE_GEMM_MIN_TILES: A/B of the small-kernel threshold
   if (min_tiles < 0) {

@@ -711,14 +711,22 @@ class Engine:
             self._db(dqkv, pre + nm["q"] + ".bias", fused=3)
         return dx0
 
-    def text_backward(self, dh, ctx):
+    def text_backward(self, dh, ctx, layers_done=None):
+        """layers_done() is called once every trainable XLM-R layer's gradients are final (after
+        the lowest trainable layer), so their all-reduce overlaps the frozen text layers' passes."""
         c = self.tcfg
         s = self.s
         nb, L = ctx["t_nb"], ctx["t_L"]
+        lo = next((i for i in range(c.num_hidden_layers)
+                   if s.trainable_layer(XLMR_NAMES["layer"].format(i=i) + XLMR_NAMES["q"] + ".weight")), None)
+        if lo is None and layers_done is not None:
+            layers_done()
         dx = dh
         for i in reversed(range(c.num_hidden_layers)):
             dx = self._xlmr_bwd(i, ctx["t_layers"][i], dx, nb, L, ctx["t_mask32"], ctx["t_hp"], ctx["t_ap"])
             ctx["t_layers"][i] = None
+            if i == lo and layers_done is not None:
+                layers_done()
         gw = s.g("text_encoder.embeddings.word_embeddings.weight")
         gp = s.g("text_encoder.embeddings.position_embeddings.weight")
         gt = s.g("text_encoder.embeddings.token_type_embeddings.weight")
@@ -1115,9 +1123,9 @@ class Engine:
     def backward(self, ctx, d_tp, d_tn, d_af, d_align, stage_done=None):
         """Backward of the whole step.  stage_done(name) is called once the gradients of a
         parameter block are final, so a data-parallel caller can start their collective while the
-        rest of the backward runs: "heads", then (text on its side stream) "text" with the current
-        stream set to that side stream, "audio_layers", "audio"; on one stream the GradSync.STAGES
-        order "heads", "audio_layers", "audio", "text"."""
+        rest of the backward runs: "heads", then (text on its side stream) "text_layers" and "text"
+        with the current stream set to that side stream, "audio_layers", "audio"; on one stream the
+        GradSync.STAGES order "heads", "audio_layers", "audio", "text_layers", "text"."""
         nb = ctx["t_nb"]
         d_tf = self._e(nb, self.m.projection_dim)
         _copy_f32(d_tp, d_tf[: nb // 2])
@@ -1133,7 +1141,7 @@ class Engine:
             main = torch.cuda.current_stream(self.s.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                self.text_backward(dth, ctx)
+                self.text_backward(dth, ctx, (lambda: stage_done("text_layers")) if stage_done else None)
                 if stage_done:
                     # the text block is final once the side stream has run its backward: its
                     # collectives (dense all-reduce, word-table row exchange) are queued behind it on
@@ -1150,7 +1158,7 @@ class Engine:
             del dah
             if stage_done:
                 stage_done("audio")
-            self.text_backward(dth, ctx)
+            self.text_backward(dth, ctx, (lambda: stage_done("text_layers")) if stage_done else None)
             if stage_done:
                 stage_done("text")
         ctx.clear()

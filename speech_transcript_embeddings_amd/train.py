@@ -191,10 +191,13 @@ class GradSync:
                       them (the frozen layers' input-gradient passes still run behind it);
       "audio"         the rest of the audio encoder (feature projection, SpecAugment embedding),
                       at the end of the audio backward;
-      "text"          the text encoder, as soon as its backward has run on the side stream: the
-                      call is made with that stream current, so this block's collectives queue
-                      behind the text backward alone and overlap the audio backward (on one
-                      stream: after the audio backward).
+      "text_layers"   the trainable XLM-R layers, once the text backward has passed the lowest
+                      of them (the frozen text layers' input-gradient passes still run behind it);
+      "text"          the rest of the text encoder (embedding LayerNorm, position and token-type
+                      tables, the word table), at the end of the text backward.
+    The text stages are signalled from the side stream the text backward runs on (that stream
+    current), so their collectives queue behind the text backward alone and overlap the audio
+    backward (on one stream: after the audio backward).
     Each block's dense ranges are all-reduced asynchronously (RCCL ring over xGMI, <= bucket_mb
     per call, average) while the remaining backward kernels run.  The 250,002 x 768
     word-embedding gradient is exchanged row-sparse: each rank extracts the rows of its own token
@@ -221,8 +224,9 @@ class GradSync:
     # in the order the backward finalises them: the heads; the trainable Conformer layers (the
     # top k, final once the backward has passed the lowest of them, while the frozen layers'
     # input gradients still run); the rest of the audio encoder (feature projection, SpecAugment
-    # embedding: final at the very end); the text encoder (side stream, joined at the end)
-    STAGES = ("heads", "audio_layers", "audio", "text")
+    # embedding: final at the very end); the trainable text layers (side stream, final once its
+    # backward has passed the lowest of them); the rest of the text encoder (end of the text backward)
+    STAGES = ("heads", "audio_layers", "audio", "text_layers", "text")
 
     def __init__(self, store, bucket_mb: int = 256, pad_id: int = 1, word_capacity: int | None = None):
         self.store = store
@@ -258,7 +262,10 @@ class GradSync:
                                             x.name.startswith("audio_encoder.encoder.layers.")),
                        "audio": span(lambda x: x.segment == "enc" and x.name.startswith("audio_encoder.") and
                                      not x.name.startswith("audio_encoder.encoder.layers.")),
-                       "text": span(lambda x: x.segment == "enc" and x.name.startswith("text_encoder."))}
+                       "text_layers": span(lambda x: x.segment == "enc" and
+                                           x.name.startswith("text_encoder.encoder.layer.")),
+                       "text": span(lambda x: x.segment == "enc" and x.name.startswith("text_encoder.") and
+                                    not x.name.startswith("text_encoder.encoder.layer."))}
         if self.words is not None and self.ranges["text"]:
             w0, w1 = self.words.offset, self.words.offset + self.words.numel
             cut = []

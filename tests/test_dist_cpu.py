@@ -91,7 +91,8 @@ def _sync_case(rank, world):
     ops.rows_extract, ops.rows_accumulate = rows_extract_ref, rows_accumulate_ref
     V, D = 50, 4
     slots = [("text_encoder.embeddings.word_embeddings.weight", 0, (V, D), "enc"),
-             ("text_encoder.encoder.layer.1.x", 200, (37,), "enc"),
+             ("text_encoder.encoder.layer.1.x", 200, (21,), "enc"),
+             ("text_encoder.embeddings.LayerNorm.weight", 221, (16,), "enc"),
              ("audio_encoder.encoder.layers.0.x", 240, (101,), "enc"),
              ("audio_encoder.feature_projection.projection.weight", 344, (13,), "enc"),
              ("text_proj.weight", 360, (45,), "head"),
@@ -386,7 +387,8 @@ def _fake_model(B, L, P=8, V=50):
     forward returns fixed embeddings and its backward writes a gradient per stage."""
     from speech_transcript_embeddings_amd.store import Slot
     slots = [("text_encoder.embeddings.word_embeddings.weight", 0, (V, 4), "enc"),
-             ("text_encoder.encoder.layer.1.x", 200, (37,), "enc"),
+             ("text_encoder.encoder.layer.1.x", 200, (21,), "enc"),
+             ("text_encoder.embeddings.LayerNorm.weight", 221, (16,), "enc"),
              ("audio_encoder.encoder.layers.0.x", 240, (101,), "enc"),
              ("audio_encoder.feature_projection.projection.weight", 344, (13,), "enc"),
              ("text_proj.weight", 360, (45,), "head")]
@@ -437,7 +439,10 @@ def _fake_model(B, L, P=8, V=50):
             gr[344:357] += 1.0
             if stage_done:
                 stage_done("audio")
-            gr[200:237] += d_tn.sum()
+            gr[200:221] += d_tn.sum()
+            if stage_done:
+                stage_done("text_layers")
+            gr[221:237] += d_tn.mean()
             for i in ctx["t_ids"].reshape(-1):
                 gr[int(i) * 4:int(i) * 4 + 4] += 0.5      # (test code: host reads are fine here)
             if stage_done:

@@ -186,7 +186,7 @@ def test_trainstep_two_ranks_gloo_same_gpu():
         assert out["replicas_equal"] and out["finite"], (r, out)
         # fp32 summation order of atomically accumulated gradients: identical to ~1e-6
         assert all(e < 1e-5 for e in out["avg_errs"].values()), (r, out["avg_errs"])
-        assert set(out["avg_errs"]) >= {"heads", "audio_layers", "audio", "text", "word_embeddings"}
+        assert set(out["avg_errs"]) >= {"heads", "audio_layers", "audio", "text_layers", "text", "word_embeddings"}
         assert out["diag_err"] < 1e-5, (r, out["diag_err"])
         assert out["inbatch_err"] < 1e-4, (r, out["inbatch_err"])
         assert out["metrics"]["samples"] == 4 and out["metrics"]["optimizer_steps"] == 1
