@@ -759,7 +759,10 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
   __builtin_amdgcn_s_barrier();
 
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-  f32x4 o[2][4];
+  f32x4 o[2][4], lw[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};   // SPLIT: Σ hi + lo P
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq)
 #pragma unroll
@@ -866,6 +869,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
       m[gq] = mnew;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
+      if (SPLIT) lw[gq] *= alpha;
       // this group's PV right after its softmax: its MFMAs run while the VALU does the next
       // group's softmax (the transposed V reads were issued before the first softmax)
       if (gq == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -879,6 +883,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
           const bf16x8 pl = pack_acc_lo(s[gq][2 * u], s[gq][2 * u + 1], pb);
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pl, o[gq][dt]);
+          lw[gq] = mfma16(ones, pl, mfma16(ones, pb, lw[gq]));   // Σ of the same hi + lo P (see rel4)
         }
       }
     }
@@ -892,7 +897,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
   for (int gq = 0; gq < 2; ++gq) {
     const int myq = qw + 16 * gq + li;
     if (myq < T) {
-      const float inv_l = 1.0f / l[gq];
+      const float inv_l = 1.0f / (SPLIT ? lw[gq][0] : l[gq]);
       bf16* O = (bf16*)a.o + (int64_t)(bT + myq) * a.ldo + h * HD;
       if (SPLIT && a.o_lo) {
         bf16* Ol = (bf16*)a.o_lo + (int64_t)(bT + myq) * a.ldolo + h * HD;
@@ -975,12 +980,17 @@ STE_DEV s16x4 ds_read_tr16_off(uint32_t addr) {
 }
 
 // SPLIT: o_lo is written (O as bf16 hi + lo, for the backward's delta = dO·O).
-// PLO: the PV product runs on P = bf16(P) + bf16(P - bf16(P)) (hi + lo within 2^-16 of p) and the
-// row sum is the fp32 sum of the exact p.  Without PLO the PV product runs on bf16 P and the row
-// sum is the MFMA sum of the SAME rounded P, so O = Σ P̃ V / Σ P̃ is a weighted mean whose weights
-// sum to 1 up to fp32 accumulation: a component common to every V row passes into O exactly, and
-// delta = dO·O cancels it in the backward's dP - delta as the exact-P delta does (the near-uniform
-// regime of tests/test_kernels_gpu.py).  Forward-only calls (no o_lo) use the same product.
+// PLO: the PV product runs on P = bf16(P) + bf16(P - bf16(P)) (hi + lo within 2^-16 of p).  O is
+// normalised by the MFMA sum of the SAME hi + lo P (against a ones operand), so O = Σ P̂ V / Σ P̂
+// is a weighted mean whose weights sum to 1 up to fp32 accumulation; the LSE the backward
+// recomputes p from uses the fp32 sum of the exact p, so that p sums to 1 too.  (Through round 5
+// O was normalised by the exact-p sum: the hi/lo split's errors do not sum to zero, a component
+// common to every V row then leaked into O at 2^-17 / sqrt(T), and delta = dO·O carried it into
+// every dS = p(dP - delta) of a near-uniform row — the distance-table gradients of c5, whose edge
+// bins sum dS over ~1,400 keys, sat 0.2 points above the bf16 floor; tests/test_fullsize_gpu.py,
+// profiles/r5_parity.txt.)  Without PLO the PV product runs on bf16 P and the row sum is the MFMA
+// sum of the same rounded P: the common component cancels in the same way.  Forward-only calls
+// (no o_lo) use the no-PLO product.
 template <bool SPLIT, bool PLO>
 __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
   static_assert(SPLIT || !PLO, "the hi/lo split of P only serves the backward's delta");
@@ -1173,7 +1183,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
         const float mnew = fmaxf(m[gq], tmax);
         const float alpha = __builtin_amdgcn_exp2f(m[gq] - mnew);
         if (PLO) lp[gq] *= alpha;
-        else lsum[gq] *= alpha;
+        lsum[gq] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
         m[gq] = mnew;
@@ -1195,12 +1205,12 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
         const bf16x8 pb = pack_acc(s[gq][2 * u], s[gq][2 * u + 1]);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pb, o[gq][dt]);
+        lsum[gq] = mfma16(ones, pb, lsum[gq]);   // row sum of the same (rounded) P, on the MFMA
         if constexpr (PLO) {
           const bf16x8 pl = pack_acc_lo(s[gq][2 * u], s[gq][2 * u + 1], pb);
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt) o[gq][dt] = mfma16(vf[dt][u], pl, o[gq][dt]);
-        } else {
-          lsum[gq] = mfma16(ones, pb, lsum[gq]);   // row sum of the same (rounded) P, on the MFMA
+          lsum[gq] = mfma16(ones, pl, lsum[gq]);
         }
       }
     }
@@ -1216,11 +1226,12 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
   }
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq) {
-    // every accumulator row holds the full row sum (MFMA form) / the 4 lanes of a row hold partials
+    // every accumulator row holds the full row sum of the P that O summed (MFMA form); the 4 lanes
+    // of a row hold partials of the exact p's sum (PLO: the LSE's)
     const float lt = PLO ? rowsum4(lp[gq]) : lsum[gq][0];
     const int myq = qw + 16 * gq + li;
     if (myq < T) {
-      const float inv_l = 1.0f / lt;
+      const float inv_l = 1.0f / lsum[gq][0];
       bf16* O = (bf16*)a.o + (int64_t)(bT + myq) * a.ldo + h * HD;
       if (SPLIT && a.o_lo) {
         bf16* Ol = (bf16*)a.o_lo + (int64_t)(bT + myq) * a.ldolo + h * HD;

@@ -20,6 +20,8 @@ attentive pooling, with a fixed random cotangent on the pooled output, run
       ads  attention dS and its distance-bin sums G rounded to bf16 for dQ = dS·K + G·E and
            dK = dSᵀ·Q (pack_acc in attn_bwd_dq_rel3 / dkv_rel3)
       apb  attention P rounded to bf16 for dV = Pᵀ·dO
+      zb   the FFN swish's pre-activation z stored bf16 for the backward (the FFN-in GEMM's
+           pre_out copy that the activation-backward epilogue reads: swish'(bf16(z)); round 5)
     (the forward's P·V runs on P = hi + lo, ~fp32, as the saving forward does; the pooling
     scorer reads the fp32 states — the [hi | lo] split image — with bf16 W.)
 Per-tensor gradient error = ||g - g_fp32|| / ||g_fp32||, printed for every flag set: all on
@@ -45,7 +47,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 from oracle import fbank_ref, ref_model as R  # noqa: E402
 
-FLAGS = ("w", "fa", "bdy", "bdx", "ads", "apb")
+FLAGS = ("w", "fa", "bdy", "bdx", "ads", "apb", "zb")
 # weight classes for the "w" attribution sets (w_<class>): which GEMMs read bf16 weights
 WCLASSES = ("qkv", "E", "o", "ffn", "conv", "pool", "fp")
 
@@ -65,6 +67,21 @@ class _Q(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         return (bf(g) if ctx.b else g), None, None
+
+
+class _SiluZ(torch.autograd.Function):
+    """swish whose backward reads the pre-activation from a bf16 copy (zb)."""
+
+    @staticmethod
+    def forward(ctx, z):
+        ctx.save_for_backward(bf(z))
+        return F.silu(z)
+
+    @staticmethod
+    def backward(ctx, g):
+        z, = ctx.saved_tensors
+        sg = torch.sigmoid(z)
+        return g * sg * (1 + z * (1 - sg))
 
 
 def q(x, f, b):
@@ -104,7 +121,7 @@ class _LinMX8(torch.autograd.Function):
 
 class Probe:
     def __init__(self, fl, autocast=False, wclasses=WCLASSES, wlayers=None, fasites=None, falayers=None,
-                 fp8=()):
+                 fp8=(), olo=None, plo=False):
         self.fl = {k: bool(fl.get(k, False)) for k in FLAGS}
         self.ac = autocast   # reference-under-autocast: scores / probabilities in bf16 storage too
         self.wclasses = set(wclasses)
@@ -113,6 +130,13 @@ class Probe:
         self.fasites = None if fasites is None else set(fasites)   # None: every site rounds (with "fa")
         self.falayers = falayers
         self.fp8 = set(fp8)   # GEMM classes (qkv, o, ffn, conv) on MX-fp8 forward operands (config 5)
+        # diagnostics of the attention's own approximations (not bf16 storage): olo = how the
+        # backward's delta = dO·O reads O ("bf16": hi + bf16 lo, the ste_attn_args.o_lo image;
+        # "fp16s": hi + fp16 lo scaled by 2^8; None: fp32); plo: the forward's PV on P = hi + lo
+        # (True: normalised by the fp32 Σ p, as attn_fwd_rel4<*, true> through round 5; "norm": by
+        # the Σ of the same hi + lo P)
+        self.olo = olo
+        self.plo = plo
 
     def fa(self, site):
         """forward rounding of an activation at `site` (qkv_in, qkv_out, o, ffn_in, ffn_h, conv_in,
@@ -144,7 +168,8 @@ class Probe:
     # ------------------------------------------------------------------ Conformer pieces
     def ffn(self, p, pre, a):
         z = self.lin(a, p[pre + "intermediate_dense.weight"], p[pre + "intermediate_dense.bias"])
-        h = q(F.silu(z), self.fa("ffn_h"), False)     # swish epilogue, stored bf16; dz rounded by the GEMM's bdy
+        sw = _SiluZ.apply(z) if self.fl["zb"] else F.silu(z)
+        h = q(sw, self.fa("ffn_h"), False)     # swish epilogue, stored bf16; dz rounded by the GEMM's bdy
         return self.lin(h, p[pre + "output_dense.weight"], p[pre + "output_dense.bias"], dx_round=False,
                         in_site="ffn_h")
 
@@ -210,7 +235,14 @@ class _Attn(torch.autograd.Function):
         if pr.ac:
             s = bf(s)
         p = torch.softmax(s, -1)
-        o = (bf(p) if pr.ac else p) @ vh
+        if pr.plo:
+            ph = bf(p)
+            pp = ph + bf(p - ph)
+            o = pp @ vh
+            if pr.plo == "norm":   # O's weights renormalised to sum to 1 (Σ of the same hi + lo P)
+                o = o / pp.sum(-1, keepdim=True)
+        else:
+            o = (bf(p) if pr.ac else p) @ vh
         if pr.ac:
             o = bf(o)
         ctx.save_for_backward(qh, kh, vh, E, p, o)
@@ -224,7 +256,12 @@ class _Attn(torch.autograd.Function):
         B, H, T, d = qh.shape
         nrel = E.shape[0]
         dp = do @ vh.transpose(-1, -2)
-        delta = (do * o).sum(-1, keepdim=True)
+        od = o
+        if ctx.pr.olo is not None:
+            oh = bf(o)
+            od = oh + (bf(o - oh) if ctx.pr.olo == "bf16" else
+                       ((o - oh) * 256.0).to(torch.float16).to(torch.float32) / 256.0)
+        delta = (do * od).sum(-1, keepdim=True)
         ds = p * (dp - delta)
         if ac:
             ds = bf(ds)
@@ -279,18 +316,20 @@ def main(argv=None):
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--sets", default="hip,autocast,minus")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--seed", type=int, default=0, help="weights / clips / cotangent draw (instance variance)")
     args = ap.parse_args(argv)
     torch.set_num_threads(args.threads)
     cfg = R.ModelCfg()
     ac = cfg.audio
-    p0 = init_params(cfg)
+    p0 = init_params(cfg, args.seed)
     n = int(args.seconds * 16000)
-    feats, _ = fbank_ref.collate([fbank_ref.extract(fbank_ref.synth_wave(1000 + i, n))[0] for i in range(args.batch)])
+    feats, _ = fbank_ref.collate([fbank_ref.extract(fbank_ref.synth_wave(1000 + 100 * args.seed + i, n))[0]
+                                  for i in range(args.batch)])
     feats = torch.as_tensor(np.asarray(feats), dtype=torch.float32)
     top = [f"audio_encoder.encoder.layers.{i}." for i in range(ac.layers - args.unfreeze, ac.layers)]
     trainable = {k for k in p0 if k.startswith("audio_encoder.feature_projection") or k.startswith("audio_pooling")
                  or any(k.startswith(t) for t in top)}
-    cot = torch.randn(args.batch, ac.hidden, generator=torch.Generator().manual_seed(5))
+    cot = torch.randn(args.batch, ac.hidden, generator=torch.Generator().manual_seed(5 + args.seed))
     t0 = time.time()
     ref, out_ref = run(p0, feats, cot, ac, args.layers, trainable, {})
     print(f"fp32 reference: {time.time() - t0:.1f} s, {len(ref)} gradient tensors", flush=True)

@@ -32,6 +32,23 @@ trainable layer from 3.3 % to 1.7 %.  The audio attentive-pooling scorer runs on
 output's [hi | lo] split image with fp32 tanh activations (r3: 2.3 % -> 1.75 %); what is left
 there is the bf16 audio encoder's forward rounding of that common component (the scorer's
 gradient Σ_l dz_l ⊗ h_l cancels across frames), the same limit as the deepest layers' q/k.
+
+The floor of THIS instance (round 5).  How far a bf16 path can get from fp32 on these tensors
+depends on the draw: the CPU probe's emulation of the HIP rounding points (tests/precision_probe.py,
+bf16-exact weights, c1 shapes) puts the worst tensor anywhere in 0.89-1.37 % over seeds 0-5
+(profiles/r5_parity.txt), so a floor measured on another draw says little about this one.  The
+bf16-exact configs therefore emulate the floor on the test's own weights, clips and cotangents:
+the audio encoder + pooling run again on the CPU with bf16 rounding at the HIP path's rounding
+points (precision_probe.Probe: forward activations, backward dY / dX operands, attention dS and
+P, the FFN pre-activation the swish backward reads) and in fp32, driven by the cotangents the
+fp32 oracle's backward delivers at the pooled output and at the encoder output's other consumers
+(cross-modal K/V, alignment).  The HIP path's worst audio tensor must lie within max(1e-2, that
+floor's worst + 0.1 points); every other tensor within 1e-2.  Measured (round 5, profiles/
+r5_parity.txt): c1 1.17 % vs floor 1.25 %, c2 0.87 / 0.90 %, c4 0.98 / 0.99 %, c5 1.10 / 1.02 %.
+The margin is not slack for the kernels: the pooling scorer's gradients move by ±0.2 points
+between runs whose forwards differ at the 1e-6 level (they difference nearly equal frames), and
+the c5 distance-table gradients of layers 12-13 carry an excess no emulated rounding point
+reproduces.
 """
 import pytest
 import torch
@@ -39,6 +56,7 @@ import torch.nn.functional as F
 
 from kref import bf16_exact_model_
 from oracle import ref_model as R
+import precision_probe as PP
 
 pytestmark = pytest.mark.gpu
 
@@ -58,9 +76,56 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-30)).item()
 
 
-@pytest.mark.timeout(900)
-@pytest.mark.parametrize("cname", list(CONFIGS))
-def test_full_size_vs_oracle(cname):
+class _AudioTap:
+    """Wraps the oracle's attentive pooling of the audio states: records the encoder output h and,
+    during the oracle's backward, the cotangents at the pooled output and at h's other consumers
+    (cross-modal K/V, alignment) — the inputs of the same-instance floor emulation."""
+
+    def __init__(self):
+        self.cap = {}
+        self.orig = R.attentive_pooling
+
+    def __enter__(self):
+        def pool(p_, pre, h, mask):
+            if pre != "audio_pooling.":
+                return self.orig(p_, pre, h, mask)
+            self.cap = {}
+            h2 = h * 1.0   # the pooling's own view of h: its hook sees only the pooling's share
+            out = self.orig(p_, pre, h2, mask)
+            if h.requires_grad:
+                h.register_hook(lambda g: self.cap.__setitem__("dh", g.detach().clone()))
+                h2.register_hook(lambda g: self.cap.__setitem__("dh_pool", g.detach().clone()))
+                out.register_hook(lambda g: self.cap.__setitem__("dpooled", g.detach().clone()))
+            return out
+        R.attentive_pooling = pool
+        return self
+
+    def __exit__(self, *exc):
+        R.attentive_pooling = self.orig
+
+
+def _floor_errs(sd, feats, acfg, trainable, cap, probe_kw=None):
+    """Per-tensor error of the emulated HIP rounding (bf16-exact weights) vs the emulation in fp32,
+    on this instance's audio weights, clips and oracle cotangents (probe_kw: extra rounding points
+    for diagnostics, precision_probe.Probe keywords)."""
+    names = [n for n in sd if n.startswith(("audio_encoder.", "audio_pooling."))]
+    tr = {n for n in names if n in trainable}
+    dpooled = cap["dpooled"]
+    dh_other = cap["dh"] - cap["dh_pool"]
+    g = {}
+    for tag, fl in (("fp32", {}), ("hip", {k: k != "w" for k in PP.FLAGS})):
+        pr = PP.Probe(fl, **(probe_kw if tag == "hip" and probe_kw else {}))
+        p = {n: sd[n].clone().requires_grad_(n in tr) for n in names}
+        h = pr.encoder(p, feats, acfg, acfg.layers)
+        pooled = pr.pool(p, h)
+        torch.autograd.backward([pooled, h], [dpooled, dh_other])
+        g[tag] = {n: p[n].grad for n in tr if p[n].grad is not None}
+    return {n: _rel(g["hip"][n], g["fp32"][n]) for n in g["fp32"] if g["fp32"][n].norm() > 1e-8}, g["fp32"]
+
+
+def _hip_vs_oracle(cname):
+    """The HIP path's forward + backward on random output cotangents and the oracle's on the same
+    weights and inputs; returns the per-tensor gradient errors and what the floor emulation needs."""
     from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
     from speech_transcript_embeddings_amd.train import synthetic_batch
     B, N, L, k, align, freeze, fp8, exact = CONFIGS[cname]
@@ -108,7 +173,9 @@ def test_full_size_vs_oracle(cname):
     p = {n: sd[n].clone().requires_grad_(n in trainable) for n in names}
     bc = {kk: v.cpu() for kk, v in batch.items()}
     torch.set_num_threads(16)
-    tpn, tnn, an, al = R.compute_pos_neg_embeddings(p, bc, cfg)
+    tap = _AudioTap()
+    with tap:
+        tpn, tnn, an, al = R.compute_pos_neg_embeddings(p, bc, cfg)
     flips = 0
     if align:
         # The confidence MLP's ReLU is a discrete gate (b*L x 384 units); pre-activations within
@@ -130,7 +197,8 @@ def test_full_size_vs_oracle(cname):
 
         R_F, R.F = R.F, _Gated()
         try:
-            tpn, tnn, an, al = R.compute_pos_neg_embeddings(p, bc, cfg)
+            with tap:
+                tpn, tnn, an, al = R.compute_pos_neg_embeddings(p, bc, cfg)
         finally:
             R.F = R_F
         assert flips < 0.01 * gate.numel(), flips
@@ -153,6 +221,15 @@ def test_full_size_vs_oracle(cname):
         assert params[n].grad is not None, n
         errs.append((_rel(params[n].grad, p[n].grad), n))
     errs.sort(reverse=True)
+    return dict(errs=errs, sd=sd, bc=bc, cfg=cfg, trainable=trainable, cap=tap.cap, p=p, flips=flips)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cname", list(CONFIGS))
+def test_full_size_vs_oracle(cname):
+    B, N, L, k, align, freeze, fp8, exact = CONFIGS[cname]
+    r = _hip_vs_oracle(cname)
+    errs, sd, bc, cfg, trainable, p, flips = (r[x] for x in ("errs", "sd", "bc", "cfg", "trainable", "p", "flips"))
     assert len(errs) > 50
     median = errs[len(errs) // 2][0]
     print(f"[{cname}] grad rel err ({'bf16-exact' if exact else 'fp32 master'} weights): worst {errs[:6]}, "
@@ -162,16 +239,29 @@ def test_full_size_vs_oracle(cname):
         # backward): measured median 12 %, worst 26 % (bf16 c5: 0.7 % / 2.1 %)
         assert median < 2e-1 and errs[0][0] < 4e-1, (median, errs[:5])
     elif exact:
-        # the kernels' arithmetic on bf16-exact weights.  c2 / c4 shapes: within north_star's 1e-2
-        # (measured 0.93 / 0.98 %).  c1 (2 s clips) and c5 (T = 1,499, every layer trainable) sit
-        # at the bf16-activation floor of the graph itself: the fp32 oracle with bf16 storage of
-        # the forward activations at the HIP path's rounding points and nothing else changed gives
-        # 1.02 % (c1) and 1.14 % (c5) on the same tensors (tests/precision_probe.py, measured
-        # 1.31 / 1.30 % here) — the trained layers' q/k, distance table and pooling-scorer gradients
-        # of a random-init encoder (near-uniform attention) amplify any 2^-9 perturbation of the
-        # hidden states; 1.5e-2 there
+        # the kernels' arithmetic on bf16-exact weights against the bf16 floor of THIS instance
+        # (module docstring): every tensor within north_star's 1e-2, except that an audio tensor
+        # may sit where the emulated HIP rounding of the same weights, clips and cotangents puts
+        # the worst one, + 0.1 points
+        floor, g_emul = _floor_errs(sd, bc["input_values"], cfg.audio, trainable, r["cap"])
+        # the emulation in fp32 is the oracle's own audio backward (same cotangents): a check
+        # that the floor was measured on the graph the oracle differentiates
+        emul_err = max(_rel(g_emul[n], p[n].grad) for n in g_emul
+                       if not n.endswith(("linear_k.bias", "attention.2.bias")))   # true gradient 0
+        fl = sorted(((e, n) for n, e in floor.items() if not n.endswith(("linear_k.bias", "attention.2.bias"))),
+                    reverse=True)
+        bound_audio = max(1e-2, fl[0][0] + 1e-3)
+        aud = [(e, n) for e, n in errs if n.startswith(("audio_encoder.", "audio_pooling."))]
+        rest = [(e, n) for e, n in errs if not n.startswith(("audio_encoder.", "audio_pooling."))]
+        print(f"[{cname}] same-instance bf16 floor (audio, emulated): worst {fl[:4]}, median "
+              f"{fl[len(fl) // 2][0]:.2e}; emulation-vs-oracle fp32 {emul_err:.1e}; audio bound {bound_audio:.4f}")
+        print(f"[{cname}] HIP vs floor on HIP's worst audio tensors: "
+              + ", ".join(f"{n.replace('audio_encoder.encoder.', '')} {e:.4f}/{floor.get(n, float('nan')):.4f}"
+                          for e, n in aud[:8]))
+        assert emul_err < 1e-4, emul_err
         assert median < 5e-3, median
-        assert errs[0][0] < (1e-2 if cname in ("c2", "c4") else 1.5e-2), errs[:5]
+        assert aud[0][0] < bound_audio, (aud[:5], fl[:5])
+        assert not rest or rest[0][0] < 1e-2, rest[:5]
     else:
         # arbitrary fp32 weights: the GEMMs read their bf16 rounding.  The fp32 reference graph
         # itself, evaluated with bf16-rounded weights and nothing else changed, moves these
