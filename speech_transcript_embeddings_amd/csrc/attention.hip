@@ -982,8 +982,10 @@ STE_DEV s16x4 ds_read_tr16_off(uint32_t addr) {
 // SPLIT: o_lo is written (O as bf16 hi + lo, for the backward's delta = dO·O).
 // PLO: the PV product runs on P = bf16(P) + bf16(P - bf16(P)) (hi + lo within 2^-16 of p).  O is
 // normalised by the MFMA sum of the SAME hi + lo P (against a ones operand), so O = Σ P̂ V / Σ P̂
-// is a weighted mean whose weights sum to 1 up to fp32 accumulation; the LSE the backward
-// recomputes p from uses the fp32 sum of the exact p, so that p sums to 1 too.  (Through round 5
+// is a weighted mean whose weights sum to 1 up to fp32 accumulation.  The LSE is formed from the
+// same sum: Σ P̂ = (1 + O(2^-17)) Σ p scales every p the backward recomputes from it by one factor
+// per row, which multiplies dS = p(dP - delta) by 1 + O(2^-17) and leaves Σ dS = 0 intact (delta
+// reads O, whose weights sum to 1).  (Through round 5
 // O was normalised by the exact-p sum: the hi/lo split's errors do not sum to zero, a component
 // common to every V row then leaked into O at 2^-17 / sqrt(T), and delta = dO·O carried it into
 // every dS = p(dP - delta) of a near-uniform row — the distance-table gradients of c5, whose edge
@@ -1099,7 +1101,6 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
   };
   float m[2] = {-INFINITY, -INFINITY};
   f32x4 o[2][4], lsum[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  float lp[2] = {0.f, 0.f};   // PLO: per-lane fp32 partial row sums of the exact p (reduced at the end)
   bf16x8 ones;
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
@@ -1182,7 +1183,6 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
       if (__builtin_amdgcn_ballot_w64(tmax > m[gq] + THRESH) != 0ull) {
         const float mnew = fmaxf(m[gq], tmax);
         const float alpha = __builtin_amdgcn_exp2f(m[gq] - mnew);
-        if (PLO) lp[gq] *= alpha;
         lsum[gq] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[gq][dt] *= alpha;
@@ -1194,10 +1194,6 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           s[gq][t][r] = (STE_ABLATE & 128) ? s[gq][t][r] - mg : __builtin_amdgcn_exp2f(s[gq][t][r] - mg);
-      if (PLO) {   // the row sum of p itself (hi + lo P sums to p within 2^-16): fp32 adds, not 2 MFMAs per u
-        f32x4 t01 = (s[gq][0] + s[gq][1]) + (s[gq][2] + s[gq][3]);
-        lp[gq] += (t01[0] + t01[1]) + (t01[2] + t01[3]);
-      }
       if (gq == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1226,12 +1222,11 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel4_kernel(ste_attn_args a) {
   }
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq) {
-    // every accumulator row holds the full row sum of the P that O summed (MFMA form); the 4 lanes
-    // of a row hold partials of the exact p's sum (PLO: the LSE's)
-    const float lt = PLO ? rowsum4(lp[gq]) : lsum[gq][0];
+    // every accumulator row holds the full row sum of the P that O summed (MFMA form)
+    const float lt = lsum[gq][0];
     const int myq = qw + 16 * gq + li;
     if (myq < T) {
-      const float inv_l = 1.0f / lsum[gq][0];
+      const float inv_l = 1.0f / lt;
       bf16* O = (bf16*)a.o + (int64_t)(bT + myq) * a.ldo + h * HD;
       if (SPLIT && a.o_lo) {
         bf16* Ol = (bf16*)a.o_lo + (int64_t)(bT + myq) * a.ldolo + h * HD;
