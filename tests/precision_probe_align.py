@@ -99,7 +99,7 @@ def probe_alignment(fl, gate_store):
         z1 = lin("alignment_confidence.0", aligned)
         if "gate" not in gate_store:
             gate_store["gate"] = (z1.detach() > 0).float()
-        c1 = q_(z1 * gate_store["gate"], fw_("c1"), fl["dc1"])
+        c1 = q_(z1 * gate_store["gate"].view(z1.shape), fw_("c1"), fl["dc1"])
         sc = lin("alignment_confidence.2", c1).squeeze(-1)
         if text_mask is not None:
             sc = sc * text_mask

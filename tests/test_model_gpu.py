@@ -167,10 +167,23 @@ def test_backward_random_cotangents(tag):
     errs.sort(reverse=True)
     print(f"[{tag}] random-cotangent grad errors, bf16-exact weights (gate flips {flips}), worst:", errs[:6],
           "median:", errs[len(errs) // 2])
-    # measured worst 0.77 / 1.15 / 0.68 / 0.87 % (noalign / align / nopool / masked); the alignment
-    # head's text_projection bias (a sum over L x heads of a gated MLP's rows) sits just above 1 %
+    # measured worst 0.77 / 1.12 / 0.65 / 0.87 % (noalign / align / nopool / masked).  With the
+    # alignment head, its text_projection bias (the end of a chain of ten bf16 rounding points,
+    # summed over L x heads of a gated MLP's rows) is checked against the bf16 floor of this
+    # instance: the head re-run on the CPU with bf16 rounding at align.py's rounding points and the
+    # HIP path's gate (tests/precision_probe_align.py, same weights, inputs and cotangents), vs
+    # the same head in fp32 (measured emulated floor 1.06 %); every other tensor within 1e-2
+    bound_head = 1e-2
+    if tag == "align":
+        import precision_probe_align as PA
+        gs = {"gate": gate}
+        ref_e = PA.run(meta, z, {f: False for f in PA.FLAGS}, gs)
+        hip_e = PA.run(meta, z, {f: True for f in PA.FLAGS}, gs)
+        floor = sorted(((rel(hip_e[n], ref_e[n]), n) for n in ref_e if ref_e[n].norm() > 1e-6), reverse=True)
+        bound_head = max(1e-2, floor[0][0] + 1e-3)
+        print(f"[{tag}] alignment head same-instance bf16 floor (emulated): worst {floor[:3]}; bound {bound_head:.4f}")
     for e, n in errs:
-        assert e < (1.5e-2 if tag == "align" else 1e-2), (n, e)
+        assert e < (bound_head if n.startswith("word_level_alignment.") else 1e-2), (n, e)
     assert errs[len(errs) // 2][0] < 5e-3
 
 
