@@ -16,6 +16,9 @@ where engine.py / the kernels round, each site behind a flag:
   tdwx  the trained text layers' dW operands X in bf16 (the forward saves the hi halves)
   afa   the audio side as the HIP path runs it, coarsely: every audio Linear output and the audio
         hidden states rounded to bf16 in the forward (the audio encoder's bf16 storage)
+  tqk   (round 5) the text attention backward recomputes P from the bf16 q / k copies against the
+        fp32 forward's LSE (p = exp(bf16(q)·bf16(k)ᵀ·scale - LSE)): P no longer sums to 1 per row
+  (diagnostic, not a flag: tqk_norm = the same with an LSE of the bf16 scores, p summing to 1)
 Per-tensor error = ||g - g_fp32|| / ||g_fp32|| over the tensors test_model_gpu.py checks.
 
     python tests/precision_probe_text.py [--tag nopool] [--sets all]
@@ -39,7 +42,7 @@ from kref import bf16_exact  # noqa: E402
 from oracle import det_init, ref_model as R  # noqa: E402
 
 GOLDEN = ROOT / "tests" / "golden"
-FLAGS = ("tdy", "tdo", "tatt", "tdwx", "afa")
+FLAGS = ("tdy", "tdo", "tatt", "tdwx", "afa", "tqk")
 
 
 def bf(t):
@@ -76,28 +79,38 @@ class _LinX(torch.autograd.Function):
 
 
 class _TAttn(torch.autograd.Function):
-    """Text SDPA (masked rows: zero weights) whose backward rounds P (for dV) and dS (for dQ/dK)."""
+    """Text SDPA (masked rows: zero weights) whose backward rounds P (for dV) and dS (for dQ/dK);
+    qk: None (backward P = the forward's), "lse" (recomputed from bf16 q / k against the fp32
+    forward's LSE) or "norm" (recomputed from bf16 q / k, normalised)."""
 
     @staticmethod
-    def forward(ctx, q, k, v, add_mask, rowok):
+    def forward(ctx, q, k, v, add_mask, rowok, qk=None):
         s = q @ k.transpose(-2, -1) / math.sqrt(q.shape[-1])
         if add_mask is not None:
             s = s + add_mask
         pr = torch.softmax(s, -1)
+        pb = pr
+        if qk is not None:
+            sb = bf(q) @ bf(k).transpose(-2, -1) / math.sqrt(q.shape[-1])
+            if add_mask is not None:
+                sb = sb + add_mask
+            pb = torch.exp(sb - torch.logsumexp(s, -1, keepdim=True)) if qk == "lse" else torch.softmax(sb, -1)
         if rowok is not None:
             pr = pr * rowok
-        ctx.save_for_backward(q, k, v, pr)
-        return pr @ v
+            pb = pb * rowok
+        o = pr @ v
+        ctx.save_for_backward(q, k, v, pb, o)
+        return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, pr = ctx.saved_tensors
+        q, k, v, pr, o = ctx.saved_tensors
         sc = 1.0 / math.sqrt(q.shape[-1])
         dp = do @ v.transpose(-2, -1)
-        ds = pr * (dp - (dp * pr).sum(-1, keepdim=True))
+        ds = pr * (dp - (do * o).sum(-1, keepdim=True))   # delta = dO·O, as the kernels form it
         dv = bf(pr).transpose(-2, -1) @ do
         dsr = bf(ds)
-        return dsr @ k * sc, dsr.transpose(-2, -1) @ q * sc, dv, None, None
+        return dsr @ k * sc, dsr.transpose(-2, -1) @ q * sc, dv, None, None, None
 
 
 def probe_text_encoder(fl):
@@ -127,8 +140,9 @@ def probe_text_encoder(fl):
             qkv = g(torch.cat([lin(pre + "attention.self.query", x), lin(pre + "attention.self.key", x),
                                lin(pre + "attention.self.value", x)], -1))
             q, k, v = (t.reshape(B, L, H, d).transpose(1, 2) for t in qkv.split(cfg.hidden, -1))
-            if fl["tatt"]:
-                o = _TAttn.apply(q, k, v, add_mask, rowok)
+            if fl["tatt"] or fl["tqk"] or fl.get("tqk_norm"):
+                o = _TAttn.apply(q, k, v, add_mask, rowok,
+                                 "lse" if fl["tqk"] else ("norm" if fl.get("tqk_norm") else None))
             else:
                 s = q @ k.transpose(-2, -1) / math.sqrt(d)
                 if add_mask is not None:
@@ -187,11 +201,13 @@ def main():
             "tdwx": ["tdwx"], "afa": ["afa"], "all": list(FLAGS), "all_but_tdy": ["tdo", "tatt", "tdwx", "afa"],
             "all_but_tatt": ["tdy", "tdo", "tdwx", "afa"], "all_but_tdwx": ["tdy", "tdo", "tatt", "afa"],
             "tatt_tdwx_afa": ["tatt", "tdwx", "afa"], "tatt_afa": ["tatt", "afa"], "tdwx_afa": ["tdwx", "afa"],
-            "tdy_tdwx_afa": ["tdy", "tdwx", "afa"], "tdy_afa": ["tdy", "afa"], "tdo_tatt_tdwx_afa": ["tdo", "tatt", "tdwx", "afa"]}
+            "tdy_tdwx_afa": ["tdy", "tdwx", "afa"], "tdy_afa": ["tdy", "afa"], "tdo_tatt_tdwx_afa": ["tdo", "tatt", "tdwx", "afa"],
+            "all_but_tqk": ["tdy", "tdo", "tatt", "tdwx", "afa"], "tqk": ["tqk"],
+            "all_tqk_norm": ["tdy", "tdo", "tatt", "tdwx", "afa", "tqk_norm"]}
     if args.sets != "all":
         sets = {k: v for k, v in sets.items() if k in args.sets.split(",")}
     for name, on in sets.items():
-        g = run(meta, z, {f: f in on for f in FLAGS})
+        g = run(meta, z, {f: f in on for f in FLAGS + ("tqk_norm",)})
         errs = sorted(((float((g[n] - ref[n]).norm() / ref[n].norm()), n) for n in ref if ref[n].norm() > 1e-6),
                       reverse=True)
         print(json.dumps({"tag": args.tag, "set": name, "flags": on, "worst": [(round(e, 5), n) for e, n in errs[:4]],
