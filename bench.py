@@ -68,6 +68,8 @@ def parse(argv=None):
                     help="freeze_encoders (config 5 = none: every encoder layer trainable)")
     ap.add_argument("--fp8", action="store_true",
                     help="config 5's fp8 MFMA GEMMs: the Conformer forward GEMMs on MX-fp8 (e4m3, 32-k block scales)")
+    ap.add_argument("--fp8-bwd", action="store_true",
+                    help="with --fp8: the Conformer input-gradient GEMMs on MX-fp8 too (opt-in A/B; weight gradients stay bf16)")
     ap.add_argument("--in-batch-weight", type=float, default=0.0,
                     help="optional in-batch-negative InfoNCE over the all-gathered global batch (0 = reference loss)")
     ap.add_argument("--eval", action="store_true",
@@ -322,6 +324,7 @@ def main(argv=None):
                                    fp8_gemm=args.fp8, audio_model_name=args.audio_model,
                                    audio_embedding_dim=768 if raw else 1024)
     model.audio_cfg.layerdrop = 0.0
+    model.fp8_bwd = bool(args.fp8 and args.fp8_bwd)
     step = TrainStep(model, warmup=100, total_steps=100000, accumulation_steps=acc,
                      in_batch_weight=args.in_batch_weight, micro_batch=micro, max_text_length=args.tokens)
     nsamp, L = int(args.seconds * 16000), args.tokens
@@ -425,7 +428,9 @@ def main(argv=None):
         cname = {(3, False): "c2" if (world == 1 and glob == 64) else "c3", (5, True): "c4"}.get(
             (args.unfreeze, args.align), "custom")
     elif args.freeze == "none":
-        cname = "c5-shape (MX-fp8 Conformer fwd GEMMs)" if args.fp8 else "c5-shape (bf16 GEMMs)"
+        cname = ("c5-shape (bf16 GEMMs)" if not args.fp8 else
+                 "c5-shape (MX-fp8 Conformer fwd + input-gradient GEMMs)" if args.fp8_bwd else
+                 "c5-shape (MX-fp8 Conformer fwd GEMMs)")
     else:
         cname = "custom"
     peak = FP8_PEAK_TFLOPS if dom == "gemm_mx8_kernel" else BF16_PEAK_TFLOPS
@@ -435,7 +440,9 @@ def main(argv=None):
                    "audio–text pairs/sec (whole node), 10s@16kHz + 64-tok, 1/2/4/8 MI355X"),
         "value": round(pairs, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": scaling,
-        "vs_baseline": None, "dtype": "bf16 + mxfp8-e4m3 (Conformer fwd GEMMs)" if args.fp8 else "bf16",
+        "vs_baseline": None, "dtype": ("bf16" if not args.fp8 else
+                                       "bf16 + mxfp8-e4m3 (Conformer fwd + dX GEMMs)" if args.fp8_bwd else
+                                       "bf16 + mxfp8-e4m3 (Conformer fwd GEMMs)"),
         "data": "synthetic (SURVEY §8d waveforms + token ids), random-init weights",
         "config": {"workload": f"{cname}: global batch {glob} = {world} GPU x {acc} micro-batch(es) of {micro} pairs, "
                                f"each pair {args.seconds:g}s@16kHz audio + {L}-tok clean + {L}-tok corrupt; "

@@ -2052,14 +2052,16 @@ bool mx8_8ph_on() {
   return v == 1;
 }
 // MX-fp8 on the persistent 8-phase kernel: the e4m3 operands passed as bf16 pairs (K, lda, ldb
-// halved), compile-time epilogues for the Conformer forward GEMMs without an fp8 output copy,
-// the run-time epilogue (which also writes the fp8 copy) otherwise
+// halved), compile-time epilogues for the Conformer forward GEMMs (and, for the opt-in MX-fp8
+// input gradients, the activation-backward dz), the run-time epilogue (which also writes the fp8
+// copy) otherwise
 #define STE_MX8_SPECS(X)                                                      \
   X(EF_BIAS | EF_CBF16, STE_ACT_NONE)                            /* QKV */         \
   X(EF_CBF16, STE_ACT_NONE)                                      /* pw conv 1 */   \
   X(EF_BIAS | EF_R, STE_ACT_NONE)                                /* O, FFN out */  \
   X(EF_BIAS | EF_C2 | EF_CBF16 | EF_Q8, STE_ACT_SWISH)           /* FFN in */      \
-  X(EF_BIAS | EF_C2 | EF_CBF16 | EF_Q8 | EF_NOC, STE_ACT_SWISH)  /* FFN in, frozen: fp8 copy only */
+  X(EF_BIAS | EF_C2 | EF_CBF16 | EF_Q8 | EF_NOC, STE_ACT_SWISH)  /* FFN in, frozen: fp8 copy only */ \
+  X(EF_Z | EF_CBF16, STE_ACT_SWISH_BWD)                          /* dz (fp8_bwd A/B) */
 
 int mx8_ef(const ste_gemm_args& a, bool q_out) { return epi_flags(a) | (q_out ? EF_Q8 : 0) | (a.C ? 0 : EF_NOC); }
 

@@ -85,6 +85,12 @@ class Engine:
         """MX-fp8 forward GEMMs in the Conformer layers (model fp8_gemm=True, BASELINE config 5)."""
         return bool(getattr(self.m, "fp8_gemm", False))
 
+    @property
+    def fp8_bwd(self):
+        """Also the Conformer layers' input-gradient GEMMs (dX = dY·W) on MX-fp8 (opt-in A/B of
+        config 5: model.fp8_bwd = True together with fp8_gemm; weight gradients stay bf16)."""
+        return self.fp8 and bool(getattr(self.m, "fp8_bwd", False))
+
     WS_BYTES = 80 << 20   # split-K slabs of the weight-gradient GEMMs (largest: 7 x 3072 x 768 fp32)
 
     @property
@@ -126,6 +132,19 @@ class Engine:
         workspace is always passed and the library decides (ste_gemm_kernel)."""
         kw.setdefault("ws", self.ws)
         return ops.linear(dy, self.s.wt(wname, fused), **kw)
+
+    def _dx_mx8(self, dy, wname, fused=1, **kw):
+        """dX = dY·W on the MX-fp8 GEMM (opt-in engine.fp8_bwd, config 5): dY block-quantised along
+        its row (the reduction axis: 32 outputs per E8M0 scale) by ste_mx8_quant, W from
+        ParamStore.wtq (Wᵀ quantised along `out`).  Same epilogues as _dx, except that a bias
+        gradient is the ordered column sum of the bf16 output (run-to-run deterministic; the MX
+        kernel has no partial-sum workspace)."""
+        kw.pop("ws", None)
+        cs = kw.pop("colsum", None)
+        out = ops.linear_mx8(ops.mx8_quant(dy), self.s.wtq(wname, fused), **kw)
+        if cs is not None:
+            ops.colsum(out, cs)
+        return out
 
     def _db(self, x, bname, fused=1):
         g = self.s.fused(bname, fused, "g") if fused > 1 else self.s.g(bname)
@@ -329,6 +348,7 @@ class Engine:
         M, D, F_ = sv["x4"].shape[0], c.hidden_size, c.intermediate_size
         H = c.num_attention_heads
         tr = sv["tr"]
+        _dx = self._dx_mx8 if self.fp8_bwd else self._dx
         # final LN
         dx4 = self._e(M, D)
         dx4b = self._e(M, D, dtype=BF16)
@@ -339,13 +359,13 @@ class Engine:
             ops.layernorm_bwd_pair(self._ln_bwd_kw(sv["x4"], sv["st6"], pre + "final_layer_norm", dx=dx4, dxb=dx4b,
                                                    out_scale=0.5, dsum=s.g(pre + "ffn2.output_dense.bias")), pending)
         # FFN2
-        dz2 = self._dx(dx4b, pre + "ffn2.output_dense.weight", act=ACT_SWISH_BWD, z=sv["z2"],
+        dz2 = _dx(dx4b, pre + "ffn2.output_dense.weight", act=ACT_SWISH_BWD, z=sv["z2"],
                             out_bf16=True, colsum=s.g(pre + "ffn2.intermediate_dense.bias"))
         if tr:
             self._dw(dx4b, sv["h2"], pre + "ffn2.output_dense.weight")
         # dX GEMMs feeding an LN backward leave bf16 (as under the reference's bf16 autocast, whose
         # Linear backward returns a bf16 input gradient); the residual-stream gradient stays fp32
-        da5 = self._dx(dz2, pre + "ffn2.intermediate_dense.weight", out_bf16=True)
+        da5 = _dx(dz2, pre + "ffn2.intermediate_dense.weight", out_bf16=True)
         if tr:
             self._dw(dz2, sv["a5"], pre + "ffn2.intermediate_dense.weight")
         del dz2
@@ -355,7 +375,7 @@ class Engine:
                      drop_p=sv["p_conv"], seed=_site_seed(sv["seed"], 1))
         del da5, dx4, dx4b
         # conv module
-        dsw = self._dx(dx3b, pre + "conv_module.pointwise_conv2.weight", out_bf16=True)
+        dsw = _dx(dx3b, pre + "conv_module.pointwise_conv2.weight", out_bf16=True)
         if tr:
             self._dw(dx3b, sv["sw"], pre + "conv_module.pointwise_conv2.weight")
         dcv = self._e(M, D, dtype=BF16)
@@ -366,7 +386,7 @@ class Engine:
         ops.glu_dwconv_bwd(sv["pw1"], s.p(pre + "conv_module.depthwise_conv.weight").view(D, -1), dcv, dpw1,
                            None if gdw is None else gdw.view(D, -1), b, T)
         del dcv
-        da3 = self._dx(dpw1, pre + "conv_module.pointwise_conv1.weight", out_bf16=True)
+        da3 = _dx(dpw1, pre + "conv_module.pointwise_conv1.weight", out_bf16=True)
         if tr:
             self._dw(dpw1, sv["a3"], pre + "conv_module.pointwise_conv1.weight")
         del dpw1
@@ -376,7 +396,7 @@ class Engine:
                      dxb=dx2b, dsum=s.g(pre + "self_attn.linear_out.bias"))
         del da3, dx3, dx3b
         # attention
-        do = self._dx(dx2b, pre + "self_attn.linear_out.weight", out_bf16=True)
+        do = _dx(dx2b, pre + "self_attn.linear_out.weight", out_bf16=True)
         if tr:
             self._dw(dx2b, sv["o"], pre + "self_attn.linear_out.weight")
         del dx2b
@@ -391,7 +411,7 @@ class Engine:
                           rel_left=c.left_max_position_embeddings, rel_right=c.right_max_position_embeddings,
                           scale=1.0 / math.sqrt(D // H), dE=gE, gwork=gwork, o_lo=sv["o_lo"])
         del do, delta, gwork
-        da2 = self._dx(dqkv, pre + "self_attn.linear_q.weight", 3, out_bf16=True)
+        da2 = _dx(dqkv, pre + "self_attn.linear_q.weight", 3, out_bf16=True)
         if tr:
             self._dw(dqkv, sv["a2"], pre + "self_attn.linear_q.weight", fused=3)
             self._db(dqkv, pre + "self_attn.linear_q.bias", fused=3)
@@ -402,11 +422,11 @@ class Engine:
                      out_scale=0.5, dsum=s.g(pre + "ffn1.output_dense.bias"))
         del da2, dx2
         # FFN1
-        dz1 = self._dx(dx1b, pre + "ffn1.output_dense.weight", act=ACT_SWISH_BWD, z=sv["z1"],
+        dz1 = _dx(dx1b, pre + "ffn1.output_dense.weight", act=ACT_SWISH_BWD, z=sv["z1"],
                             out_bf16=True, colsum=s.g(pre + "ffn1.intermediate_dense.bias"))
         if tr:
             self._dw(dx1b, sv["h1"], pre + "ffn1.output_dense.weight")
-        da1 = self._dx(dz1, pre + "ffn1.intermediate_dense.weight", out_bf16=True)
+        da1 = _dx(dz1, pre + "ffn1.intermediate_dense.weight", out_bf16=True)
         if tr:
             self._dw(dz1, sv["a1"], pre + "ffn1.intermediate_dense.weight")
         del dz1

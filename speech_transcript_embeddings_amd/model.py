@@ -63,6 +63,7 @@ class EnhancedAudioTextModel(nn.Module):
                  audio_layers_to_unfreeze=5, device="cuda", spec_augment=True, fp8_gemm=False):
         super().__init__()
         self.fp8_gemm = fp8_gemm
+        self.fp8_bwd = False   # opt-in with fp8_gemm: the Conformer input-gradient GEMMs on MX-fp8 too
         self.text_cfg = _resolve(text_model_name, _TEXT_CONFIGS, TextConfig)
         self.audio_cfg = _resolve(audio_model_name, _AUDIO_CONFIGS, AudioConfig)
         with torch.device("meta"):  # no host-side weights: values are initialised in the HBM store

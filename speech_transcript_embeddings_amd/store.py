@@ -124,6 +124,7 @@ class ParamStore:
         self._versions = {}
         self._wt = {}          # (name, count) -> (Wᵀ bf16, param versions, opt_epoch) (see wt())
         self._wq = {}          # (name, count) -> ((W e4m3, E8M0 scales), versions, opt_epoch) (see wq())
+        self._wtq = {}         # (name, count) -> ((Wᵀ e4m3, E8M0 scales), the wt() tensor, its rebuild stamp)
         self._w2 = {}          # (name, count) -> ([W | W] bf16 [out, 2·in], versions, opt_epoch) (see w2())
         self._wt2 = {}         # (name, count) -> ([Wᵀ | Wᵀ], the wt() tensor, its rebuild stamp) (see wt2())
         self._wt_stamp = {}    # (name, count) -> number of wt() rebuilds (wt2 follows them)
@@ -183,6 +184,19 @@ class ParamStore:
         src = self.fused(name, count, "w") if count > 1 else self.w(name)
         q = ops.mx8_quant(src, *(ent[0] if ent is not None else (None, None)))
         self._wq[key] = (q, versions, self.opt_epoch)
+        return q
+
+    def wtq(self, name: str, count: int = 1):
+        """Wᵀ as MX-fp8 (e4m3 [in, out] + E8M0 scales [in, out/32], blocks of 32 along `out`): the B
+        operand of the opt-in MX-fp8 input-gradient GEMMs dX = dY·W (engine.fp8_bwd).  Quantised
+        from wt() and rebuilt whenever wt() rebuilds its transpose."""
+        key = (name, count)
+        wt = self.wt(name, count)
+        ent = self._wtq.get(key)
+        if ent is not None and ent[1] is wt and ent[2] == self._wt_stamp.get(key):
+            return ent[0]
+        q = ops.mx8_quant(wt, *(ent[0] if ent is not None else (None, None)))
+        self._wtq[key] = (q, wt, self._wt_stamp.get(key))
         return q
 
     def w2(self, name: str, count: int = 1):

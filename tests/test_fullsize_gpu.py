@@ -66,6 +66,8 @@ CONFIGS = {  # name: (batch, samples, tokens, unfreeze k, align, freeze_encoders
     "c4": (2, 160000, 64, 5, True, "partial", False, True),
     "c5": (1, 480000, 64, 3, False, "none", False, True),
     "c5_fp8": (1, 480000, 64, 3, False, "none", True, True),
+    # + the Conformer input-gradient GEMMs on MX-fp8 (opt-in engine.fp8_bwd)
+    "c5_fp8bwd": (1, 480000, 64, 3, False, "none", "bwd", True),
     # end to end with arbitrary fp32 master weights: the bf16 quantisation of the weights included
     "c2_fp32w": (2, 160000, 64, 3, False, "partial", False, False),
 }
@@ -131,7 +133,8 @@ def _hip_vs_oracle(cname):
     B, N, L, k, align, freeze, fp8, exact = CONFIGS[cname]
     torch.manual_seed(0)
     model = EnhancedAudioTextModel(use_word_alignment=align, text_layers_to_unfreeze=k, audio_layers_to_unfreeze=k,
-                                   freeze_encoders=freeze, device="cuda", fp8_gemm=fp8)
+                                   freeze_encoders=freeze, device="cuda", fp8_gemm=bool(fp8))
+    model.fp8_bwd = fp8 == "bwd"
     if exact:
         bf16_exact_model_(model)
     model.eval()
@@ -234,7 +237,13 @@ def test_full_size_vs_oracle(cname):
     median = errs[len(errs) // 2][0]
     print(f"[{cname}] grad rel err ({'bf16-exact' if exact else 'fp32 master'} weights): worst {errs[:6]}, "
           f"median {median:.2e}, n={len(errs)}, gate flips {flips}")
-    if fp8:
+    if fp8 == "bwd":
+        # MX-fp8 forward AND input-gradient GEMMs (dY and Wᵀ in e4m3 with 32-k block scales; the
+        # weight gradients bf16): the backward's own e4m3 rounding of every layer's dY compounds
+        # over 24 layers (measured in profiles/r5o_fp8bwd.txt; no north_star bound for fp8)
+        print(f"[{cname}] fp8 backward: median {median:.3f}, worst {errs[0][0]:.3f}")
+        assert median < 3e-1 and errs[0][0] < 6e-1, (median, errs[:5])
+    elif fp8:
         # elementwise vs fp32 with fp8-quantised forward activations (straight-through bf16
         # backward): measured median 12 %, worst 26 % (bf16 c5: 0.7 % / 2.1 %)
         assert median < 2e-1 and errs[0][0] < 4e-1, (median, errs[:5])

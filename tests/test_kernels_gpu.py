@@ -239,6 +239,27 @@ def test_gemm_mx8(ops, M, N, K):
     assert torch.equal(q2[0], q[0]) and torch.equal(q2[1], q[1])
 
 
+# the opt-in MX-fp8 input gradient (engine.fp8_bwd): dz = (dY·W) ⊙ swish'(z) with z bf16, on the
+# single-stage kernel (128 tiles) and the persistent 8-phase one (252 tiles); the dX operand pair
+# is dY quantised along its row and Wᵀ (ParamStore.wtq) quantised along `out`
+@pytest.mark.parametrize("M", [8000, 16000])
+def test_gemm_mx8_act_bwd(ops, M):
+    from speech_transcript_embeddings_amd import _lib
+    torch.manual_seed(9)
+    N, K = 1024, 4096   # the dz GEMM's shape class: K = the FFN width, N = its output
+    dh = (torch.randn(M, K, device=DEV) * 0.1).bfloat16()
+    wt = (torch.randn(N, K, device=DEV) * 0.03).bfloat16()   # Wᵀ as the MX B operand [N, K]
+    z = torch.randn(M, N, device=DEV).bfloat16()
+    dq, wq = ops.mx8_quant(dh), ops.mx8_quant(wt)
+    out = ops.linear_mx8(dq, wq, act=_lib.ACT_SWISH_BWD, z=z, out_bf16=True)
+    v = _mx8_dequant(*dq) @ _mx8_dequant(*wq).T
+    zz = z.double()
+    sg = torch.sigmoid(zz)
+    ref = v * sg * (1 + zz * (1 - sg))
+    assert rel_err(out.double(), ref) < 1e-2
+    assert rel_err(out.double(), (dh.double() @ wt.double().T) * sg * (1 + zz * (1 - sg))) < 6e-2
+
+
 def test_layernorm_mx8_output(ops):
     """LN forward's fused MX-fp8 copy (fp8_gemm: the LN feeding a Conformer Linear): scales are
     ceil(log2(amax/448)) of the fp32 output's 32-column blocks, payload = e4m3(y / 2^e)."""
