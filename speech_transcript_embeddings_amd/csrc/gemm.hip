@@ -2043,11 +2043,17 @@ extern "C" int ste_mx8_quant(const void* x, int64_t ldx, int rows, int K, void* 
 
 namespace {
 // STE_MX8_8PH=0: the single-stage gemm_mx8_kernel for every shape (A/B runs)
+// OFF in the shipped library (round 5): the persistent 8-phase MX kernel returns wrong products at
+// every shape it was planned for (>= 240 tiles), in every tree since it was added in round 3
+// (profiles/r5_mx8_bisect.py, profiles/r5q_mx8_bisect.txt); the round-3 unit test never reached
+// its compile-time epilogues and the c5 fp8 parity test runs 1,499 rows (single-stage kernel).
+// MX-fp8 GEMMs take the single-stage gemm_mx8_kernel; libste_ab.so with STE_MX8_8PH=1 keeps the
+// 8-phase form for debugging (tests/test_kernels_gpu.py::test_gemm_mx8_8ph_specs checks it)
 bool mx8_8ph_on() {
   static int v = -1;
   if (v < 0) {
     const char* e = STE_AB_ENV("STE_MX8_8PH");
-    v = (e && e[0] == '0') ? 0 : 1;
+    v = (e && e[0] == '1') ? 1 : 0;
   }
   return v == 1;
 }

@@ -239,6 +239,64 @@ def test_gemm_mx8(ops, M, N, K):
     assert torch.equal(q2[0], q[0]) and torch.equal(q2[1], q[1])
 
 
+# every compile-time epilogue of the persistent 8-phase MX kernel (STE_MX8_SPECS) at >= 240 tiles,
+# the shapes where the library would take that kernel: against the dequantised operands in fp64.
+# The shipped library plans them on the single-stage kernel (the 8-phase MX kernel is off: its
+# products were wrong, gemm.hip mx8_8ph_on); under libste_ab.so + STE_MX8_8PH=1 this checks the
+# 8-phase form
+@pytest.mark.parametrize("spec", ["bias_bf16", "bf16", "bias_r", "ffn_in_q8", "ffn_in_q8_noc", "dz"])
+def test_gemm_mx8_8ph_specs(ops, spec):
+    import ctypes
+    from speech_transcript_embeddings_amd import _lib
+    torch.manual_seed(10)
+    M, K = 16000, 1024
+    N = 4096 if spec.startswith("ffn_in") else 1024
+    x = (torch.randn(M, K, device=DEV) * 0.5).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.03).bfloat16()
+    xq, wq = ops.mx8_quant(x), ops.mx8_quant(w)
+    v = _mx8_dequant(*xq) @ _mx8_dequant(*wq).T
+    bias = torch.randn(N, device=DEV)
+    kw, q = {}, None
+    if spec == "bias_bf16":
+        kw = dict(bias=bias, out_bf16=True)
+        ref = v + bias.double()
+    elif spec == "bf16":
+        kw = dict(out_bf16=True)
+        ref = v
+    elif spec == "bias_r":
+        r = torch.randn(M, N, device=DEV)
+        kw = dict(bias=bias, residual=r)
+        ref = v + bias.double() + r.double()
+    elif spec.startswith("ffn_in"):
+        pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        q = (torch.empty(M, N, device=DEV, dtype=torch.uint8), torch.empty(M, N // 32, device=DEV, dtype=torch.uint8))
+        kw = dict(bias=bias, act=_lib.ACT_SWISH, out_bf16=True, pre_out=pre, q_out=q)
+        if spec.endswith("noc"):
+            kw["out"] = False
+        zz = v + bias.double()
+        ref = zz * torch.sigmoid(zz)
+    else:
+        z = torch.randn(M, N, device=DEV).bfloat16()
+        kw = dict(act=_lib.ACT_SWISH_BWD, z=z, out_bf16=True)
+        zz = z.double()
+        sg = torch.sigmoid(zz)
+        ref = v * sg * (1 + zz * (1 - sg))
+    args = _lib.GemmArgs(M=M, N=N, K=K, batch=1, a_kc=1, b_kc=1, A=1, B=1, lda=K, ldb=K, ldc=N, alpha=1.0,
+                         C=0 if kw.get("out") is False else 1, c_bf16=int(bool(kw.get("out_bf16"))),
+                         bias=1 if "bias" in kw else 0, R=1 if "residual" in kw else 0, ldr=N,
+                         C2=1 if "pre_out" in kw else 0, ldc2=N, Z=1 if "z" in kw else 0, ldz=N,
+                         act=kw.get("act", 0))
+    eight = int(_lib.fn("ste_gemm_mx8_kernel")(ctypes.byref(args), int(q is not None)))
+    assert eight == (1 if _lib.AB_BUILD and _lib.ab_env("STE_MX8_8PH", "0") == "1" else 0), eight
+    y = ops.linear_mx8(xq, wq, **kw)
+    if y is not False and kw.get("out") is not False:
+        assert rel_err(y.double(), ref) < (1e-2 if kw.get("out_bf16") else 1e-4), spec
+    if spec.startswith("ffn_in"):
+        if not spec.endswith("noc"):
+            assert rel_err(pre.double(), v + bias.double()) < 1e-2
+        assert rel_err(_mx8_dequant(*q), ref) < 5e-2
+
+
 # the opt-in MX-fp8 input gradient (engine.fp8_bwd): dz = (dY·W) ⊙ swish'(z) with z bf16, on the
 # single-stage kernel (128 tiles) and the persistent 8-phase one (252 tiles); the dX operand pair
 # is dY quantised along its row and Wᵀ (ParamStore.wtq) quantised along `out`
