@@ -944,6 +944,10 @@ template <int OFF>
 STE_DEV void ds_u8_hi(int& r, uint32_t addr) {
   asm volatile("ds_read_u8_d16_hi %0, %1 offset:%2" : "+v"(r) : "v"(addr), "i"(OFF) : "memory");
 }
+template <int OFF>
+STE_DEV void ds_u8(int& r, uint32_t addr) {
+  asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF) : "memory");
+}
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4m __attribute__((ext_vector_type(4)));
 // the MX operand of row rb + (l & 15): bytes k 16g..16g+15 and 64+16g.. of its swizzled 128-B row
@@ -963,10 +967,14 @@ template <int N, typename F>
 STE_DEV void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
-// scales: byte 2*(X&1) of sx / 2*(Y&1) of sy (see ds_u8_lo / ds_u8_hi)
+// scales: each in byte 0 of its own register (ds_read_u8), read with scale-select 0 — the form the
+// single-stage kernel (and the lane/scale probe) uses.  Round 5: the first form packed two scales
+// per register (ds_read_u8_d16 / _d16_hi) and picked byte 2 with the builtin's scale-select
+// argument, which read a zero byte (a 2^-127 scale) for every odd row / column group: 3/4 of
+// every tile came out ~0 since the kernel was added (profiles/r5q_mx8_bisect.txt, r5_mx8_diag.py)
 template <int X, int Y>
 STE_DEV f32x4 mfma_mx(const i32x8& x, const i32x8& y, f32x4 c, int sx, int sy) {
-  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(x, y, c, 0, 0, 2 * (X & 1), sx, 2 * (Y & 1), sy);
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(x, y, c, 0, 0, 0, sx, 0, sy);
 }
 }  // namespace ph8
 
@@ -1253,7 +1261,7 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p, M
       // MX: the K-tile's 12 scale bytes of this lane in 6 registers, read with phase 0's fragments
       // (S(t) is staged with A-half 0 of K-tile t and retired by the same waits): sca[i >> 1] holds
       // A row group i (rows wm*128 + 16i..), scb[j >> 1] B column group j
-      int sca[4] = {0, 0, 0, 0}, scb[2] = {0, 0};
+      int sca[8] = {0, 0, 0, 0, 0, 0, 0, 0}, scb[4] = {0, 0, 0, 0};
       if constexpr (MX) {
         typedef __attribute__((address_space(3))) char lds_char_t;
         // the lane id regenerated (mbcnt) behind an opaque copy each K-tile: the addresses are rebuilt
@@ -1264,12 +1272,12 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p, M
         const uint32_t sbase = (uint32_t)(uintptr_t)(lds_char_t*)smem + SC_OFF + (t & 1) * SC_STAGE + (ln >> 4) +
                                (ln & 15) * 4;
         const uint32_t aa = sbase + wm * 512, ab = sbase + 1024 + wn * 128;
-        ds_u8_lo<0>(sca[0], aa);    ds_u8_hi<64>(sca[0], aa);
-        ds_u8_lo<128>(sca[1], aa);  ds_u8_hi<192>(sca[1], aa);
-        ds_u8_lo<256>(sca[2], aa);  ds_u8_hi<320>(sca[2], aa);
-        ds_u8_lo<384>(sca[3], aa);  ds_u8_hi<448>(sca[3], aa);
-        ds_u8_lo<0>(scb[0], ab);    ds_u8_hi<64>(scb[0], ab);
-        ds_u8_lo<512>(scb[1], ab);  ds_u8_hi<576>(scb[1], ab);
+        ds_u8<0>(sca[0], aa);    ds_u8<64>(sca[1], aa);
+        ds_u8<128>(sca[2], aa);  ds_u8<192>(sca[3], aa);
+        ds_u8<256>(sca[4], aa);  ds_u8<320>(sca[5], aa);
+        ds_u8<384>(sca[6], aa);  ds_u8<448>(sca[7], aa);
+        ds_u8<0>(scb[0], ab);    ds_u8<64>(scb[1], ab);
+        ds_u8<512>(scb[2], ab);  ds_u8<576>(scb[3], ab);
       }
       // ---- phase 0
       if constexpr (MX) {
@@ -1299,8 +1307,8 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p, M
           constexpr int i = decltype(ic)::value;
           static_for<2>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            acc[i][j] = SW ? mfma_mx<j, i>(mb0[j], ma0[i], acc[i][j], scb[0], sca[i >> 1])
-                           : mfma_mx<i, j>(ma0[i], mb0[j], acc[i][j], sca[i >> 1], scb[0]);
+            acc[i][j] = SW ? mfma_mx<j, i>(mb0[j], ma0[i], acc[i][j], scb[j], sca[i])
+                           : mfma_mx<i, j>(ma0[i], mb0[j], acc[i][j], sca[i], scb[j]);
           });
         });
       } else {
@@ -1333,8 +1341,8 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p, M
           constexpr int i = decltype(ic)::value;
           static_for<2>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            acc[i][2 + j] = SW ? mfma_mx<j, i>(mb1[j], ma0[i], acc[i][2 + j], scb[1], sca[i >> 1])
-                               : mfma_mx<i, j>(ma0[i], mb1[j], acc[i][2 + j], sca[i >> 1], scb[1]);
+            acc[i][2 + j] = SW ? mfma_mx<j, i>(mb1[j], ma0[i], acc[i][2 + j], scb[2 + j], sca[i])
+                               : mfma_mx<i, j>(ma0[i], mb1[j], acc[i][2 + j], sca[i], scb[2 + j]);
           });
         });
       } else {
@@ -1369,8 +1377,8 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p, M
           constexpr int i = decltype(ic)::value;
           static_for<2>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            acc[4 + i][2 + j] = SW ? mfma_mx<j, i>(mb1[j], ma1[i], acc[4 + i][2 + j], scb[1], sca[2 + (i >> 1)])
-                                   : mfma_mx<i, j>(ma1[i], mb1[j], acc[4 + i][2 + j], sca[2 + (i >> 1)], scb[1]);
+            acc[4 + i][2 + j] = SW ? mfma_mx<j, i>(mb1[j], ma1[i], acc[4 + i][2 + j], scb[2 + j], sca[4 + i])
+                                   : mfma_mx<i, j>(ma1[i], mb1[j], acc[4 + i][2 + j], sca[4 + i], scb[2 + j]);
           });
         });
       } else {
@@ -1393,8 +1401,8 @@ __global__ __launch_bounds__(ph8::NT, 1) void gemm_8ph_kernel(ste_gemm_args p, M
           constexpr int i = decltype(ic)::value;
           static_for<2>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            acc[4 + i][j] = SW ? mfma_mx<j, i>(mb0[j], ma1[i], acc[4 + i][j], scb[0], sca[2 + (i >> 1)])
-                               : mfma_mx<i, j>(ma1[i], mb0[j], acc[4 + i][j], sca[2 + (i >> 1)], scb[0]);
+            acc[4 + i][j] = SW ? mfma_mx<j, i>(mb0[j], ma1[i], acc[4 + i][j], scb[j], sca[4 + i])
+                               : mfma_mx<i, j>(ma1[i], mb0[j], acc[4 + i][j], sca[4 + i], scb[j]);
           });
         });
       } else {
