@@ -240,9 +240,10 @@ def test_full_size_vs_oracle(cname):
     if fp8 == "bwd":
         # MX-fp8 forward AND input-gradient GEMMs (dY and Wᵀ in e4m3 with 32-k block scales; the
         # weight gradients bf16): the backward's own e4m3 rounding of every layer's dY compounds
-        # over 24 layers (measured in profiles/r5o_fp8bwd.txt; no north_star bound for fp8)
+        # over 24 layers — measured median 14.5 %, worst 34.5 % against the forward-only fp8's
+        # 12 % / 29 % (profiles/r5o_fullsize.log; north_star states no fp8 bound)
         print(f"[{cname}] fp8 backward: median {median:.3f}, worst {errs[0][0]:.3f}")
-        assert median < 3e-1 and errs[0][0] < 6e-1, (median, errs[:5])
+        assert median < 2e-1 and errs[0][0] < 4.5e-1, (median, errs[:5])
     elif fp8:
         # elementwise vs fp32 with fp8-quantised forward activations (straight-through bf16
         # backward): measured median 12 %, worst 26 % (bf16 c5: 0.7 % / 2.1 %)
