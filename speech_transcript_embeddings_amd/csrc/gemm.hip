@@ -971,7 +971,9 @@ STE_DEV void static_for(F&& f) {
 // single-stage kernel (and the lane/scale probe) uses.  Round 5: the first form packed two scales
 // per register (ds_read_u8_d16 / _d16_hi) and picked byte 2 with the builtin's scale-select
 // argument, which read a zero byte (a 2^-127 scale) for every odd row / column group: 3/4 of
-// every tile came out ~0 since the kernel was added (profiles/r5q_mx8_bisect.txt, r5_mx8_diag.py)
+// every tile came out ~0 since the kernel was added (profiles/r5q_mx8_bisect.txt, r5_mx8_diag.py).
+// The six extra registers cost 9-26 spilled VGPRs in the MX instantiations; the kernel still runs
+// the c5 fp8 step 2.7 % faster than the single-stage one (profiles/r5t_*)
 template <int X, int Y>
 STE_DEV f32x4 mfma_mx(const i32x8& x, const i32x8& y, f32x4 c, int sx, int sy) {
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(x, y, c, 0, 0, 0, sx, 0, sy);
@@ -2051,17 +2053,16 @@ extern "C" int ste_mx8_quant(const void* x, int64_t ldx, int rows, int K, void* 
 
 namespace {
 // STE_MX8_8PH=0: the single-stage gemm_mx8_kernel for every shape (A/B runs)
-// OFF in the shipped library (round 5): the persistent 8-phase MX kernel returns wrong products at
-// every shape it was planned for (>= 240 tiles), in every tree since it was added in round 3
-// (profiles/r5_mx8_bisect.py, profiles/r5q_mx8_bisect.txt); the round-3 unit test never reached
-// its compile-time epilogues and the c5 fp8 parity test runs 1,499 rows (single-stage kernel).
-// MX-fp8 GEMMs take the single-stage gemm_mx8_kernel; libste_ab.so with STE_MX8_8PH=1 keeps the
-// 8-phase form for debugging (tests/test_kernels_gpu.py::test_gemm_mx8_8ph_specs checks it)
+// Round 5: until the scale-select fix (mfma_mx) the persistent 8-phase MX kernel returned wrong
+// products at every shape it was planned for (>= 240 tiles), in every tree since round 3
+// (profiles/r5q_mx8_bisect.txt); tests/test_kernels_gpu.py::test_gemm_mx8_8ph_specs now checks
+// each of its compile-time epilogues there.  libste_ab.so with STE_MX8_8PH=0: the single-stage
+// gemm_mx8_kernel for every MX GEMM (A/B)
 bool mx8_8ph_on() {
   static int v = -1;
   if (v < 0) {
     const char* e = STE_AB_ENV("STE_MX8_8PH");
-    v = (e && e[0] == '1') ? 1 : 0;
+    v = (e && e[0] == '0') ? 0 : 1;
   }
   return v == 1;
 }

@@ -240,10 +240,10 @@ def test_gemm_mx8(ops, M, N, K):
 
 
 # every compile-time epilogue of the persistent 8-phase MX kernel (STE_MX8_SPECS) at >= 240 tiles,
-# the shapes where the library would take that kernel: against the dequantised operands in fp64.
-# The shipped library plans them on the single-stage kernel (the 8-phase MX kernel is off: its
-# products were wrong, gemm.hip mx8_8ph_on); under libste_ab.so + STE_MX8_8PH=1 this checks the
-# 8-phase form
+# the shapes where the library takes that kernel: against the dequantised operands in fp64 (round
+# 5: its scale-select bug had made 3/4 of every tile ~0 since round 3, unseen because no test
+# reached these epilogues; libste_ab.so + STE_MX8_8PH=0 runs the same checks on the single-stage
+# kernel)
 @pytest.mark.parametrize("spec", ["bias_bf16", "bf16", "bias_r", "ffn_in_q8", "ffn_in_q8_noc", "dz"])
 def test_gemm_mx8_8ph_specs(ops, spec):
     import ctypes
@@ -287,7 +287,7 @@ def test_gemm_mx8_8ph_specs(ops, spec):
                          C2=1 if "pre_out" in kw else 0, ldc2=N, Z=1 if "z" in kw else 0, ldz=N,
                          act=kw.get("act", 0))
     eight = int(_lib.fn("ste_gemm_mx8_kernel")(ctypes.byref(args), int(q is not None)))
-    assert eight == (1 if _lib.AB_BUILD and _lib.ab_env("STE_MX8_8PH", "0") == "1" else 0), eight
+    assert eight == (0 if _lib.ab_env("STE_MX8_8PH", "1") == "0" else 1), eight
     y = ops.linear_mx8(xq, wq, **kw)
     if y is not False and kw.get("out") is not False:
         assert rel_err(y.double(), ref) < (1e-2 if kw.get("out_bf16") else 1e-4), spec
