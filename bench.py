@@ -70,6 +70,9 @@ def parse(argv=None):
                     help="config 5's fp8 MFMA GEMMs: the Conformer forward GEMMs on MX-fp8 (e4m3, 32-k block scales)")
     ap.add_argument("--fp8-bwd", action="store_true",
                     help="with --fp8: the Conformer input-gradient GEMMs on MX-fp8 too (opt-in A/B; weight gradients stay bf16)")
+    ap.add_argument("--overlap-optimizer", action="store_true",
+                    help="clip + AdamW on a stream of their own, overlapped with the next step's forward "
+                         "(TrainStep(overlap_optimizer=True); opt-in A/B, DESIGN §3)")
     ap.add_argument("--in-batch-weight", type=float, default=0.0,
                     help="optional in-batch-negative InfoNCE over the all-gathered global batch (0 = reference loss)")
     ap.add_argument("--eval", action="store_true",
@@ -326,7 +329,8 @@ def main(argv=None):
     model.audio_cfg.layerdrop = 0.0
     model.fp8_bwd = bool(args.fp8 and args.fp8_bwd)
     step = TrainStep(model, warmup=100, total_steps=100000, accumulation_steps=acc,
-                     in_batch_weight=args.in_batch_weight, micro_batch=micro, max_text_length=args.tokens)
+                     in_batch_weight=args.in_batch_weight, micro_batch=micro, max_text_length=args.tokens,
+                     overlap_optimizer=args.overlap_optimizer)
     nsamp, L = int(args.seconds * 16000), args.tokens
     # resident synthetic inputs, a different shard per rank and micro-batch
     data = [synthetic_batch(micro, nsamp, L, device=f"cuda:{local}", seed=k, rank=rank) for k in range(acc)]
@@ -401,8 +405,11 @@ def main(argv=None):
     achieved = fl / tm / 1e12
     gemm_time = sum(a[2] for a in agg.values()) / args.trace_steps
     hagg = {}
+    # the optimizer's launches (Σg², AdamW) on its own stream with overlap_optimizer: they share
+    # the chip with the next step's forward, so their event intervals are in-step times
+    opt_sid = step._opt_stream.cuda_stream if getattr(step, "_opt_stream", None) is not None else None
     for name, nb, e0, e1, sid in htrace:
-        if sid != own:
+        if sid != own and not (sid == opt_sid and name in ("adamw", "sumsq")):
             continue
         a = hagg.setdefault(name, [0, 0.0, 0.0])
         a[0] += 1

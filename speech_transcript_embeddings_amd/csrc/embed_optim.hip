@@ -120,6 +120,20 @@ __global__ __launch_bounds__(64) void sumsq_final_kernel(const double* part, int
   if (threadIdx.x == 0) acc[0] += t;
 }
 
+// One element of clip + AdamW.  Every path of adamw_kernel (two groups a stride apart, one group,
+// scalar tail) goes through this, with the roundings spelled out (explicit fma, no contraction), so
+// an element's result does not depend on which path it falls in: the update is then invariant to
+// how the flat buffer is split into launches (TrainStep(overlap_optimizer=True) runs it per block).
+__device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v, float coef, float decay, float b1,
+                                           float b2, float step, float bc2_sqrt, float eps) {
+#pragma clang fp contract(off)
+  const float gc = g * coef;
+  m = __builtin_fmaf(b1, m, (1.f - b1) * gc);
+  v = __builtin_fmaf(b2, v, ((1.f - b2) * gc) * gc);
+  const float den = sqrtf(v) / bc2_sqrt + eps;
+  p = __builtin_fmaf(-step, m / den, p * decay);
+}
+
 __global__ __launch_bounds__(NT) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                  float* __restrict__ m, float* __restrict__ v, bf16* __restrict__ pb,
                                                  int64_t n, float lr, float b1, float b2, float eps, float wd,
@@ -131,18 +145,18 @@ __global__ __launch_bounds__(NT) void adamw_kernel(float* __restrict__ p, const 
   }
   const float step = lr / bc1;
   const float decay = 1.f - lr * wd;
-  auto upd4 = [&](f32x4& pv, f32x4 gv, f32x4& mv, f32x4& vv) {
-    gv *= coef;
+  auto upd4 = [&](f32x4& pv, const f32x4& gv, f32x4& mv, f32x4& vv) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      pv[e] *= decay;
-      mv[e] = b1 * mv[e] + (1.f - b1) * gv[e];
-      vv[e] = b2 * vv[e] + (1.f - b2) * gv[e] * gv[e];
-      pv[e] -= step * mv[e] / (sqrtf(vv[e]) / bc2_sqrt + eps);
+      float pe = pv[e], me = mv[e], ve = vv[e];
+      adamw_elem(pe, gv[e], me, ve, coef, decay, b1, b2, step, bc2_sqrt, eps);
+      pv[e] = pe;
+      mv[e] = me;
+      vv[e] = ve;
     }
   };
   // bulk: two 4-element groups a grid-stride apart per iteration, all eight 16-B loads issued before
-  // the arithmetic (more bytes in flight per lane than the one-group loop: 4.75 -> ? TB/s in-step)
+  // the arithmetic (more bytes in flight per lane than the one-group loop)
   const int64_t stride = (int64_t)gridDim.x * NT * 4;
   int64_t i = ((int64_t)blockIdx.x * NT + threadIdx.x) * 4;
   for (; i + stride + 3 < n; i += 2 * stride) {
@@ -166,28 +180,21 @@ __global__ __launch_bounds__(NT) void adamw_kernel(float* __restrict__ p, const 
   for (; i < n; i += stride) {
     if (i + 3 < n) {
       f32x4 pv = *reinterpret_cast<f32x4*>(p + i);
-      const f32x4 gv = *reinterpret_cast<const f32x4*>(g + i) * coef;
+      const f32x4 gv = *reinterpret_cast<const f32x4*>(g + i);
       f32x4 mv = *reinterpret_cast<f32x4*>(m + i);
       f32x4 vv = *reinterpret_cast<f32x4*>(v + i);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        pv[e] *= decay;
-        mv[e] = b1 * mv[e] + (1.f - b1) * gv[e];
-        vv[e] = b2 * vv[e] + (1.f - b2) * gv[e] * gv[e];
-        pv[e] -= step * mv[e] / (sqrtf(vv[e]) / bc2_sqrt + eps);
-      }
+      upd4(pv, gv, mv, vv);
       *reinterpret_cast<f32x4*>(p + i) = pv;
       *reinterpret_cast<f32x4*>(m + i) = mv;
       *reinterpret_cast<f32x4*>(v + i) = vv;
       if (pb) store_bf16x4(pb + i, pv);
     } else {
       for (int64_t j = i; j < n; ++j) {
-        const float gv = g[j] * coef;
-        float pv = p[j] * decay;
-        m[j] = b1 * m[j] + (1.f - b1) * gv;
-        v[j] = b2 * v[j] + (1.f - b2) * gv * gv;
-        pv -= step * m[j] / (sqrtf(v[j]) / bc2_sqrt + eps);
+        float pv = p[j], mv = m[j], vv = v[j];
+        adamw_elem(pv, g[j], mv, vv, coef, decay, b1, b2, step, bc2_sqrt, eps);
         p[j] = pv;
+        m[j] = mv;
+        v[j] = vv;
         if (pb) pb[j] = (bf16)pv;
       }
     }

@@ -102,6 +102,18 @@ class Engine:
             w = self._ws[key] = torch.empty(self.WS_BYTES // 4, device=self.s.device, dtype=F32)
         return w
 
+    def _await_params(self, *names):
+        """Order the current stream after the overlapped optimizer's update of these parameter
+        blocks (TrainStep(overlap_optimizer=True) sets param_events; waiting on a finished event
+        costs nothing)."""
+        evs = getattr(self, "param_events", None)
+        if evs:
+            cur = torch.cuda.current_stream(self.s.device)
+            for n in names:
+                ev = evs.get(n)
+                if ev is not None:
+                    cur.wait_event(ev)
+
     def _side_stream(self):
         if not (self.overlap and self.s.device.type == "cuda"):
             return None
@@ -171,7 +183,9 @@ class Engine:
         SpecAugment needs them, one device->host sync)."""
         if self.raw_audio:
             from . import wav2vec2
+            self._await_params("audio", "late")
             return wav2vec2.forward(self, feats, mask_i64, train, base_seed, ctx, save, lengths=lengths)
+        self._await_params("audio")   # feature projection (and SpecAugment's embedding)
         c = self.acfg
         b, T, fin = feats.shape
         M = b * T
@@ -206,9 +220,13 @@ class Engine:
         order = [i for i in range(nl) if run[i]]
         layers = [None] * nl
         pre1 = None
+        lo = next((i for i in range(nl)
+                   if self.s.trainable_layer(f"audio_encoder.encoder.layers.{i}.ffn1_layer_norm.weight")), nl)
         for k, i in enumerate(order):
             last = i == nl - 1
             nxt = order[k + 1] if (self.ln_pair and k + 1 < len(order)) else None
+            if i >= lo or (nxt is not None and nxt >= lo):
+                self._await_params("late")   # the trainable layers (this one, or the next one's LN)
             x, xb, sv, pre1 = self._conformer_fwd(i, x, b, T, maskf, mask32, train, _site_seed(base_seed, 100 + i),
                                                   last, save, pre1=pre1, nxt=nxt)
             layers[i] = sv if save else None
@@ -491,6 +509,7 @@ class Engine:
 
     # ================================================================= text
     def text_forward(self, ids, mask_i64, train, base_seed, ctx, save=True):
+        self._await_params("text")
         c = self.tcfg
         s = self.s
         nb, L = ids.shape
@@ -968,6 +987,7 @@ class Engine:
         return kv, seqb
 
     def heads_forward(self, th, thb, ah, ahb, train, base_seed, ctx):
+        self._await_params("late", "text")
         m = self.m
         nb, L = ctx["t_nb"], ctx["t_L"]
         b = nb // 2

@@ -287,6 +287,20 @@ class ParamStore:
             ev.record(stream)
         self._prebuilt = (ev, stream, set())
 
+    def refresh_transposes_in(self, runs):
+        """refresh_transposes for the weights inside the flat-buffer runs [(a, b), ...], on the
+        current stream (TrainStep(overlap_optimizer=True): the optimizer stream, right after the
+        AdamW of that block, so the block's event covers its transposes too and no consumer waits
+        on a global rebuild event)."""
+        if self.device.type != "cuda":
+            return
+        self._prebuilt = None
+        inside = lambda k: any(a <= self.slots[k[0]].offset < b for a, b in runs)  # noqa: E731
+        for cache, build in ((self._wt, self.wt), (self._w2, self.w2)):
+            for k in [k for k, ent in cache.items() if ent[2] != self.opt_epoch
+                      and self.slots[k[0]].segment in ("enc", "head") and inside(k)]:
+                build(*k)
+
     def _wait_prebuilt(self):
         pb = getattr(self, "_prebuilt", None)
         if pb is None:

@@ -160,22 +160,44 @@ class FusedAdamW:
         reads the on-device Σg² (host sync)."""
         return math.sqrt(float(self.sumsq.item()))
 
-    def step(self, lr_factor: float = 1.0):
+    def step(self, lr_factor: float = 1.0, phases=None, on_phase=None):
+        """Clip + AdamW.  phases: [(name, [(a, b), ...]), ...] — the update split into flat-buffer
+        runs launched phase by phase, with a CUDA event recorded after each (returned as
+        {name: event}), so the next forward can wait for just the parameters it is about to read
+        (TrainStep(overlap_optimizer=True)).  AdamW is elementwise, so the split changes no value;
+        each run takes its group's learning rate from the segment it lies in; on_phase(runs) runs
+        after each phase's update, before its event (the block's cached transposes)."""
         st = self.store
         self.t += 1
         self.last_factor = lr_factor
         self.sumsq.zero_()
         if self.max_norm is not None:
             ops.sumsq(st.grad[: st.n_grad], self.sumsq, self.sumsq_part)
-        for gr in self.groups:
-            a, b = gr["range"]
-            if b <= a:
-                continue
+
+        def upd(a, b, lr):
             ops.adamw(st.master[a:b], st.grad[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b], st.shadow[a:b],
-                      lr=gr["lr"] * lr_factor, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps, wd=self.wd,
+                      lr=lr * lr_factor, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps, wd=self.wd,
                       step=self.t, sumsq_acc=self.sumsq if self.max_norm is not None else None,
                       max_norm=self.max_norm or 1.0)
-        st.mark_synced()
+        events = {}
+        if phases is None:
+            for gr in self.groups:
+                a, b = gr["range"]
+                if b > a:
+                    upd(a, b, gr["lr"])
+            st.mark_synced()
+            return events
+        st.mark_synced()   # first: on_phase sees this step's weights as the ones to rebuild from
+        for name, runs in phases:
+            for a, b in runs:
+                gr = next(g for g in self.groups if g["range"][0] <= a and b <= g["range"][1])
+                upd(a, b, gr["lr"])
+            if on_phase is not None:
+                on_phase(runs)
+            ev = torch.cuda.Event()
+            ev.record()
+            events[name] = ev
+        return events
 
     def zero_grad(self):
         self.store.grad.zero_()
@@ -520,7 +542,8 @@ class TrainStep:
 
     def __init__(self, model: EnhancedAudioTextModel, lr=2.1e-3, warmup=100, total_steps=10000, temperature=0.1,
                  alignment_weight=0.5, corrupt_gamma=0.35, max_norm=1.0, pad_value=1.0, gather_embeddings=True,
-                 accumulation_steps=1, in_batch_weight=0.0, micro_batch=None, max_text_length=None):
+                 accumulation_steps=1, in_batch_weight=0.0, micro_batch=None, max_text_length=None,
+                 overlap_optimizer=False):
         """accumulation_steps (ref train_epoch :1064-1117): each call is one micro-batch whose loss
         gradient is scaled by 1/accumulation_steps and summed into the flat gradient buffer; the
         data-parallel sync, clip, AdamW and scheduler step run on every accumulation_steps-th
@@ -532,7 +555,13 @@ class TrainStep:
         Data parallel: rank 0's layerdrop seed is broadcast so every rank drops the same Conformer
         layers (tf:…wav2vec2_bert…:519-522 draws one number per layer per batch).  micro_batch and
         max_text_length (the reference pads transcripts to it, ref :838-851) fix the word-table
-        exchange capacity (GradSync) up front; without them it is agreed on every optimizer step."""
+        exchange capacity (GradSync) up front; without them it is agreed on every optimizer step.
+        overlap_optimizer (CUDA): clip + AdamW run on a stream of their own, split into the
+        parameter blocks the next forward reads in order — the feature projection first, then the
+        text encoder, then the trainable Conformer layers and the heads — and that forward waits
+        for each block right before its first read, so the update of the late blocks overlaps the
+        fbank and the frozen Conformer layers.  Parameters read outside the step between steps
+        (checkpointing, evaluation on another stream): call sync() first."""
         self.model = model
         self.acc = max(1, int(accumulation_steps))
         self._micro = 0
@@ -549,6 +578,17 @@ class TrainStep:
         self.exchange = EmbeddingExchange(temperature, in_batch_weight) if self.gather_embeddings else None
         self.in_batch_weight = float(in_batch_weight)
         self.last = {}
+        st = model.store
+        self.overlap = bool(overlap_optimizer) and st.device.type == "cuda"
+        self._opt_stream = torch.cuda.Stream(device=st.device) if self.overlap else None
+        self._opt_tail = None
+        if self.overlap:
+            gs = self.gradsync
+            text = gs.ranges["text"] + gs.ranges["text_layers"]
+            if gs.words is not None:
+                text = text + [(gs.words.offset, gs.words.offset + gs.words.numel)]
+            self._phases = [("audio", gs.ranges["audio"]), ("text", sorted(text)),
+                            ("late", gs.ranges["audio_layers"] + gs.ranges["heads"])]
         self._sync_layerdrop_seed()
 
     def _sync_layerdrop_seed(self):
@@ -630,6 +670,7 @@ class TrainStep:
         ops.l2norm_bwd(tn_all[B:], nrm[B:2 * B], dtn, g_tn)
         ops.l2norm_bwd(an, nrm[2 * B:], dan, g_a)
         if self._micro == 0:
+            self._await_optimizer()   # the previous step's AdamW has read these gradients
             st.grad.zero_()
             self._ids = []
         self._ids.append(ctx["t_ids"].reshape(-1))
@@ -647,19 +688,42 @@ class TrainStep:
 
     def epoch_metrics(self):
         """train_epoch's return dict (ref :1156-1162) over the global batch, synced once."""
+        self._await_optimizer()
         out = self.exchange.epoch_metrics() if self.exchange is not None else {}
         out["optimizer_steps"] = self.opt.t
         return out
 
     def _optimizer_step(self):
-        self.gradsync.finish()
-        self.opt.step(self.sched.factor())  # reference order: optimizer.step() then scheduler.step()
-        self.sched.step()
-        # the updated weights' cached Wᵀ (dX GEMM operands) rebuild on the side stream, under
-        # the next forward
-        self.model.store.refresh_transposes(self.model.engine._side_stream())
+        eng = self.model.engine
+        if self.overlap:
+            main = torch.cuda.current_stream(self.model.store.device)
+            self._opt_stream.wait_stream(main)
+            with torch.cuda.stream(self._opt_stream):
+                self.gradsync.finish()
+                # each block's cached transposes rebuilt right after its update, under its event
+                eng.param_events = self.opt.step(self.sched.factor(), phases=self._phases,
+                                                 on_phase=self.model.store.refresh_transposes_in)
+                self.sched.step()
+                self._opt_tail = torch.cuda.Event()
+                self._opt_tail.record()
+        else:
+            self.gradsync.finish()
+            self.opt.step(self.sched.factor())  # reference order: optimizer.step() then scheduler.step()
+            self.sched.step()
+            # the updated weights' cached Wᵀ (dX GEMM operands) rebuild on the side stream, under
+            # the next forward
+            self.model.store.refresh_transposes(eng._side_stream())
         self._micro = 0
         self._ids = []
+
+    def _await_optimizer(self):
+        if self._opt_tail is not None:
+            torch.cuda.current_stream(self.model.store.device).wait_event(self._opt_tail)
+
+    def sync(self):
+        """Order the current stream after the last optimizer step (overlap_optimizer): parameters,
+        moments and gradients are then safe to read or write on it."""
+        self._await_optimizer()
 
     def flush(self):
         """Step on a partial accumulation window (ref :1064-1066 `is_last_batch`): sync the
@@ -676,10 +740,12 @@ class TrainStep:
     def optimizer_state_dict(self):
         """The optimizer state as the reference's training loop would save it after this many
         optimizer.step(); scheduler.step() pairs (group lr = the next step's scheduled lr)."""
+        self._await_optimizer()
         return self.opt.state_dict(lr_factor=self.sched.factor())
 
     def load_optimizer_state_dict(self, sd):
         """Restore moments + step count and put the warmup schedule at the same step."""
+        self._await_optimizer()
         self.opt.load_state_dict(sd)
         self.sched.step_count = self.opt.t
 

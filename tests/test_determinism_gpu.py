@@ -51,3 +51,39 @@ def test_train_step_bitwise_reproducible():
         pytest.fail(f"{int(diff.sum())} gradient entries differ between identical steps, in {bad[:12]}")
     assert torch.equal(s0, s1)                   # clip_grad_norm_'s Σg², hence the clip coefficient
     assert float(g0.abs().sum()) > 0
+
+
+@pytest.mark.timeout(600)
+def test_overlapped_optimizer_bitwise_equal():
+    """TrainStep(overlap_optimizer=True): clip + AdamW on their own stream, split into the blocks
+    the next forward reads in order, each awaited right before its first read.  Three steps at a
+    real learning rate (each step's forward reads the previous update) give bit-identical
+    weights, moments, losses and gradients to the serial optimizer — a missed wait would read a
+    half-updated weight or zero a gradient AdamW has not read yet."""
+    from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
+    from speech_transcript_embeddings_amd.train import TrainStep, synthetic_batch
+    B, N, L = 4, 64000, 32
+    out = []
+    for overlap in (False, True):
+        torch.manual_seed(0)
+        model = EnhancedAudioTextModel(use_word_alignment=True, text_layers_to_unfreeze=3, audio_layers_to_unfreeze=3,
+                                       device="cuda", spec_augment=False)
+        model.audio_cfg.layerdrop = 0.0
+        step = TrainStep(model, lr=1e-3, warmup=1, total_steps=10, micro_batch=B, max_text_length=L,
+                         overlap_optimizer=overlap)
+        batches = [synthetic_batch(B, N, L, device="cuda", seed=10 + i) for i in range(3)]
+        torch.cuda.synchronize()
+        losses = []
+        for i in range(3):                     # back to back: step i+1's forward overlaps step i's AdamW
+            torch.manual_seed(100 + i)
+            losses.append(step(*batches[i]).clone())
+        step.sync()
+        torch.cuda.synchronize()
+        st = model.store
+        out.append((torch.stack(losses), st.grad[: st.n_grad].clone(), st.master.clone(), step.opt.exp_avg.clone(),
+                    step.opt.exp_avg_sq.clone(), st.shadow.clone()))
+    (l0, g0, m0, a0, v0, s0), (l1, g1, m1, a1, v1, s1) = out
+    assert torch.equal(l0, l1), (l0.tolist(), l1.tolist())
+    assert torch.equal(g0, g1)
+    assert torch.equal(m0, m1) and torch.equal(a0, a1) and torch.equal(v0, v1) and torch.equal(s0, s1)
+    assert float((a0 != 0).sum()) > 0

@@ -1531,3 +1531,28 @@ def test_adamw_clip(ops):
               max_norm=0.05)
     assert rel_err(p, pr.detach()) < 1e-6
     assert torch.equal(pb, p.bfloat16())
+
+
+def test_adamw_split_invariant(ops):
+    """The update of an element does not depend on how the flat buffer is cut into launches (bulk
+    two-group loop, one-group loop, scalar tail all round alike): TrainStep(overlap_optimizer=True)
+    runs AdamW per parameter block and must match the one-launch-per-group update bit for bit."""
+    torch.manual_seed(9)
+    n = 3_000_011
+    p0 = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV) * 0.01
+    m0 = torch.randn(n, device=DEV) * 1e-3
+    v0 = torch.rand(n, device=DEV) * 1e-5
+    acc = torch.zeros(1, device=DEV, dtype=torch.float64)
+    ops.sumsq(g, acc)
+    kw = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, wd=0.01, step=3, sumsq_acc=acc, max_norm=1.0)
+    outs = []
+    for cuts in ([0, n], [0, 4, 1_048_580, 1_048_600, 2_999_996, n], [0, 123_456, 2_000_000, n]):
+        p, m, v = p0.clone(), m0.clone(), v0.clone()
+        pb = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+        for a, b in zip(cuts, cuts[1:]):
+            ops.adamw(p[a:b], g[a:b], m[a:b], v[a:b], pb[a:b], **kw)
+        outs.append((p, m, v, pb))
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert torch.equal(x, y)
