@@ -4,19 +4,21 @@
 // feature_extraction_seamless_m4t.py:112-138,240-301, tf:audio_utils.py:809-1017),
 // plus the collate padding of ref:training/trainer_unfreeze.py:880-921.
 //
-// Kernel 1 (one wavefront per 400-sample frame, 4 waves per block, 4 frames per wave):
+// Kernel 1 (one wavefront per 400-sample frame at a time, 4 waves per block, 4 frames per wave):
 //   x*2^15 -> remove frame mean -> pre-emphasis 0.97 (y0 *= 0.03) -> povey window
 //   -> 512-point radix-8 Stockham FFT in registers (fp32, twiddles from double sincos) -> |X|^2
-//   -> 80 kaldi-scale triangular mel filters built in mel space (sparse, per-block
-//   table) -> max(1.1920929e-7, .) -> natural log.
-// Kernel 2 (one 1024-thread block per clip, rows staged through LDS): per-mel-bin mean and
-// unbiased variance over the clip's frames exactly as numpy evaluates them on the extractor's
-// float32 log-mel array (tf:…seamless_m4t…:256-261: x.mean(0), x.var(0, ddof=1), (x - mean)/sqrt(var + 1e-7)):
-// float32 sums accumulated frame by frame in order (numpy's reduction over a non-contiguous
-// axis), IEEE float32 division and square root.  A bin whose frames are all equal (silence at
-// the log floor) therefore reproduces the reference's non-zero rounding residue bit for bit.
-// Kernel 3 (rows of many clips per block): (x - mean)/std, pad odd frame counts with
-// padding_value, stack frame pairs into 160-d rows, zero rows beyond the clip, write the mask.
+//   -> 80 kaldi-scale triangular mel filters built in mel space (sparse, taps in registers)
+//   -> max(1.1920929e-7, .) -> natural log.
+// Kernel 2 (one block per clip and group of NB mel bins, the group's columns staged into LDS):
+// per-mel-bin mean and unbiased variance over the clip's frames exactly as numpy evaluates them
+// on the extractor's float32 log-mel array (tf:…seamless_m4t…:256-261: x.mean(0), x.var(0, ddof=1),
+// (x - mean)/sqrt(var + 1e-7)): float32 sums accumulated frame by frame in order (numpy's
+// reduction over a non-contiguous axis), IEEE float32 division and square root.  A bin whose
+// frames are all equal (silence at the log floor) therefore reproduces the reference's non-zero
+// rounding residue bit for bit.  The same block then writes (x - mean)/std for its bins, pads odd
+// frame counts with padding_value, stacks frame pairs into 160-d rows, zeroes rows beyond the clip
+// and (bin group 0) writes the mask.  Clips too long for the LDS columns take the separate
+// statistics (kernel 2b) and normalise / stack (kernel 3) kernels.
 // HBM-bound: 4 B/sample in, 640 B per stacked frame + mask out.
 #include "common.h"
 #include "../../include/ste.h"
@@ -39,7 +41,7 @@ constexpr int T_TW = 0, T_WIN = 512, T_MSTART = 912, T_MLEN = 992, T_MOFF = 1072
 #include "fbank_tables.h"
 namespace {
 
-constexpr int FRAMES_PER_WAVE = 4;
+constexpr int FRAMES_PER_WAVE = 4, MEL_GROUP = 4;   // frames per wave (default; 8 / 16 in A/B builds), per mel stage
 constexpr int XPAD = NFFT + NFFT / 8;   // exchange buffer: one float2 of padding per 8
 
 STE_DEV int xpad(int i) { return i + (i >> 3); }
@@ -74,120 +76,166 @@ STE_DEV void dft8(float2 (&v)[8]) {
 // per-wave LDS buffer, twiddles e^{-2πik/512} from the fp64-built table; the input needs no
 // bit reversal and lane j ends with X[j + 64 r].  (The radix-2 version took 9 LDS round trips
 // per frame and half of the kernel's time.)
+// Everything a lane needs for every frame is loaded once per wave into registers: its 7 window
+// values, its 14 pass-2/3 twiddles and the taps of its mel filters.  The next frame's samples are
+// loaded before the current frame's FFT runs.  The wave's 4 frames leave their power spectra in
+// LDS, and then the mel stage runs for all 4 at once: lane l sums low mel l (≤ 10 taps) for each
+// of the 4 frames, and high mel 64 + (l & 15) (≤ 16 taps) for frame l >> 4.  The taps are
+// unrolled to fixed counts, zero-weighted past a filter's length, so a lane's LDS reads issue
+// together instead of one round trip per tap.  Each filter still sums its taps in order, with
+// one fma per tap.
+constexpr int LOW_TAPS = 10, HIGH_TAPS = 16;   // max taps of mels 0..63 / 64..79 (fbank_tables.h)
+
+template <int FPW>
 __global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restrict__ wav, int64_t ld_wav,
                                                          const int32_t* __restrict__ lengths, int Fmax,
                                                          float* __restrict__ work) {
   const float* tab = reinterpret_cast<const float*>(g_fbank_tab_bits);
+  const int* tabi = reinterpret_cast<const int*>(g_fbank_tab_bits);
   __shared__ float2 sbuf[4][XPAD];
-  __shared__ float2 stw[NFFT / 2];
-  __shared__ float swin[FRAME];
-  __shared__ int sm_start[NMEL], sm_len[NMEL], sm_off[NMEL];
-  __shared__ float sm_w[MAXNZ];
-  __shared__ float spow[4][NBIN + 3];
+  __shared__ float spow[4][MEL_GROUP][NBIN + 3];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int b = blockIdx.y;
-  for (int k = tid; k < NFFT / 2; k += 256) stw[k] = make_float2(tab[T_TW + 2 * k], tab[T_TW + 2 * k + 1]);
-  for (int n = tid; n < FRAME; n += 256) swin[n] = tab[T_WIN + n];
-  if (tid < NMEL) {
-    const int* ti = reinterpret_cast<const int*>(tab);
-    sm_start[tid] = ti[T_MSTART + tid];
-    sm_len[tid] = ti[T_MLEN + tid];
-    sm_off[tid] = ti[T_MOFF + tid];
-  }
-  for (int i = tid; i < MAXNZ; i += 256) sm_w[i] = tab[T_MW + i];
-  __syncthreads();
-
   const int len = lengths[b];
-  const int F = len >= FRAME ? 1 + (len - FRAME) / HOP : 0;
-  float2* buf = sbuf[w];
-  for (int fi = 0; fi < FRAMES_PER_WAVE; ++fi) {
-  const int f = (blockIdx.x * 4 + w) * FRAMES_PER_WAVE + fi;
-  if (f >= F || f >= Fmax) return;  // whole wave exits; no block barrier follows
-  const float* x = wav + (int64_t)b * ld_wav + (int64_t)f * HOP;
-  float c[7];
-  float s = 0.f;
+  const int F = min(len >= FRAME ? 1 + (len - FRAME) / HOP : 0, Fmax);
+  const int f0 = (blockIdx.x * 4 + w) * FPW;
+  if (f0 >= F) return;  // whole wave exits; this kernel has no block barrier
+
+  float win[7];
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     const int n = lane + 64 * i;
-    c[i] = n < FRAME ? x[n] * 32768.0f : 0.f;
-    s += c[i];
+    win[i] = n < FRAME ? tab[T_WIN + n] : 0.f;
   }
-  const float mean = wave_sum(s) * (1.0f / FRAME);
+  // twiddles of passes 2 and 3 (Ns = 8, 64): W512^(r (j mod Ns) 64 / Ns), r = 1..7
+  float2 tw[2][7];
 #pragma unroll
-  for (int i = 0; i < 7; ++i) c[i] = c[i] - mean;   // n >= FRAME: masked below
-  // pre-emphasis (x[n] - 0.97 x[n-1], x[0] * 0.03) and window: x[n-1] is lane-1's value, or
-  // lane 63's of the previous row for lane 0
-  float2 v[8];
+  for (int p = 0; p < 2; ++p) {
+    const int step = p == 0 ? (lane & 7) * 8 : lane;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int n = lane + 64 * i;
-    float val = 0.f;
-    if (i < 7) {
-      // lane - 1's value by DPP wave_shr:1 and lane 63's by v_readlane (no ds_bpermute round trips)
-      const float up = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, c[i]), 0x138,
-                                                                               0xF, 0xF, false));
-      const float wrap = i > 0 ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, c[i - 1]), 63))
-                               : 0.f;
-      const float prev = lane > 0 ? up : wrap;
-      if (n < FRAME) {
-        val = (n == 0) ? c[i] * (1.0f - 0.97f) : c[i] - 0.97f * prev;
-        val *= swin[n];
+    for (int r = 1; r < 8; ++r) {
+      const int k = r * step;   // < 512
+      float2 t = make_float2(tab[T_TW + 2 * (k & 255)], tab[T_TW + 2 * (k & 255) + 1]);
+      if (k & 256) t = make_float2(-t.x, -t.y);
+      tw[p][r - 1] = t;
+    }
+  }
+  // mel taps: low mel `lane`, high mel 64 + (lane & 15)
+  const int ml = lane, mh = 64 + (lane & 15);
+  const int stl = tabi[T_MSTART + ml], sth = tabi[T_MSTART + mh];
+  float wl[LOW_TAPS], wh[HIGH_TAPS];
+  {
+    const int lnl = tabi[T_MLEN + ml], ofl = tabi[T_MOFF + ml];
+    const int lnh = tabi[T_MLEN + mh], ofh = tabi[T_MOFF + mh];
+#pragma unroll
+    for (int i = 0; i < LOW_TAPS; ++i) wl[i] = i < lnl ? tab[T_MW + ofl + i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < HIGH_TAPS; ++i) wh[i] = i < lnh ? tab[T_MW + ofh + i] : 0.f;
+  }
+
+  float2* buf = sbuf[w];
+  const float* xb = wav + (int64_t)b * ld_wav;
+  float c[7];
+  auto load = [&](int f) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int n = lane + 64 * i;
+      c[i] = (f < F && n < FRAME) ? xb[(int64_t)f * HOP + n] : 0.f;
+    }
+  };
+  // the reference logs the float64 mel energies and rounds to float32 (np.log(...).astype(float32)).
+  // At the floor (silent frames) that exact constant matters: a clip's identical rows leave
+  // numpy's CMVN rounding residue in the output, so it is the float64 log rounded once; above
+  // it, fp32 logf (<= 1 ulp) is far inside the FFT's own fp32 rounding
+  auto logmel = [](float e) { return e > MEL_FLOOR ? logf(e) : LOG_MEL_FLOOR; };
+  load(f0);
+  for (int g0 = f0; g0 < min(f0 + FPW, F); g0 += MEL_GROUP) {
+#pragma unroll
+  for (int q = 0; q < MEL_GROUP; ++q) {
+    float x[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) x[i] = c[i] * 32768.0f;
+    load(g0 + q + 1);   // in flight under this frame's FFT (zeros past the clip: no read)
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) s += x[i];
+    const float mean = wave_sum(s) * (1.0f / FRAME);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) x[i] = x[i] - mean;   // n >= FRAME: masked below
+    // pre-emphasis (x[n] - 0.97 x[n-1], x[0] * 0.03) and window: x[n-1] is lane-1's value, or
+    // lane 63's of the previous row for lane 0
+    float2 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int n = lane + 64 * i;
+      float val = 0.f;
+      if (i < 7) {
+        // lane - 1's value by DPP wave_shr:1 and lane 63's by v_readlane (no ds_bpermute round trips)
+        const float up = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x[i]), 0x138,
+                                                                                 0xF, 0xF, false));
+        const float wrap =
+            i > 0 ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x[i - 1]), 63)) : 0.f;
+        const float prev = lane > 0 ? up : wrap;
+        if (n < FRAME) {
+          val = (n == 0) ? x[i] * (1.0f - 0.97f) : x[i] - 0.97f * prev;
+          val *= win[i];
+        }
+      }
+      v[i] = make_float2(val, 0.f);
+    }
+    // Stockham radix-8: pass Ns in {1, 8, 64}; lane j reads points j + 64 r, twiddles by
+    // W512^(r (j mod Ns) 64/Ns), runs dft8 and writes (j/Ns) Ns 8 + (j mod Ns) + r Ns
+#pragma unroll
+    for (int pass = 0; pass < 3; ++pass) {
+      const int Ns = pass == 0 ? 1 : pass == 1 ? 8 : 64;
+      if (pass > 0) {
+#pragma unroll
+        for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tw[pass - 1][r - 1]);
+      }
+      dft8(v);
+      if (pass < 2) {
+        const int base = (lane / Ns) * Ns * 8 + (lane & (Ns - 1));
+#pragma unroll
+        for (int r = 0; r < 8; ++r) buf[xpad(base + r * Ns)] = v[r];
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = buf[xpad(lane + 64 * r)];
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
       }
     }
-    v[i] = make_float2(val, 0.f);
-  }
-  // Stockham radix-8: pass Ns in {1, 8, 64}; lane j reads points j + 64 r, twiddles by
-  // W512^(r (j mod Ns) 64/Ns), runs dft8 and writes (j/Ns) Ns 8 + (j mod Ns) + r Ns
+    // lane j holds X[j + 64 r]: power of bins 0..256
+    float* pw = spow[w][q];
 #pragma unroll
-  for (int pass = 0; pass < 3; ++pass) {
-    const int Ns = pass == 0 ? 1 : pass == 1 ? 8 : 64;
-    if (pass > 0) {
-      const int jm = lane & (Ns - 1), step = jm * (64 / Ns);
-#pragma unroll
-      for (int r = 1; r < 8; ++r) {
-        const int k = r * step;                       // < 512
-        float2 tw = stw[k & 255];
-        if (k & 256) tw = make_float2(-tw.x, -tw.y);
-        v[r] = cmul(v[r], tw);
-      }
+    for (int r = 0; r < 5; ++r) {
+      const int k = lane + 64 * r;
+      if (k < NBIN) pw[k] = v[r].x * v[r].x + v[r].y * v[r].y;
     }
-    dft8(v);
-    if (pass < 2) {
-      const int base = (lane / Ns) * Ns * 8 + (lane & (Ns - 1));
-#pragma unroll
-      for (int r = 0; r < 8; ++r) buf[xpad(base + r * Ns)] = v[r];
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int r = 0; r < 8; ++r) v[r] = buf[xpad(lane + 64 * r)];
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-  // lane j holds X[j + 64 r]: power of bins 0..256
-  float* pw = spow[w];
-#pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const int k = lane + 64 * r;
-    if (k < NBIN) pw[k] = v[r].x * v[r].x + v[r].y * v[r].y;
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
-  float* out = work + ((int64_t)b * Fmax + f) * NMEL;
-  for (int m = lane; m < NMEL; m += 64) {
-    const int st = sm_start[m], ln = sm_len[m], of = sm_off[m];
+  float* out = work + ((int64_t)b * Fmax + g0) * NMEL;
+#pragma unroll
+  for (int q = 0; q < MEL_GROUP; ++q) {
+    const float* pw = spow[w][q] + stl;
     float acc = 0.f;
-    for (int i = 0; i < ln; ++i) acc += sm_w[of + i] * pw[st + i];
-    // the reference logs the float64 mel energies and rounds to float32 (np.log(...).astype(float32)).
-    // At the floor (silent frames) that exact constant matters: a clip's identical rows leave
-    // numpy's CMVN rounding residue in the output, so it is the float64 log rounded once; above
-    // it, fp32 logf (<= 1 ulp) is far inside the FFT's own fp32 rounding
-    out[m] = acc > MEL_FLOOR ? logf(acc) : LOG_MEL_FLOOR;
+#pragma unroll
+    for (int i = 0; i < LOW_TAPS; ++i) acc = __builtin_fmaf(wl[i], pw[i], acc);
+    if (g0 + q < F) out[q * NMEL + ml] = logmel(acc);
+  }
+  {
+    const int q = lane >> 4;
+    const float* pw = spow[w][q] + sth;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < HIGH_TAPS; ++i) acc = __builtin_fmaf(wh[i], pw[i], acc);
+    if (g0 + q < F) out[q * NMEL + mh] = logmel(acc);
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  }  // frames of this wave
+  __builtin_amdgcn_wave_barrier();   // the next group's power rows overwrite these
+  }  // groups of 4 frames
 }
 
 // per-clip CMVN statistics: stats[b][m] = mean, stats[b][NMEL + m] = sqrt(var + 1e-7)
@@ -277,6 +325,120 @@ __global__ __launch_bounds__(256) void fbank_norm_kernel(const int32_t* __restri
   }
 }
 
+// CMVN statistics and the normalise / stack / pad / mask step in one kernel, for a group of NB mel
+// bins of one clip per block (NB·B blocks instead of B): the group's log-mel columns are staged
+// whole into LDS, transposed (bin-major, so a chain reads 4 frames per ds_read_b128), the NB
+// statistics chains run exactly as fbank_stats_kernel's (frame-ordered float32 sums, IEEE
+// division and square root: numpy's rounding), and the block then writes its bins' columns of
+// every stacked row from LDS.  The block of bin group 0 also writes the mask.  Used when
+// NB · Fp · 4 B fits the 64 KB of LDS (NB = 16 up to 10 s clips, NB = 4 up to 40 s); longer
+// clips take fbank_stats_kernel + fbank_norm_kernel.
+constexpr int SN_NT = 256;
+template <int NB>
+__global__ __launch_bounds__(SN_NT) void fbank_stats_norm_kernel(const int32_t* __restrict__ lengths, int Fmax, int Fp,
+                                                                int Tmax, const float* __restrict__ work,
+                                                                float* __restrict__ stats, float pad_value,
+                                                                float* __restrict__ feats, int64_t* __restrict__ mask,
+                                                                int mask_mode) {
+  extern __shared__ float4 sn_lds4[];
+  float* col = reinterpret_cast<float*>(sn_lds4);   // [NB][Fp]
+  __shared__ float s_mean[NB], s_std[NB];
+  const int b = blockIdx.y, m0 = blockIdx.x * NB, tid = threadIdx.x;
+  const int len = lengths[b];
+  const int F = min(len >= FRAME ? 1 + (len - FRAME) / HOP : 0, Fmax);
+  const int Tb = (F + 1) / 2;
+  const float* x = work + (int64_t)b * Fmax * NMEL + m0;
+  // stage: lane (f, j) reads bin m0 + j of frame f (NB-float runs of a 320-B row), writes col[j][f]
+#pragma unroll 16
+  for (int e = tid; e < F * NB; e += SN_NT) {
+    const int f = e / NB, j = e % NB;
+    col[j * Fp + f] = x[(int64_t)f * NMEL + j];
+  }
+  __syncthreads();
+  if (tid < NB) {
+    // one chain per bin, frame by frame, 4 frames per ds_read_b128
+    const float* c = col + tid * Fp;
+    const float4* c4 = reinterpret_cast<const float4*>(c);
+    const int F4 = F & ~3;
+    float sum = 0.f;
+#pragma unroll 4
+    for (int f = 0; f < F4; f += 4) {
+      const float4 v = c4[f >> 2];
+      sum = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(sum, v.x), v.y), v.z), v.w);
+    }
+    for (int f = F4; f < F; ++f) sum = __fadd_rn(sum, c[f]);
+    const float mean = F > 0 ? __fdiv_rn(sum, (float)F) : 0.f;
+    float q = 0.f;
+    auto sq = [&](float a) {
+      const float d = __fsub_rn(a, mean);
+      q = __fadd_rn(q, __fmul_rn(d, d));
+    };
+#pragma unroll 4
+    for (int f = 0; f < F4; f += 4) {
+      const float4 v = c4[f >> 2];
+      sq(v.x);
+      sq(v.y);
+      sq(v.z);
+      sq(v.w);
+    }
+    for (int f = F4; f < F; ++f) sq(c[f]);
+    const float var = F > 1 ? __fdiv_rn(q, (float)(F - 1)) : 0.f;
+    const float sd = __fsqrt_rn(__fadd_rn(var, 1e-7f));
+    s_mean[tid] = mean;
+    s_std[tid] = sd;
+    stats[(int64_t)b * 2 * NMEL + m0 + tid] = mean;
+    stats[(int64_t)b * 2 * NMEL + NMEL + m0 + tid] = sd;
+  }
+  __syncthreads();
+  // stacked row t = [frame 2t | frame 2t + 1]: this block's columns m0 + j of both halves
+  float* o = feats + (int64_t)b * Tmax * (2 * NMEL) + m0;
+  const float fill = mask_mode == 0 ? 0.f : pad_value;
+  auto value = [&](int t, int h, int j) {
+    const int f = 2 * t + h;
+    // beyond the clip: collate zero-padding (mode 0) or the extractor's batch padding value (mode 1)
+    if (t >= Tb) return fill;
+    return f < F ? __fdiv_rn(__fsub_rn(col[j * Fp + f], s_mean[j]), s_std[j]) : pad_value;
+  };
+#pragma unroll 4
+  for (int e = tid; e < Tmax * 2 * NB; e += SN_NT) {
+    const int t = e / (2 * NB), r = e % (2 * NB), h = r / NB, j = r % NB;
+    o[(int64_t)t * (2 * NMEL) + h * NMEL + j] = value(t, h, j);
+  }
+  if (blockIdx.x == 0) {
+    for (int t = tid; t < Tmax; t += SN_NT) {
+      int64_t mv;
+      if (mask_mode == 0) mv = t < Tb ? 1 : 0;
+      else mv = (t < Tb && 2 * t + 1 < F) ? 1 : 0;
+      mask[(int64_t)b * Tmax + t] = mv;
+    }
+  }
+}
+
+template <int NB>
+void launch_stats_norm(int B, int Fmax, int Fp, int Tmax, const int32_t* lengths, const float* work, float* stats,
+                       float pad_value, float* feats, int64_t* mask, int mask_mode, hipStream_t s) {
+  hipLaunchKernelGGL(fbank_stats_norm_kernel<NB>, dim3(NMEL / NB, B), dim3(SN_NT), (size_t)NB * Fp * 4, s,
+                     lengths, Fmax, Fp, Tmax, work, stats, pad_value, feats, mask, mask_mode);
+}
+
+bool stats_norm(int B, int Fmax, int Tmax, const int32_t* lengths, const float* work, float* stats, float pad_value,
+                float* feats, int64_t* mask, int mask_mode, hipStream_t s) {
+  // the largest bin group whose columns fit 64 KB of LDS (with the static mean / std rows)
+  const int Fp = (Fmax + 3) & ~3;
+  const int64_t col_bytes = (int64_t)Fp * 4, lds = 65536 - 256;
+  if (16 * col_bytes <= lds)
+    launch_stats_norm<16>(B, Fmax, Fp, Tmax, lengths, work, stats, pad_value, feats, mask, mask_mode, s);
+  else if (8 * col_bytes <= lds)
+    launch_stats_norm<8>(B, Fmax, Fp, Tmax, lengths, work, stats, pad_value, feats, mask, mask_mode, s);
+  else if (4 * col_bytes <= lds)
+    launch_stats_norm<4>(B, Fmax, Fp, Tmax, lengths, work, stats, pad_value, feats, mask, mask_mode, s);
+  else if (2 * col_bytes <= lds)
+    launch_stats_norm<2>(B, Fmax, Fp, Tmax, lengths, work, stats, pad_value, feats, mask, mask_mode, s);
+  else
+    return false;
+  return true;
+}
+
 }  // namespace
 
 extern "C" int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* lengths, int B, int Tmax, float pad_value,
@@ -285,15 +447,28 @@ extern "C" int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* length
   const int Fmax = 2 * Tmax;
   hipStream_t s = (hipStream_t)stream;
   float* logmel = work;
-  const int fpb = 4 * FRAMES_PER_WAVE;
-  hipLaunchKernelGGL(fbank_logmel_kernel, dim3((Fmax + fpb - 1) / fpb, B), dim3(256), 0, s, wav, ld_wav, lengths,
-                     Fmax, logmel);
+  // A/B builds: STE_FBANK_FPW = 4 / 8 / 16 frames per wave
+  const char* ef = STE_AB_ENV("STE_FBANK_FPW");
+  const int fpw = ef ? atoi(ef) : FRAMES_PER_WAVE;
+  const unsigned gx = (unsigned)((Fmax + 4 * fpw - 1) / (4 * fpw));
+  if (fpw == 16)
+    hipLaunchKernelGGL(fbank_logmel_kernel<16>, dim3(gx, B), dim3(256), 0, s, wav, ld_wav, lengths, Fmax, logmel);
+  else if (fpw == 8)
+    hipLaunchKernelGGL(fbank_logmel_kernel<8>, dim3(gx, B), dim3(256), 0, s, wav, ld_wav, lengths, Fmax, logmel);
+  else
+    hipLaunchKernelGGL(fbank_logmel_kernel<4>, dim3(gx, B), dim3(256), 0, s, wav, ld_wav, lengths, Fmax, logmel);
   STE_CHECK_LAUNCH();
   float* stats = work + (int64_t)B * Fmax * NMEL;
-  hipLaunchKernelGGL(fbank_stats_kernel, dim3(B), dim3(STATS_NT), 0, s, lengths, Fmax, logmel, stats);
-  STE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(fbank_norm_kernel, dim3((Tmax + NORM_ROWS - 1) / NORM_ROWS, B), dim3(256), 0, s, lengths, Fmax,
-                     Tmax, logmel, stats, pad_value, feats, mask, mask_mode);
+  // fused statistics + normalise; A/B builds: STE_FBANK_SN=old takes the separate kernels
+  const char* e = STE_AB_ENV("STE_FBANK_SN");
+  const bool fused = !(e && e[0] == 'o') &&
+                     stats_norm(B, Fmax, Tmax, lengths, logmel, stats, pad_value, feats, mask, mask_mode, s);
+  if (!fused) {
+    hipLaunchKernelGGL(fbank_stats_kernel, dim3(B), dim3(STATS_NT), 0, s, lengths, Fmax, logmel, stats);
+    STE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(fbank_norm_kernel, dim3((Tmax + NORM_ROWS - 1) / NORM_ROWS, B), dim3(256), 0, s, lengths, Fmax,
+                       Tmax, logmel, stats, pad_value, feats, mask, mask_mode);
+  }
   STE_CHECK_LAUNCH();
   return 0;
 }

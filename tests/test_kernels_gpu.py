@@ -1130,6 +1130,31 @@ def test_fbank_config_size_clips_match_reference_extractor(ops):
         assert e <= FBANK_ATOL, (c, e)
 
 
+def test_fbank_bin_group_paths_agree(ops):
+    """The fused statistics + normalise kernel picks its bin group (16, 8, 4, 2 mel bins per block)
+    from the batch's frame capacity 2·Tmax, and past 2-bin columns of 64 KB falls back to the
+    separate statistics and normalise kernels.  A padded Tmax drives the same clips through every
+    path: identical features (bit for bit: the same frame-ordered sums and IEEE divisions), the
+    padding rows of each mask mode, and the masks."""
+    torch.manual_seed(3)
+    lens = [160000, 123457, 48000, 400, 399]   # 10 s, ragged, 3 s, one frame, no frame
+    N = max(lens)
+    wav = torch.randn(len(lens), N, device=DEV) * 0.1
+    for i, n in enumerate(lens):
+        wav[i, n:] = 0
+    lt = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    T0 = 499
+    for mode in (0, 1):
+        base, bmask = ops.fbank(wav, lt, T0, pad_value=1.0, mask_mode=mode)
+        # Tmax -> Fp = 2 Tmax: 16 bins (T0), 8 (1,500), 4 (3,000), 2 (6,000), fallback (17,000)
+        for T in (1500, 3000, 6000, 17000):
+            f, m = ops.fbank(wav, lt, T, pad_value=1.0, mask_mode=mode)
+            assert torch.equal(f[:, :T0], base), (mode, T)
+            assert torch.equal(m[:, :T0], bmask), (mode, T)
+            assert not m[:, T0:].any()
+            assert bool((f[:, T0:] == (0.0 if mode == 0 else 1.0)).all()), (mode, T)
+
+
 def test_feature_extractor_api():
     """Drop-in extractor (ref:856-866 call shape) per clip and batched vs the real extractor's output."""
     from conftest import GOLDEN
