@@ -290,34 +290,35 @@ STE_DEV void ln_flush(const ste_ln_bwd_args& a, const LnAcc<MAXC>& acc, float (*
   }
 }
 
-// out_k[col] += Σ_block ws[k][block][col] in a fixed order (16 interleaved slices of the blocks,
-// then the slices in order): grid (ceil(cols / 64), 3), 1024 threads, 8 loads in flight per thread
+// out_k[col] += Σ_block ws[k][block][col] in a fixed order (CS_SL interleaved slices of the
+// blocks, then the slices in order): 16 columns x 64 slices per block, grid (ceil(cols / 16), 3),
+// 1024 threads, 8 loads in flight per thread (3 x 64 blocks at 1,024 columns instead of 3 x 16)
+constexpr int CS_CW = 16, CS_SL = 1024 / CS_CW;
 __global__ __launch_bounds__(1024) void ln_colsum_kernel(const float* __restrict__ ws, int nblk, int cols,
                                                          float* dgamma, float* dbeta, float* dsum) {
   float* const out = blockIdx.y == 0 ? dgamma : (blockIdx.y == 1 ? dbeta : dsum);
   if (!out) return;  // uniform
-  __shared__ float red[16][64];
-  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + c;
+  __shared__ float red[CS_SL][CS_CW];
+  const int c = threadIdx.x % CS_CW, sl = threadIdx.x / CS_CW;
+  const int col = blockIdx.x * CS_CW + c;
   float acc = 0.f;
   if (col < cols) {
     const float* p = ws + (int64_t)blockIdx.y * nblk * cols + col;
     int b = sl;
-    for (; b + 7 * 16 < nblk; b += 8 * 16) {
+    for (; b + 7 * CS_SL < nblk; b += 8 * CS_SL) {
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(b + 16 * u) * cols];
+      for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(b + CS_SL * u) * cols];
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc += v[u];
     }
-    for (; b < nblk; b += 16) acc += p[(int64_t)b * cols];
+    for (; b < nblk; b += CS_SL) acc += p[(int64_t)b * cols];
   }
   red[sl][c] = acc;
   __syncthreads();
   if (sl == 0 && col < cols) {
     float t = red[0][c];
-#pragma unroll
-    for (int k = 1; k < 16; ++k) t += red[k][c];
+    for (int k = 1; k < CS_SL; ++k) t += red[k][c];
     out[col] += t;
   }
 }
@@ -394,7 +395,7 @@ inline bool ws_ok(const ste_ln_bwd_args& a, int nblk) {
 }
 inline void colsum(const ste_ln_bwd_args& a, int nblk, hipStream_t s) {
   if (!a.ws || !(a.dgamma || a.dbeta || a.dsum)) return;
-  hipLaunchKernelGGL(ln_colsum_kernel, dim3((unsigned)((a.cols + 63) / 64), 3), dim3(1024), 0, s, (const float*)a.ws,
+  hipLaunchKernelGGL(ln_colsum_kernel, dim3((unsigned)((a.cols + CS_CW - 1) / CS_CW), 3), dim3(1024), 0, s, (const float*)a.ws,
                      nblk, a.cols, a.dgamma, a.dbeta, a.dsum);
 }
 

@@ -81,34 +81,36 @@ __global__ void colsum_kernel(const void* x, int is_bf16, int64_t rows, int cols
     }
   }
 }
-// out[b·cols + c] += Σ_r part[(b·R + r)·cols + c] in a fixed order (16 interleaved slices of the
-// rows, then the slices in order): the ordered second pass of every deterministic column sum
-// (GEMM bias gradients, ste_colsum, depthwise-conv and SpecAugment gradients).  grid
-// (ceil(cols / 64), batch), 1024 threads, 8 loads in flight per thread
+// out[b·cols + c] += Σ_r part[(b·R + r)·cols + c] in a fixed order (RS_SL interleaved slices of
+// the rows, then the slices in order): the ordered second pass of every deterministic column sum
+// (GEMM bias gradients, ste_colsum, depthwise-conv and SpecAugment gradients).  A block owns
+// RS_CW columns (64-B row segments) and RS_SL = 64 row slices, so a 1,024-column sum spreads over
+// 64 blocks instead of 16 and each thread walks R / 64 rows, 8 loads in flight.
+// grid (ceil(cols / RS_CW), batch), 1024 threads
+constexpr int RS_CW = 16, RS_SL = 1024 / RS_CW;
 __global__ __launch_bounds__(1024) void rowsum_ordered_kernel(const float* __restrict__ part, int64_t R, int cols,
                                                               float* out) {
-  __shared__ float red[16][64];
-  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + c;
+  __shared__ float red[RS_SL][RS_CW];
+  const int c = threadIdx.x % RS_CW, sl = threadIdx.x / RS_CW;
+  const int col = blockIdx.x * RS_CW + c;
   float acc = 0.f;
   if (col < cols) {
     const float* p = part + (int64_t)blockIdx.y * R * cols + col;
     int64_t r = sl;
-    for (; r + 7 * 16 < R; r += 8 * 16) {
+    for (; r + 7 * RS_SL < R; r += 8 * RS_SL) {
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = p[(r + 16 * u) * cols];
+      for (int u = 0; u < 8; ++u) v[u] = p[(r + RS_SL * u) * cols];
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc += v[u];
     }
-    for (; r < R; r += 16) acc += p[r * cols];
+    for (; r < R; r += RS_SL) acc += p[r * cols];
   }
   red[sl][c] = acc;
   __syncthreads();
   if (sl == 0 && col < cols) {
     float t = red[0][c];
-#pragma unroll
-    for (int k = 1; k < 16; ++k) t += red[k][c];
+    for (int k = 1; k < RS_SL; ++k) t += red[k][c];
     out[(int64_t)blockIdx.y * cols + col] += t;
   }
 }
@@ -234,7 +236,7 @@ extern "C" int ste_spec_mask_bwd(float* dx, int64_t ld, const int32_t* spec, con
 extern "C" int ste_rowsum_ordered(const float* part, int64_t rows, int cols, int batch, float* out, void* stream) {
   if (rows <= 0 || cols <= 0 || batch <= 0) return 0;
   if (!part || !out) return STE_ERR_ARG;
-  hipLaunchKernelGGL(rowsum_ordered_kernel, dim3((cols + 63) / 64, batch), dim3(1024), 0, (hipStream_t)stream, part,
+  hipLaunchKernelGGL(rowsum_ordered_kernel, dim3((cols + RS_CW - 1) / RS_CW, batch), dim3(1024), 0, (hipStream_t)stream, part,
                      rows, cols, out);
   STE_CHECK_LAUNCH();
   return 0;
