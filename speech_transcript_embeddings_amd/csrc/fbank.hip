@@ -4,11 +4,11 @@
 // feature_extraction_seamless_m4t.py:112-138,240-301, tf:audio_utils.py:809-1017),
 // plus the collate padding of ref:training/trainer_unfreeze.py:880-921.
 //
-// Kernel 1 (one wavefront per 400-sample frame at a time, 4 waves per block, 4 frames per wave):
+// Kernel 1 (one wavefront per 400-sample frame, 4 waves per block, 4 frames per wave):
 //   x*2^15 -> remove frame mean -> pre-emphasis 0.97 (y0 *= 0.03) -> povey window
 //   -> 512-point radix-8 Stockham FFT in registers (fp32, twiddles from double sincos) -> |X|^2
-//   -> 80 kaldi-scale triangular mel filters built in mel space (sparse, taps in registers)
-//   -> max(1.1920929e-7, .) -> natural log.
+//   -> 80 kaldi-scale triangular mel filters built in mel space (sparse, per-block
+//   table) -> max(1.1920929e-7, .) -> natural log.
 // Kernel 2 (one block per clip and group of NB mel bins, the group's columns staged into LDS):
 // per-mel-bin mean and unbiased variance over the clip's frames exactly as numpy evaluates them
 // on the extractor's float32 log-mel array (tf:…seamless_m4t…:256-261: x.mean(0), x.var(0, ddof=1),
@@ -41,7 +41,7 @@ constexpr int T_TW = 0, T_WIN = 512, T_MSTART = 912, T_MLEN = 992, T_MOFF = 1072
 #include "fbank_tables.h"
 namespace {
 
-constexpr int FRAMES_PER_WAVE = 4, MEL_GROUP = 4;   // frames per wave (default; 8 / 16 in A/B builds), per mel stage
+constexpr int FRAMES_PER_WAVE = 4;
 constexpr int XPAD = NFFT + NFFT / 8;   // exchange buffer: one float2 of padding per 8
 
 STE_DEV int xpad(int i) { return i + (i >> 3); }
@@ -76,166 +76,120 @@ STE_DEV void dft8(float2 (&v)[8]) {
 // per-wave LDS buffer, twiddles e^{-2πik/512} from the fp64-built table; the input needs no
 // bit reversal and lane j ends with X[j + 64 r].  (The radix-2 version took 9 LDS round trips
 // per frame and half of the kernel's time.)
-// Everything a lane needs for every frame is loaded once per wave into registers: its 7 window
-// values, its 14 pass-2/3 twiddles and the taps of its mel filters.  The next frame's samples are
-// loaded before the current frame's FFT runs.  The wave's 4 frames leave their power spectra in
-// LDS, and then the mel stage runs for all 4 at once: lane l sums low mel l (≤ 10 taps) for each
-// of the 4 frames, and high mel 64 + (l & 15) (≤ 16 taps) for frame l >> 4.  The taps are
-// unrolled to fixed counts, zero-weighted past a filter's length, so a lane's LDS reads issue
-// together instead of one round trip per tap.  Each filter still sums its taps in order, with
-// one fma per tap.
-constexpr int LOW_TAPS = 10, HIGH_TAPS = 16;   // max taps of mels 0..63 / 64..79 (fbank_tables.h)
-
-template <int FPW>
 __global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restrict__ wav, int64_t ld_wav,
                                                          const int32_t* __restrict__ lengths, int Fmax,
                                                          float* __restrict__ work) {
   const float* tab = reinterpret_cast<const float*>(g_fbank_tab_bits);
-  const int* tabi = reinterpret_cast<const int*>(g_fbank_tab_bits);
   __shared__ float2 sbuf[4][XPAD];
-  __shared__ float spow[4][MEL_GROUP][NBIN + 3];
+  __shared__ float2 stw[NFFT / 2];
+  __shared__ float swin[FRAME];
+  __shared__ int sm_start[NMEL], sm_len[NMEL], sm_off[NMEL];
+  __shared__ float sm_w[MAXNZ];
+  __shared__ float spow[4][NBIN + 3];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int b = blockIdx.y;
-  const int len = lengths[b];
-  const int F = min(len >= FRAME ? 1 + (len - FRAME) / HOP : 0, Fmax);
-  const int f0 = (blockIdx.x * 4 + w) * FPW;
-  if (f0 >= F) return;  // whole wave exits; this kernel has no block barrier
+  for (int k = tid; k < NFFT / 2; k += 256) stw[k] = make_float2(tab[T_TW + 2 * k], tab[T_TW + 2 * k + 1]);
+  for (int n = tid; n < FRAME; n += 256) swin[n] = tab[T_WIN + n];
+  if (tid < NMEL) {
+    const int* ti = reinterpret_cast<const int*>(tab);
+    sm_start[tid] = ti[T_MSTART + tid];
+    sm_len[tid] = ti[T_MLEN + tid];
+    sm_off[tid] = ti[T_MOFF + tid];
+  }
+  for (int i = tid; i < MAXNZ; i += 256) sm_w[i] = tab[T_MW + i];
+  __syncthreads();
 
-  float win[7];
+  const int len = lengths[b];
+  const int F = len >= FRAME ? 1 + (len - FRAME) / HOP : 0;
+  float2* buf = sbuf[w];
+  for (int fi = 0; fi < FRAMES_PER_WAVE; ++fi) {
+  const int f = (blockIdx.x * 4 + w) * FRAMES_PER_WAVE + fi;
+  if (f >= F || f >= Fmax) return;  // whole wave exits; no block barrier follows
+  const float* x = wav + (int64_t)b * ld_wav + (int64_t)f * HOP;
+  float c[7];
+  float s = 0.f;
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     const int n = lane + 64 * i;
-    win[i] = n < FRAME ? tab[T_WIN + n] : 0.f;
+    c[i] = n < FRAME ? x[n] * 32768.0f : 0.f;
+    s += c[i];
   }
-  // twiddles of passes 2 and 3 (Ns = 8, 64): W512^(r (j mod Ns) 64 / Ns), r = 1..7
-  float2 tw[2][7];
+  const float mean = wave_sum(s) * (1.0f / FRAME);
 #pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int step = p == 0 ? (lane & 7) * 8 : lane;
+  for (int i = 0; i < 7; ++i) c[i] = c[i] - mean;   // n >= FRAME: masked below
+  // pre-emphasis (x[n] - 0.97 x[n-1], x[0] * 0.03) and window: x[n-1] is lane-1's value, or
+  // lane 63's of the previous row for lane 0
+  float2 v[8];
 #pragma unroll
-    for (int r = 1; r < 8; ++r) {
-      const int k = r * step;   // < 512
-      float2 t = make_float2(tab[T_TW + 2 * (k & 255)], tab[T_TW + 2 * (k & 255) + 1]);
-      if (k & 256) t = make_float2(-t.x, -t.y);
-      tw[p][r - 1] = t;
-    }
-  }
-  // mel taps: low mel `lane`, high mel 64 + (lane & 15)
-  const int ml = lane, mh = 64 + (lane & 15);
-  const int stl = tabi[T_MSTART + ml], sth = tabi[T_MSTART + mh];
-  float wl[LOW_TAPS], wh[HIGH_TAPS];
-  {
-    const int lnl = tabi[T_MLEN + ml], ofl = tabi[T_MOFF + ml];
-    const int lnh = tabi[T_MLEN + mh], ofh = tabi[T_MOFF + mh];
-#pragma unroll
-    for (int i = 0; i < LOW_TAPS; ++i) wl[i] = i < lnl ? tab[T_MW + ofl + i] : 0.f;
-#pragma unroll
-    for (int i = 0; i < HIGH_TAPS; ++i) wh[i] = i < lnh ? tab[T_MW + ofh + i] : 0.f;
-  }
-
-  float2* buf = sbuf[w];
-  const float* xb = wav + (int64_t)b * ld_wav;
-  float c[7];
-  auto load = [&](int f) {
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int n = lane + 64 * i;
-      c[i] = (f < F && n < FRAME) ? xb[(int64_t)f * HOP + n] : 0.f;
-    }
-  };
-  // the reference logs the float64 mel energies and rounds to float32 (np.log(...).astype(float32)).
-  // At the floor (silent frames) that exact constant matters: a clip's identical rows leave
-  // numpy's CMVN rounding residue in the output, so it is the float64 log rounded once; above
-  // it, fp32 logf (<= 1 ulp) is far inside the FFT's own fp32 rounding
-  auto logmel = [](float e) { return e > MEL_FLOOR ? logf(e) : LOG_MEL_FLOOR; };
-  load(f0);
-  for (int g0 = f0; g0 < min(f0 + FPW, F); g0 += MEL_GROUP) {
-#pragma unroll
-  for (int q = 0; q < MEL_GROUP; ++q) {
-    float x[7];
-#pragma unroll
-    for (int i = 0; i < 7; ++i) x[i] = c[i] * 32768.0f;
-    load(g0 + q + 1);   // in flight under this frame's FFT (zeros past the clip: no read)
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) s += x[i];
-    const float mean = wave_sum(s) * (1.0f / FRAME);
-#pragma unroll
-    for (int i = 0; i < 7; ++i) x[i] = x[i] - mean;   // n >= FRAME: masked below
-    // pre-emphasis (x[n] - 0.97 x[n-1], x[0] * 0.03) and window: x[n-1] is lane-1's value, or
-    // lane 63's of the previous row for lane 0
-    float2 v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int n = lane + 64 * i;
-      float val = 0.f;
-      if (i < 7) {
-        // lane - 1's value by DPP wave_shr:1 and lane 63's by v_readlane (no ds_bpermute round trips)
-        const float up = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x[i]), 0x138,
-                                                                                 0xF, 0xF, false));
-        const float wrap =
-            i > 0 ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x[i - 1]), 63)) : 0.f;
-        const float prev = lane > 0 ? up : wrap;
-        if (n < FRAME) {
-          val = (n == 0) ? x[i] * (1.0f - 0.97f) : x[i] - 0.97f * prev;
-          val *= win[i];
-        }
-      }
-      v[i] = make_float2(val, 0.f);
-    }
-    // Stockham radix-8: pass Ns in {1, 8, 64}; lane j reads points j + 64 r, twiddles by
-    // W512^(r (j mod Ns) 64/Ns), runs dft8 and writes (j/Ns) Ns 8 + (j mod Ns) + r Ns
-#pragma unroll
-    for (int pass = 0; pass < 3; ++pass) {
-      const int Ns = pass == 0 ? 1 : pass == 1 ? 8 : 64;
-      if (pass > 0) {
-#pragma unroll
-        for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tw[pass - 1][r - 1]);
-      }
-      dft8(v);
-      if (pass < 2) {
-        const int base = (lane / Ns) * Ns * 8 + (lane & (Ns - 1));
-#pragma unroll
-        for (int r = 0; r < 8; ++r) buf[xpad(base + r * Ns)] = v[r];
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = buf[xpad(lane + 64 * r)];
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
+  for (int i = 0; i < 8; ++i) {
+    const int n = lane + 64 * i;
+    float val = 0.f;
+    if (i < 7) {
+      // lane - 1's value by DPP wave_shr:1 and lane 63's by v_readlane (no ds_bpermute round trips)
+      const float up = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, c[i]), 0x138,
+                                                                               0xF, 0xF, false));
+      const float wrap = i > 0 ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, c[i - 1]), 63))
+                               : 0.f;
+      const float prev = lane > 0 ? up : wrap;
+      if (n < FRAME) {
+        val = (n == 0) ? c[i] * (1.0f - 0.97f) : c[i] - 0.97f * prev;
+        val *= swin[n];
       }
     }
-    // lane j holds X[j + 64 r]: power of bins 0..256
-    float* pw = spow[w][q];
+    v[i] = make_float2(val, 0.f);
+  }
+  // Stockham radix-8: pass Ns in {1, 8, 64}; lane j reads points j + 64 r, twiddles by
+  // W512^(r (j mod Ns) 64/Ns), runs dft8 and writes (j/Ns) Ns 8 + (j mod Ns) + r Ns
 #pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const int k = lane + 64 * r;
-      if (k < NBIN) pw[k] = v[r].x * v[r].x + v[r].y * v[r].y;
+  for (int pass = 0; pass < 3; ++pass) {
+    const int Ns = pass == 0 ? 1 : pass == 1 ? 8 : 64;
+    if (pass > 0) {
+      const int jm = lane & (Ns - 1), step = jm * (64 / Ns);
+#pragma unroll
+      for (int r = 1; r < 8; ++r) {
+        const int k = r * step;                       // < 512
+        float2 tw = stw[k & 255];
+        if (k & 256) tw = make_float2(-tw.x, -tw.y);
+        v[r] = cmul(v[r], tw);
+      }
     }
+    dft8(v);
+    if (pass < 2) {
+      const int base = (lane / Ns) * Ns * 8 + (lane & (Ns - 1));
+#pragma unroll
+      for (int r = 0; r < 8; ++r) buf[xpad(base + r * Ns)] = v[r];
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = buf[xpad(lane + 64 * r)];
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  // lane j holds X[j + 64 r]: power of bins 0..256
+  float* pw = spow[w];
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int k = lane + 64 * r;
+    if (k < NBIN) pw[k] = v[r].x * v[r].x + v[r].y * v[r].y;
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
-  float* out = work + ((int64_t)b * Fmax + g0) * NMEL;
-#pragma unroll
-  for (int q = 0; q < MEL_GROUP; ++q) {
-    const float* pw = spow[w][q] + stl;
+  float* out = work + ((int64_t)b * Fmax + f) * NMEL;
+  for (int m = lane; m < NMEL; m += 64) {
+    const int st = sm_start[m], ln = sm_len[m], of = sm_off[m];
     float acc = 0.f;
-#pragma unroll
-    for (int i = 0; i < LOW_TAPS; ++i) acc = __builtin_fmaf(wl[i], pw[i], acc);
-    if (g0 + q < F) out[q * NMEL + ml] = logmel(acc);
-  }
-  {
-    const int q = lane >> 4;
-    const float* pw = spow[w][q] + sth;
-    float acc = 0.f;
-#pragma unroll
-    for (int i = 0; i < HIGH_TAPS; ++i) acc = __builtin_fmaf(wh[i], pw[i], acc);
-    if (g0 + q < F) out[q * NMEL + mh] = logmel(acc);
+    for (int i = 0; i < ln; ++i) acc += sm_w[of + i] * pw[st + i];
+    // the reference logs the float64 mel energies and rounds to float32 (np.log(...).astype(float32)).
+    // At the floor (silent frames) that exact constant matters: a clip's identical rows leave
+    // numpy's CMVN rounding residue in the output, so it is the float64 log rounded once; above
+    // it, fp32 logf (<= 1 ulp) is far inside the FFT's own fp32 rounding
+    out[m] = acc > MEL_FLOOR ? logf(acc) : LOG_MEL_FLOOR;
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();   // the next group's power rows overwrite these
-  }  // groups of 4 frames
+  __builtin_amdgcn_wave_barrier();
+  }  // frames of this wave
 }
 
 // per-clip CMVN statistics: stats[b][m] = mean, stats[b][NMEL + m] = sqrt(var + 1e-7)
@@ -447,16 +401,9 @@ extern "C" int ste_fbank(const float* wav, int64_t ld_wav, const int32_t* length
   const int Fmax = 2 * Tmax;
   hipStream_t s = (hipStream_t)stream;
   float* logmel = work;
-  // A/B builds: STE_FBANK_FPW = 4 / 8 / 16 frames per wave
-  const char* ef = STE_AB_ENV("STE_FBANK_FPW");
-  const int fpw = ef ? atoi(ef) : FRAMES_PER_WAVE;
-  const unsigned gx = (unsigned)((Fmax + 4 * fpw - 1) / (4 * fpw));
-  if (fpw == 16)
-    hipLaunchKernelGGL(fbank_logmel_kernel<16>, dim3(gx, B), dim3(256), 0, s, wav, ld_wav, lengths, Fmax, logmel);
-  else if (fpw == 8)
-    hipLaunchKernelGGL(fbank_logmel_kernel<8>, dim3(gx, B), dim3(256), 0, s, wav, ld_wav, lengths, Fmax, logmel);
-  else
-    hipLaunchKernelGGL(fbank_logmel_kernel<4>, dim3(gx, B), dim3(256), 0, s, wav, ld_wav, lengths, Fmax, logmel);
+  const int fpb = 4 * FRAMES_PER_WAVE;
+  hipLaunchKernelGGL(fbank_logmel_kernel, dim3((Fmax + fpb - 1) / fpb, B), dim3(256), 0, s, wav, ld_wav, lengths,
+                     Fmax, logmel);
   STE_CHECK_LAUNCH();
   float* stats = work + (int64_t)B * Fmax * NMEL;
   // fused statistics + normalise; A/B builds: STE_FBANK_SN=old takes the separate kernels
