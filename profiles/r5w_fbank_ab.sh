@@ -1,5 +1,5 @@
 #!/bin/bash
-# fbank variants (libste_ab.so): frames per wave of the log-mel kernel (STE_FBANK_FPW); round 5 also
+# fbank variants (libste_ab.so): frames per wave of a log-mel rewrite (STE_FBANK_FPW, since reverted); round 5 also
 # ran STE_FBANK_SN = old / fused statistics variants the same way (profiles/r5w_fbank_ab.txt)
 set -e
 mkdir -p gpurun_out

@@ -1260,7 +1260,6 @@ constexpr int DQ3_T_OFF = MASK_OFF + 512;
 constexpr int DQ3_LDS = DQ3_T_OFF + 4 * DQ3_WQ * GT3 * 4;
 }  // namespace rel2
 
-template <bool GFIX>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a) {
   using namespace rel2;
   extern __shared__ __attribute__((aligned(16))) char sm[];
@@ -1371,8 +1370,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
 #pragma unroll
     for (int i = 0; i < 4; ++i) dq[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float glo[2] = {0.f, 0.f}, ghi[2] = {0.f, 0.f};
-  // GFIX: the row's Σ dS, Σ P and the edge bins' Σ P (see the G-row finish)
-  float sall[2] = {0.f, 0.f}, pall[2] = {0.f, 0.f}, plo[2] = {0.f, 0.f}, phi[2] = {0.f, 0.f};
 
   for (int kt = 0; kt < nkt; ++kt) {
     const char* tK = sm + (kt & 1) * KV;
@@ -1445,31 +1442,15 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
             sc[gq][t][r] = ((okp >> bit) & 1u) ? sc[gq][t][r] : fill;
           }
       }
-      float bsum = 0.f, psum = 0.f;
+      float bsum = 0.f;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = sc[gq][t][r];
-          const float ds = p * (dp[gq][t][r] - dl[gq]);
+          const float ds = sc[gq][t][r] * (dp[gq][t][r] - dl[gq]);
           sc[gq][t][r] = ds;
           bsum += ds;
-          if constexpr (GFIX) {
-            psum += p;
-            if (band) {
-              const int d = kb + 16 * t + 4 * g + r - myq;
-              plo[gq] += d <= -left ? p : 0.f;
-              phi[gq] += d >= right ? p : 0.f;
-            }
-          }
         }
-      if constexpr (GFIX) {
-        sall[gq] += bsum;
-        pall[gq] += psum;
-        if (!band) {
-          if (all_lo) plo[gq] += psum; else phi[gq] += psum;
-        }
-      }
       if (!band) {
         if (all_lo) glo[gq] += bsum; else ghi[gq] += bsum;
       } else {
@@ -1513,19 +1494,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_rel3_kernel(ste_attn_args a
   for (int gq = 0; gq < 2; ++gq) {
     glo[gq] = rowsum4(glo[gq]);
     ghi[gq] = rowsum4(ghi[gq]);
-    if constexpr (GFIX) {
-      // Σ_j dS_ij is 0 for the exact delta = Σ_j P_ij dP_ij; delta from dO·O leaves the row a
-      // residue Σ dS that the clamped bins (most of a long row's keys) collect almost whole.
-      // Re-based on the row-consistent delta (δ' = δ + Σ dS / Σ P), each clamped bin drops its
-      // share Σ dS · Σ_bin P / Σ P.
-      const float sa = rowsum4(sall[gq]), pa = rowsum4(pall[gq]);
-      const float pl = rowsum4(plo[gq]), ph = rowsum4(phi[gq]);
-      if (pa > 0.f) {
-        const float r = sa / pa;
-        glo[gq] -= r * pl;
-        ghi[gq] -= r * ph;
-      }
-    }
     const int myq = qw + 16 * gq + li;
     float* row = tb + (16 * gq + li) * GT3;
     for (int j = 1 + g; j < nrel - 1; j += 4) {
@@ -1992,11 +1960,6 @@ bool rel_fwd_plo() {
   static const bool v = !ab_is("STE_ATTN_PLO", '0');
   return v;
 }
-// STE_ATTN_GFIX=1: the dQ kernel re-bases its clamped distance bins on the row-consistent delta
-bool rel_gfix() {
-  static const bool v = ab_is("STE_ATTN_GFIX", '1');
-  return v;
-}
 
 int check(const ste_attn_args* a) {
   if (!a || a->B <= 0 || a->T <= 0 || a->H <= 0) return STE_ERR_ARG;
@@ -2060,8 +2023,7 @@ extern "C" int ste_attention_bwd(const ste_attn_args* a, void* stream) {
   if (a->rel_E && a->drop_p == 0.f) {
     static_assert(NREL < rel2::GT3, "bin GT3-1 is the dQ kernel's spare slot");
     dim3 gq((unsigned)(((a->T + rel2::DQ3_Q - 1) / rel2::DQ3_Q) * a->H * a->B));
-    if (rel_gfix()) hipLaunchKernelGGL(attn_bwd_dq_rel3_kernel<true>, gq, dim3(NT), rel2::DQ3_LDS, s, *a);
-    else hipLaunchKernelGGL(attn_bwd_dq_rel3_kernel<false>, gq, dim3(NT), rel2::DQ3_LDS, s, *a);
+    hipLaunchKernelGGL(attn_bwd_dq_rel3_kernel, gq, dim3(NT), rel2::DQ3_LDS, s, *a);
     STE_CHECK_LAUNCH();
     dim3 gk((unsigned)(((a->T + rel2::KB - 1) / rel2::KB) * a->H * a->B));
     hipLaunchKernelGGL(attn_bwd_dkv_rel3_kernel, gk, dim3(NT), rel2::DKV3_LDS, s, *a);
