@@ -98,6 +98,9 @@ __global__ __launch_bounds__(NT) void glu_dwconv_bwd_kernel(const bf16* __restri
   constexpr int ROWS = TT + K - 1;
   __shared__ float lds[(DW ? 2 : 1) * ROWS * CC];
   __shared__ float sw[CC * K];
+  // DW: the tile's own rows of pre (a | gate, bf16) kept from the staging pass for the GLU
+  // backward, which otherwise re-reads them from HBM (72 KB in all: still 2 blocks per CU)
+  __shared__ bf16x8 sag[DW ? TT * (CC / 8) * 2 : 1];
   float (*sd)[CC] = reinterpret_cast<float (*)[CC]>(lds);              // dout rows t0 .. t0+TT+K-2
   float (*sg)[CC] = reinterpret_cast<float (*)[CC]>(lds + ROWS * CC);  // g rows t0-(K-1) .. t0+TT-1 (DW only)
   const int b = blockIdx.z, c0 = blockIdx.y * CC;
@@ -130,6 +133,11 @@ __global__ __launch_bounds__(NT) void glu_dwconv_bwd_kernel(const bf16* __restri
     if (DW) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) sg[r][c8 + e] = (tg >= 0 && tg < T) ? (float)av[e] * sigmoidf_((float)gv[e]) : 0.f;
+      if (r >= K - 1) {   // row t0 + (r - (K-1)) of this tile
+        const int q = (r - (K - 1)) * (CC / 8) + c8 / 8;
+        sag[2 * q] = av;
+        sag[2 * q + 1] = gv;
+      }
     }
   }
   __syncthreads();
@@ -169,8 +177,14 @@ __global__ __launch_bounds__(NT) void glu_dwconv_bwd_kernel(const bf16* __restri
     const int t = t0 + r;
     if (t >= T) continue;
     const int64_t row = (int64_t)(b * T + t);
-    const bf16x8 av = *reinterpret_cast<const bf16x8*>(pre + row * 2 * C + c0 + c8);
-    const bf16x8 gv = *reinterpret_cast<const bf16x8*>(pre + row * 2 * C + C + c0 + c8);
+    bf16x8 av, gv;
+    if constexpr (DW) {
+      av = sag[2 * i];   // i = r * (CC / 8) + c8 / 8: the staged row r, channels c8..c8+7
+      gv = sag[2 * i + 1];
+    } else {
+      av = *reinterpret_cast<const bf16x8*>(pre + row * 2 * C + c0 + c8);
+      gv = *reinterpret_cast<const bf16x8*>(pre + row * 2 * C + C + c0 + c8);
+    }
     bf16x8 da, dgate;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
