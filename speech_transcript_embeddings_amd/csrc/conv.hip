@@ -113,24 +113,38 @@ __global__ __launch_bounds__(NT) void glu_dwconv_bwd_kernel(const bf16* __restri
   // DW: a block walks several 64-row tiles (grid.x < tiles) and keeps its dW partials in
   // registers across them, so each (channel, tap) address takes one atomic per block, not per tile
   const int ntile = (T + TT - 1) / TT;
+  // DW (a block walks several tiles): the tile's staging loads (16 B of 8 channels per item) live
+  // in registers, and the next tile's are issued right after this tile's reach LDS, so their
+  // latency hides under this tile's compute.  Frozen layers (one tile per block) stage directly:
+  // the registers would cost them occupancy for nothing.
+  constexpr int ITEMS = ROWS * (CC / 8), PER = DW ? (ITEMS + NT - 1) / NT : 1;
+  bf16x8 rdv[PER], rav[PER], rgv[PER];
+  auto fetch = [&](int t0) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int i = tid + u * NT, r = i / (CC / 8), c8 = (i % (CC / 8)) * 8;
+      const int td = t0 + r, tg = t0 - (K - 1) + r;
+      rdv[u] = (i < ITEMS && td < T) ? *reinterpret_cast<const bf16x8*>(dout + (int64_t)(b * T + td) * C + c0 + c8)
+                                     : bf16x8{};
+      const bool ok = i < ITEMS && tg >= 0 && tg < T;
+      const bf16* p = pre + (int64_t)(b * T + (ok ? tg : 0)) * (2 * C) + c0 + c8;
+      rav[u] = ok ? *reinterpret_cast<const bf16x8*>(p) : bf16x8{};
+      rgv[u] = ok ? *reinterpret_cast<const bf16x8*>(p + C) : bf16x8{};
+    }
+  };
+  if (DW && (int)blockIdx.x < ntile) fetch(blockIdx.x * TT);
   for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
   const int t0 = tile * TT;
   __syncthreads();   // sw staged / the previous tile's LDS reads done
-  for (int i = tid; i < ROWS * (CC / 8); i += NT) {  // 16-B loads of 8 channels
-    const int r = i / (CC / 8), c8 = (i % (CC / 8)) * 8;
-    const int td = t0 + r;
-    bf16x8 dv = bf16x8{};
-    if (td < T) dv = *reinterpret_cast<const bf16x8*>(dout + (int64_t)(b * T + td) * C + c0 + c8);
-    bf16x8 av = bf16x8{}, gv = bf16x8{};
-    const int tg = t0 - (K - 1) + r;
-    if (DW && tg >= 0 && tg < T) {
-      const bf16* p = pre + (int64_t)(b * T + tg) * (2 * C) + c0 + c8;
-      av = *reinterpret_cast<const bf16x8*>(p);
-      gv = *reinterpret_cast<const bf16x8*>(p + C);
-    }
+  if constexpr (DW) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) sd[r][c8 + e] = (float)dv[e];
-    if (DW) {
+    for (int u = 0; u < PER; ++u) {
+      const int i = tid + u * NT, r = i / (CC / 8), c8 = (i % (CC / 8)) * 8;
+      if (i >= ITEMS) continue;
+      const int tg = t0 - (K - 1) + r;
+      const bf16x8 dv = rdv[u], av = rav[u], gv = rgv[u];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sd[r][c8 + e] = (float)dv[e];
 #pragma unroll
       for (int e = 0; e < 8; ++e) sg[r][c8 + e] = (tg >= 0 && tg < T) ? (float)av[e] * sigmoidf_((float)gv[e]) : 0.f;
       if (r >= K - 1) {   // row t0 + (r - (K-1)) of this tile
@@ -138,6 +152,16 @@ __global__ __launch_bounds__(NT) void glu_dwconv_bwd_kernel(const bf16* __restri
         sag[2 * q] = av;
         sag[2 * q + 1] = gv;
       }
+    }
+    if (tile + (int)gridDim.x < ntile) fetch((tile + gridDim.x) * TT);
+  } else {
+    for (int i = tid; i < ITEMS; i += NT) {  // 16-B loads of 8 channels
+      const int r = i / (CC / 8), c8 = (i % (CC / 8)) * 8;
+      const int td = t0 + r;
+      bf16x8 dv = bf16x8{};
+      if (td < T) dv = *reinterpret_cast<const bf16x8*>(dout + (int64_t)(b * T + td) * C + c0 + c8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sd[r][c8 + e] = (float)dv[e];
     }
   }
   __syncthreads();
