@@ -134,6 +134,7 @@ __device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v
   p = __builtin_fmaf(-step, m / den, p * decay);
 }
 
+template <bool NTL>
 __global__ __launch_bounds__(NT) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                  float* __restrict__ m, float* __restrict__ v, bf16* __restrict__ pb,
                                                  int64_t n, float lr, float b1, float b2, float eps, float wd,
@@ -155,23 +156,32 @@ __global__ __launch_bounds__(NT) void adamw_kernel(float* __restrict__ p, const 
       vv[e] = ve;
     }
   };
+  // NTL: non-temporal (streaming) loads and stores of the four fp32 arrays
+  auto ld = [](const float* q) -> f32x4 {
+    if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(q));
+    else return *reinterpret_cast<const f32x4*>(q);
+  };
+  auto st = [](float* q, f32x4 x) {
+    if constexpr (NTL) __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(q));
+    else *reinterpret_cast<f32x4*>(q) = x;
+  };
   // bulk: two 4-element groups a grid-stride apart per iteration, all eight 16-B loads issued before
   // the arithmetic (more bytes in flight per lane than the one-group loop)
   const int64_t stride = (int64_t)gridDim.x * NT * 4;
   int64_t i = ((int64_t)blockIdx.x * NT + threadIdx.x) * 4;
   for (; i + stride + 3 < n; i += 2 * stride) {
-    f32x4 pv0 = *reinterpret_cast<const f32x4*>(p + i), pv1 = *reinterpret_cast<const f32x4*>(p + i + stride);
-    const f32x4 gv0 = *reinterpret_cast<const f32x4*>(g + i), gv1 = *reinterpret_cast<const f32x4*>(g + i + stride);
-    f32x4 mv0 = *reinterpret_cast<const f32x4*>(m + i), mv1 = *reinterpret_cast<const f32x4*>(m + i + stride);
-    f32x4 vv0 = *reinterpret_cast<const f32x4*>(v + i), vv1 = *reinterpret_cast<const f32x4*>(v + i + stride);
+    f32x4 pv0 = ld(p + i), pv1 = ld(p + i + stride);
+    const f32x4 gv0 = ld(g + i), gv1 = ld(g + i + stride);
+    f32x4 mv0 = ld(m + i), mv1 = ld(m + i + stride);
+    f32x4 vv0 = ld(v + i), vv1 = ld(v + i + stride);
     upd4(pv0, gv0, mv0, vv0);
     upd4(pv1, gv1, mv1, vv1);
-    *reinterpret_cast<f32x4*>(p + i) = pv0;
-    *reinterpret_cast<f32x4*>(m + i) = mv0;
-    *reinterpret_cast<f32x4*>(v + i) = vv0;
-    *reinterpret_cast<f32x4*>(p + i + stride) = pv1;
-    *reinterpret_cast<f32x4*>(m + i + stride) = mv1;
-    *reinterpret_cast<f32x4*>(v + i + stride) = vv1;
+    st(p + i, pv0);
+    st(m + i, mv0);
+    st(v + i, vv0);
+    st(p + i + stride, pv1);
+    st(m + i + stride, mv1);
+    st(v + i + stride, vv1);
     if (pb) {
       store_bf16x4(pb + i, pv0);
       store_bf16x4(pb + i + stride, pv1);
@@ -347,7 +357,15 @@ extern "C" int ste_adamw(float* p, const float* g, float* m, float* v, void* p_b
   if (p_bf16 && (((uintptr_t)p_bf16) & 7)) return STE_ERR_ARG;
   const float bc1 = 1.f - powf(beta1, (float)step);
   const float bc2s = sqrtf(1.f - powf(beta2, (float)step));
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, p, g, m, v, (bf16*)p_bf16, n,
+  // the fp32 arrays stream through with non-temporal loads / stores (nothing re-reads them before
+  // the next step; -3 % per launch, bitwise identical, profiles/r5a_adamw_nt.txt); A/B builds:
+  // STE_ADAMW_NT=0 for plain accesses
+  const char* ent = STE_AB_ENV("STE_ADAMW_NT");
+  if (!(ent && ent[0] == '0'))
+    hipLaunchKernelGGL(adamw_kernel<true>, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, p, g, m, v,
+                       (bf16*)p_bf16, n, lr, beta1, beta2, eps, wd, bc1, bc2s, sumsq, max_norm);
+  else
+  hipLaunchKernelGGL(adamw_kernel<false>, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, p, g, m, v, (bf16*)p_bf16, n,
                      lr, beta1, beta2, eps, wd, bc1, bc2s, sumsq, max_norm);
   STE_CHECK_LAUNCH();
   return 0;
