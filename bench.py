@@ -440,7 +440,7 @@ def main(argv=None):
                  "c5-shape (MX-fp8 Conformer fwd GEMMs)")
     else:
         cname = "custom"
-    peak = FP8_PEAK_TFLOPS if dom == "gemm_mx8_kernel" else BF16_PEAK_TFLOPS
+    peak = FP8_PEAK_TFLOPS if dom in ("gemm_mx8_kernel", "gemm_8ph_kernel<mx8>") else BF16_PEAK_TFLOPS
     traffic, traffic_src = hbm_traffic(dom, c5=c5)
     out = {
         "metric": ("evaluated audio–text pairs/sec, forward only (whole node), 10s@16kHz + 64-tok" if args.eval else

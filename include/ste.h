@@ -139,6 +139,13 @@ int ste_gemm_mx8(const ste_gemm_args* args, const void* a_scales, const void* b_
  * 4 GiB because its DMA sources are 32-bit offsets), 0 = the single-stage kernel (64-bit
  * addressing, any shape).  q_out: whether an MX-fp8 output copy is requested. */
 int ste_gemm_mx8_kernel(const ste_gemm_args* args, int q_out);
+/* Plan thresholds (process-wide, host-only): the fewest 256x256 output tiles for which ste_gemm
+ * plans the persistent 8-phase bf16 kernel and ste_gemm_mx8 the 8-phase MX one (both 240 by
+ * default: about one wave of 256 CUs).  A value <= 0 leaves that threshold unchanged; the previous
+ * values are returned through prev_bf16 / prev_mx8 (either may be NULL).  Parity tests lower them
+ * so that a B <= 4 batch runs the same kernel instantiations as the b = 64 bench step; the planned
+ * kernels accept any tile count (partial edge tiles take their guarded epilogue). */
+int ste_gemm_plan_min_tiles(int bf16_tiles, int mx8_tiles, int* prev_bf16, int* prev_mx8);
 /* bf16 x [rows][K] (row stride ldx) -> e4m3 q [rows][K] and E8M0 scales [rows][K/32]:
  * scale 2^e, e = ceil(log2(amax/448)) per 32-element block (no saturation; zero blocks 2^-127). */
 int ste_mx8_quant(const void* x, int64_t ldx, int rows, int K, void* q, void* scales, void* stream);

@@ -147,6 +147,7 @@ _SIGS = {
                           c_void_p]),
     "ste_gemm_mx8": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ste_gemm_mx8_kernel": (c_int, [C.POINTER(GemmArgs), c_int]),
+    "ste_gemm_plan_min_tiles": (c_int, [c_int, c_int, C.POINTER(c_int), C.POINTER(c_int)]),
     "ste_mx8_quant": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "ste_attn_pool_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -83,6 +83,10 @@ def load_checkpoint(path, model=None, optimizer=None, *, map_location=None, stri
     (strict by default, as inference.py does) and optimizer_state_dict into `optimizer` (a
     FusedAdamW or TrainStep) when given; returns the checkpoint dict."""
     ckpt = _safe_load(path, map_location if map_location is not None else "cpu")
+    if optimizer is not None and hasattr(optimizer, "sync"):
+        # an update still running on the optimizer's own stream (overlap_optimizer) writes the
+        # master weights: the load below must come after it, not race it
+        optimizer.sync()
     if model is not None:
         model.load_state_dict(ckpt["model_state_dict"], strict=strict)
     if optimizer is not None and "optimizer_state_dict" in ckpt:

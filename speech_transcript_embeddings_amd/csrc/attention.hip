@@ -910,9 +910,12 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_rel2_kernel(ste_attn_args a) {
       }
       // natural-log LSE.  A row whose every key is masked (scores all finfo.min, as in the
       // reference: a uniform distribution over the T keys) is stored as -inf: fp32 cannot
-      // hold finfo.min + log(T), and the v2 backward kernels read -inf as "p = 1/T".
+      // hold finfo.min + log(T), and the v2 backward kernels read -inf as "p = 1/T".  SPLIT: the LSE
+      // from the same MFMA sum of hi + lo P that normalised O (as rel4), so the backward's p sums to
+      // the weights O was formed with and Σ dS stays 0
       if (g == 0)
-        a.lse[(int64_t)(b * H + h) * T + myq] = m[gq] == NEG_MASK ? -INFINITY : (m[gq] + log2f(l[gq])) * LN2;
+        a.lse[(int64_t)(b * H + h) * T + myq] =
+            m[gq] == NEG_MASK ? -INFINITY : (m[gq] + log2f(SPLIT ? lw[gq][0] : l[gq])) * LN2;
     }
   }
 }

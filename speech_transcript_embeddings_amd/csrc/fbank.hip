@@ -181,11 +181,11 @@ __global__ __launch_bounds__(256) void fbank_logmel_kernel(const float* __restri
     const int st = sm_start[m], ln = sm_len[m], of = sm_off[m];
     float acc = 0.f;
     for (int i = 0; i < ln; ++i) acc += sm_w[of + i] * pw[st + i];
-    // the reference logs the float64 mel energies and rounds to float32 (np.log(...).astype(float32)).
-    // At the floor (silent frames) that exact constant matters: a clip's identical rows leave
-    // numpy's CMVN rounding residue in the output, so it is the float64 log rounded once; above
-    // it, fp32 logf (<= 1 ulp) is far inside the FFT's own fp32 rounding
-    out[m] = acc > MEL_FLOOR ? logf(acc) : LOG_MEL_FLOOR;
+    // the reference logs the float64 mel energies and rounds to float32 (np.log(...).astype(float32)):
+    // the float64 log rounded once, as there (one scalar per mel bin per frame: cheap here).  At the
+    // floor (silent frames) that exact constant matters most: a clip's identical rows leave numpy's
+    // CMVN rounding residue in the output
+    out[m] = acc > MEL_FLOOR ? (float)log((double)acc) : LOG_MEL_FLOOR;
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();

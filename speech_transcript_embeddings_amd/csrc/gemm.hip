@@ -1690,15 +1690,19 @@ bool big_ok_shape(const ste_gemm_args& a) {
   if (!a.b_kc && (a.N % 8)) return false;
   return true;
 }
+// plan thresholds (ste_gemm_plan_min_tiles; the A/B build also reads STE_GEMM_MIN_TILES)
+int g_min_tiles_bf16 = -1, g_min_tiles_mx8 = 240;
+int min_tiles_bf16() {
+  if (g_min_tiles_bf16 < 0) {
+    const char* e = STE_AB_ENV("STE_GEMM_MIN_TILES");
+    g_min_tiles_bf16 = e ? atoi(e) : 240;
+  }
+  return g_min_tiles_bf16;
+}
 bool big_ok(const ste_gemm_args& a) {
   if (!big_ok_shape(a)) return false;
   const long tiles = (long)((a.M + 255) / 256) * ((a.N + 255) / 256) * a.batch;
-  static int min_tiles = -1;   // STE_GEMM_MIN_TILES: A/B of the small-kernel threshold
-  if (min_tiles < 0) {
-    const char* e = STE_AB_ENV("STE_GEMM_MIN_TILES");
-    min_tiles = e ? atoi(e) : 240;
-  }
-  return tiles >= min_tiles;
+  return tiles >= min_tiles_bf16();
 }
 
 }  // namespace
@@ -2088,7 +2092,7 @@ int mx8_ef(const ste_gemm_args& a, bool q_out) { return epi_flags(a) | (q_out ? 
 bool mx8_8ph_plan(const ste_gemm_args& a, bool q_out) {
   if (!mx8_8ph_on() || gemm_mode() != 2) return false;
   const int64_t nb = (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256);
-  if (nb < 240 || (q_out && (a.N % 256) != 0)) return false;   // fp8 copy per FULL 256-column tile
+  if (nb < g_min_tiles_mx8 || (q_out && (a.N % 256) != 0)) return false;   // fp8 copy per FULL 256-column tile
   const uint64_t lim = 1ull << 32;
   if ((uint64_t)a.M * (uint64_t)a.lda >= lim || (uint64_t)a.N * (uint64_t)a.ldb >= lim) return false;
   const int ef = mx8_ef(a, q_out);
@@ -2118,6 +2122,14 @@ int launch_mx8_8ph(const ste_gemm_args& a8, const Mx8Args& mx, hipStream_t s) {
   return -1;   // other epilogues: the single-stage kernel
 }
 }  // namespace
+
+extern "C" int ste_gemm_plan_min_tiles(int bf16_tiles, int mx8_tiles, int* prev_bf16, int* prev_mx8) {
+  if (prev_bf16) *prev_bf16 = min_tiles_bf16();
+  if (prev_mx8) *prev_mx8 = g_min_tiles_mx8;
+  if (bf16_tiles > 0) g_min_tiles_bf16 = bf16_tiles;
+  if (mx8_tiles > 0) g_min_tiles_mx8 = mx8_tiles;
+  return 0;
+}
 
 extern "C" int ste_gemm_mx8_kernel(const ste_gemm_args* args, int q_out) {
   if (!args) return STE_ERR_ARG;

@@ -124,7 +124,9 @@ def gemm(a, b, *, a_kc=True, b_kc=True, M=None, N=None, K=None, out=None, out_bf
 
         def launch():
             call("ste_gemm_mx8", C.byref(args), ptr(mx8[0]), ptr(mx8[1]), ptr(q8[0]), ptr(q8[1]), _s())
-        name = "gemm_mx8_kernel"
+        # which MX kernel the library plans (the persistent 8-phase one or the single-stage one)
+        name = "gemm_mx8_kernel" if GEMM_TRACE is None or not int(fn("ste_gemm_mx8_kernel")(
+            C.byref(args), int(q8[0] is not None))) else "gemm_8ph_kernel<mx8>"
     elif f32:
         def launch():
             call("ste_gemm_f32", C.byref(args), _s())
@@ -190,6 +192,28 @@ def gemm_kernel_name(args: GemmArgs) -> str:
     buf = C.create_string_buffer(128)
     call("ste_gemm_kernel_name", C.byref(args), buf, 128)
     return buf.value.decode()
+
+
+def gemm_plan_min_tiles(bf16=0, mx8=0):
+    """Set the 8-phase kernels' plan thresholds (ste_gemm_plan_min_tiles: fewest 256x256 output
+    tiles; <= 0 keeps one) and return the previous (bf16, mx8) pair."""
+    pb, pm = C.c_int(), C.c_int()
+    call("ste_gemm_plan_min_tiles", int(bf16), int(mx8), C.byref(pb), C.byref(pm))
+    return pb.value, pm.value
+
+
+class bench_gemm_plan:
+    """Context manager for parity tests: every GEMM with at least one 256x256 output tile is planned
+    on the persistent 8-phase kernels (bf16 and MX-fp8) the b = 64 bench step runs, so a B <= 4
+    batch exercises the same compile-time epilogue instantiations (their guarded partial-tile path
+    at the edges); the library's thresholds are restored on exit."""
+
+    def __enter__(self):
+        self.prev = gemm_plan_min_tiles(1, 1)
+        return self
+
+    def __exit__(self, *exc):
+        gemm_plan_min_tiles(*self.prev)
 
 
 def linear(x, w, bias=None, **kw):

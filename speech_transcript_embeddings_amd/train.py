@@ -70,6 +70,14 @@ class FusedAdamW:
         self.sumsq_part = torch.zeros(ops.SUMSQ_PARTS, device=st.device, dtype=torch.float64)  # ordered Σg²
         self.t = 0
         self.last_factor = 1.0
+        # the event after the last update when it ran on another stream (TrainStep's
+        # overlap_optimizer): every host-side read or write of the optimizer's buffers waits on it
+        self.tail = None
+
+    def sync(self):
+        """Order the current stream after the last update (a no-op when it ran on this stream)."""
+        if self.tail is not None:
+            torch.cuda.current_stream(self.store.device).wait_event(self.tail)
 
     # ------------------------------------------------------- torch.optim format
     def _ref_groups(self):
@@ -99,6 +107,7 @@ class FusedAdamW:
                 return self.state_dict()
             finally:
                 self.last_factor = saved
+        self.sync()
         st = self.store
         state, groups, idx = {}, [], 0
         for gi, names in enumerate(self._ref_groups()):
@@ -121,6 +130,7 @@ class FusedAdamW:
         base learning rates (initial_lr, or lr without a scheduler) and the shared
         betas / eps / weight decay."""
         st = self.store
+        self.sync()   # the moments are rewritten below: after the last update has read them
         ref = self._ref_groups()
         pgs = sd["param_groups"]
         if len(pgs) != len(ref) or any(len(g["params"]) != len(r) for g, r in zip(pgs, ref)):
@@ -157,7 +167,9 @@ class FusedAdamW:
 
     def total_norm(self):
         """clip_grad_norm_'s return value for the last step (the pre-clip global gradient norm);
-        reads the on-device Σg² (host sync)."""
+        reads the on-device Σg² (host sync), after the update that produced it (overlap_optimizer:
+        another stream, which the current one would not otherwise wait for)."""
+        self.sync()
         return math.sqrt(float(self.sumsq.item()))
 
     def step(self, lr_factor: float = 1.0, phases=None, on_phase=None):
@@ -200,6 +212,7 @@ class FusedAdamW:
         return events
 
     def zero_grad(self):
+        self.sync()   # the last update has read the gradients
         self.store.grad.zero_()
 
 
@@ -236,9 +249,10 @@ class GradSync:
     transcript to max_text_length, ref :838-851); a step with more ids than a configured capacity
     raises on every rank alike only if every rank's count exceeds it, so the configured value must
     be a true bound.  When the caller cannot say, the capacity is agreed on EVERY optimizer step by
-    ensure_capacity() (a MAX all-reduce that TrainStep makes before the step's kernels are queued),
-    so ranks with different token counts (length-bucketed padding) always take the same path.  A
-    step's backward therefore holds no collective of its own and no host wait.
+    start_capacity() (a MAX all-reduce that TrainStep starts before the step's kernels are queued,
+    on a stream of its own, read back at the text stage), so ranks with different token counts
+    (length-bucketed padding) always take the same path.  A step's backward therefore holds no
+    collective of its own and no host wait on the step's streams.
     `finish()` waits for every collective (on the current stream) before clip + AdamW.
     """
 
@@ -259,6 +273,8 @@ class GradSync:
         self.capacity = None if word_capacity is None else int(word_capacity)
         self.configured = word_capacity is not None
         self._agreed = False   # unconfigured: the capacity was agreed for the current step
+        self._pending_cap = None   # start_capacity()'s (event, pinned host value, device value)
+        self._cap_stream = None
         grad_slots = [sl for sl in store.slots.values() if sl.segment in ("enc", "head")]
 
         ordered = sorted(grad_slots, key=lambda x: x.offset)
@@ -328,8 +344,7 @@ class GradSync:
     def ensure_capacity(self, n_ids: int) -> int:
         """The step's word-table exchange capacity.  Configured: checked (raises when a step
         carries more ids).  Not configured: the MAX of every rank's n_ids, agreed with a blocking
-        all-reduce on every call — TrainStep makes that call once per optimizer step, before the
-        step's kernels are queued, so it never stalls a backward and never goes stale."""
+        all-reduce (TrainStep uses start_capacity(), which does not block the host)."""
         if not self.active() or self.words is None:
             return int(n_ids)
         if not self.configured:
@@ -339,9 +354,43 @@ class GradSync:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             self.capacity = int(t.item())
             self._agreed = True
+            self._pending_cap = None
         elif n_ids > self.capacity:
             raise RuntimeError(f"{n_ids} token ids in one step exceed the word-table exchange capacity "
                                f"{self.capacity} (TrainStep(micro_batch=, max_text_length=) sets it)")
+        return self.capacity
+
+    def start_capacity(self, n_ids: int):
+        """ensure_capacity() without a host wait, for TrainStep: made once per optimizer step before
+        the step's kernels are queued.  Not configured, on RCCL: the MAX all-reduce runs on a stream
+        of its own (nothing queued there to wait for) and its result is copied to pinned host memory
+        under an event, which the text stage reads (resolve) — so the host keeps running ahead of
+        the GPU instead of draining the previous step at every step start.  Gloo (host
+        tensors) and configured capacities: ensure_capacity() itself."""
+        if not self.active() or self.words is None:
+            return
+        dev = self.store.device
+        if self.configured or not (dist.get_backend() == "nccl" and dev.type == "cuda"):
+            self.ensure_capacity(n_ids)
+            return
+        if self._cap_stream is None:
+            self._cap_stream = torch.cuda.Stream(device=dev)
+        with torch.cuda.stream(self._cap_stream):
+            t = torch.tensor([int(n_ids)], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=True).wait()   # this stream waits for it
+            host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+            host.copy_(t, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        self._pending_cap = (ev, host, t)
+        self._agreed = True
+
+    def _agreed_capacity(self) -> int:
+        if self._pending_cap is not None:
+            ev, host, _ = self._pending_cap
+            ev.synchronize()
+            self.capacity = int(host.item())
+            self._pending_cap = None
         return self.capacity
 
     def _sparse_words(self, ids, cap_ids):
@@ -378,7 +427,7 @@ class GradSync:
             if self.configured or not self._agreed:
                 n = self.ensure_capacity(ids.numel() if ids is not None else 0)
             else:   # agreed for this step before its kernels were queued
-                n = self.capacity
+                n = self._agreed_capacity()
             self._agreed = False
             if ids is not None and self.sparse_pays(n):   # n, hence the choice, equal on every rank
                 self._sparse_words(ids, n)
@@ -638,7 +687,7 @@ class TrainStep:
         if self._micro + 1 == self.acc:   # the window's last micro-batch: check the word-table exchange
             # capacity (agreed across ranks here if not configured) before any kernel is queued
             n_ids = batch["input_ids_pos"].numel() + batch["input_ids_neg"].numel()
-            self.gradsync.ensure_capacity(n_ids + sum(int(t.numel()) for t in (self._ids if self._micro else [])))
+            self.gradsync.start_capacity(n_ids + sum(int(t.numel()) for t in (self._ids if self._micro else [])))
         tf_p, tf_n, af, align, ctx = eng.forward(batch, True)
         B, P = af.shape
         # L2 normalise, similarity matrix S = A·[Tp;Tn]^T (fp32 MFMA), loss on its diagonals
@@ -706,6 +755,7 @@ class TrainStep:
                 self.sched.step()
                 self._opt_tail = torch.cuda.Event()
                 self._opt_tail.record()
+            self.opt.tail = self._opt_tail
         else:
             self.gradsync.finish()
             self.opt.step(self.sched.factor())  # reference order: optimizer.step() then scheduler.step()

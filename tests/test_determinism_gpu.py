@@ -77,13 +77,17 @@ def test_overlapped_optimizer_bitwise_equal():
         for i in range(3):                     # back to back: step i+1's forward overlaps step i's AdamW
             torch.manual_seed(100 + i)
             losses.append(step(*batches[i]).clone())
+        # read straight after the step, without step.sync(): total_norm() itself must wait for the
+        # optimizer stream's Σg²
+        tnorm = step.opt.total_norm()
         step.sync()
         torch.cuda.synchronize()
         st = model.store
         out.append((torch.stack(losses), st.grad[: st.n_grad].clone(), st.master.clone(), step.opt.exp_avg.clone(),
-                    step.opt.exp_avg_sq.clone(), st.shadow.clone()))
-    (l0, g0, m0, a0, v0, s0), (l1, g1, m1, a1, v1, s1) = out
+                    step.opt.exp_avg_sq.clone(), st.shadow.clone(), tnorm))
+    (l0, g0, m0, a0, v0, s0, n0), (l1, g1, m1, a1, v1, s1, n1) = out
     assert torch.equal(l0, l1), (l0.tolist(), l1.tolist())
+    assert n0 == n1 and n0 > 0, (n0, n1)
     assert torch.equal(g0, g1)
     assert torch.equal(m0, m1) and torch.equal(a0, a1) and torch.equal(v0, v1) and torch.equal(s0, s1)
     assert float((a0 != 0).sum()) > 0

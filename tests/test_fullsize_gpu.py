@@ -72,7 +72,24 @@ CONFIGS = {  # name: (batch, samples, tokens, unfreeze k, align, freeze_encoders
     "c5_fp8bwd": (1, 480000, 64, 3, False, "none", "bwd", True),
     # end to end with arbitrary fp32 master weights: the bf16 quantisation of the weights included
     "c2_fp32w": (2, 160000, 64, 3, False, "partial", False, False),
+    # the bench's kernel plan: every GEMM with a 256x256 output tile on the
+    # persistent 8-phase kernels (ops.bench_gemm_plan), so this B = 2 / B = 1 instance runs the
+    # compile-time epilogue instantiations the b = 64 step runs (<515,1>, <516,11>, <548,11>,
+    # <65,0>, <72,0>, <513,0>, <512,0> ...) and, at c5 with fp8, the 8-phase MX-fp8 kernel
+    "c2_8ph": (2, 160000, 64, 3, False, "partial", False, True),
+    "c5_fp8_8ph": (1, 480000, 64, 3, False, "none", True, True),
 }
+BENCH_PLAN = {"c2_8ph", "c5_fp8_8ph"}
+# Seeded draws of (weights, clips, cotangents) per bf16-exact config: draw 0 is the original
+# instance (model 0, data 3, cotangent 5); draw d >= 1 is profiles/r5_seed_sweep.py's seed d - 1
+# (model 100 + d - 1, data 200 + d - 1, cotangent 300 + d - 1).
+DRAWS = {"c1": 3, "c2": 3, "c4": 3, "c5": 3}
+CASES = [(c, d) for c in CONFIGS for d in range(DRAWS.get(c, 1))]
+EXCESS = {}   # config -> {draw: HIP's worst audio tensor minus the same-instance floor's worst}
+
+
+def _seeds(draw):
+    return (0, 3, 5) if draw == 0 else (100 + draw - 1, 200 + draw - 1, 300 + draw - 1)
 
 
 def _rel(a, b):
@@ -130,7 +147,8 @@ def _floor_errs(sd, feats, acfg, trainable, cap, probe_kw=None):
 def _hip_vs_oracle(cname, model_seed=0, data_seed=3, cot_seed=5):
     """The HIP path's forward + backward on random output cotangents and the oracle's on the same
     weights and inputs; returns the per-tensor gradient errors and what the floor emulation needs.
-    The seeds default to the test's instance (profiles/r5_seed_sweep.py draws others)."""
+    The seeds default to the test's instance (profiles/r5_seed_sweep.py draws others).  BENCH_PLAN
+    configs run the HIP side under ops.bench_gemm_plan() and record the GEMM kernels it launched."""
     from speech_transcript_embeddings_amd.model import EnhancedAudioTextModel
     from speech_transcript_embeddings_amd.train import synthetic_batch
     B, N, L, k, align, freeze, fp8, exact = CONFIGS[cname]
@@ -157,16 +175,27 @@ def _hip_vs_oracle(cname, model_seed=0, data_seed=3, cot_seed=5):
         return r
 
     A.align_forward = capture
+    plan = ops.bench_gemm_plan() if cname in BENCH_PLAN else None
+    kernels = set()
+    if plan is not None:
+        plan.__enter__()
+        ops.GEMM_TRACE = []
     try:
-        outs = list(EnhancedAudioTextModel.compute_pos_neg_embeddings(model, batch))
+        try:
+            outs = list(EnhancedAudioTextModel.compute_pos_neg_embeddings(model, batch))
+        finally:
+            A.align_forward = fwd
+        if align:
+            outs.append(model.last_alignment_scores)
+        g = torch.Generator().manual_seed(cot_seed)
+        cots = [torch.randn(o.shape, generator=g) for o in outs]
+        torch.autograd.backward(outs, [c.cuda() for c in cots])
+        torch.cuda.synchronize()
     finally:
-        A.align_forward = fwd
-    if align:
-        outs.append(model.last_alignment_scores)
-    g = torch.Generator().manual_seed(cot_seed)
-    cots = [torch.randn(o.shape, generator=g) for o in outs]
-    torch.autograd.backward(outs, [c.cuda() for c in cots])
-    torch.cuda.synchronize()
+        if plan is not None:
+            kernels = {t[0] for t in ops.GEMM_TRACE}
+            ops.GEMM_TRACE = None
+            plan.__exit__(None, None, None)
 
     if freeze == "none":
         cfg = R.ModelCfg(use_word_alignment=align, text_layers_to_unfreeze=12, audio_layers_to_unfreeze=24)
@@ -227,19 +256,37 @@ def _hip_vs_oracle(cname, model_seed=0, data_seed=3, cot_seed=5):
         assert params[n].grad is not None, n
         errs.append((_rel(params[n].grad, p[n].grad), n))
     errs.sort(reverse=True)
-    return dict(errs=errs, sd=sd, bc=bc, cfg=cfg, trainable=trainable, cap=tap.cap, p=p, flips=flips)
+    return dict(errs=errs, sd=sd, bc=bc, cfg=cfg, trainable=trainable, cap=tap.cap, p=p, flips=flips,
+                kernels=kernels)
+
+
+# the 8-phase instantiations a bench-plan instance must have launched (the c2 step's hot epilogues)
+BENCH_KERNELS = {
+    "c2_8ph": {"gemm_8ph_kernel<true, true, 515, 1>", "gemm_8ph_kernel<true, true, 516, 11>",
+               "gemm_8ph_kernel<true, true, 548, 11>", "gemm_8ph_kernel<true, true, 65, 0>",
+               "gemm_8ph_kernel<true, true, 72, 0>", "gemm_8ph_kernel<true, true, 513, 0>",
+               "gemm_8ph_kernel<true, true, 512, 0>"},
+    "c5_fp8_8ph": {"gemm_8ph_kernel<mx8>", "gemm_8ph_kernel<true, true, 548, 11>",
+                   "gemm_8ph_kernel<true, true, 512, 0>"},
+}
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("cname", list(CONFIGS))
-def test_full_size_vs_oracle(cname):
+@pytest.mark.parametrize("cname,draw", CASES, ids=[f"{c}-d{d}" if DRAWS.get(c, 1) > 1 else c for c, d in CASES])
+def test_full_size_vs_oracle(cname, draw):
     B, N, L, k, align, freeze, fp8, exact = CONFIGS[cname]
-    r = _hip_vs_oracle(cname)
+    r = _hip_vs_oracle(cname, *_seeds(draw))
     errs, sd, bc, cfg, trainable, p, flips = (r[x] for x in ("errs", "sd", "bc", "cfg", "trainable", "p", "flips"))
     assert len(errs) > 50
     median = errs[len(errs) // 2][0]
-    print(f"[{cname}] grad rel err ({'bf16-exact' if exact else 'fp32 master'} weights): worst {errs[:6]}, "
+    tag = f"{cname} draw {draw}" if DRAWS.get(cname, 1) > 1 else cname
+    print(f"[{tag}] grad rel err ({'bf16-exact' if exact else 'fp32 master'} weights): worst {errs[:6]}, "
           f"median {median:.2e}, n={len(errs)}, gate flips {flips}")
+    if cname in BENCH_PLAN:
+        print(f"[{tag}] GEMM kernels launched: {sorted(r['kernels'])}")
+        missing = BENCH_KERNELS[cname] - r["kernels"]
+        assert not missing, (missing, sorted(r["kernels"]))
+        assert not any(kn.startswith("gemm_bf16_kernel<true") for kn in r["kernels"]), sorted(r["kernels"])
     if fp8 == "bwd":
         # MX-fp8 forward AND input-gradient GEMMs (dY and Wᵀ in e4m3 with 32-k block scales; the
         # weight gradients bf16): the backward's own e4m3 rounding of every layer's dY compounds
@@ -263,12 +310,19 @@ def test_full_size_vs_oracle(cname):
                        if not n.endswith(("linear_k.bias", "attention.2.bias")))   # true gradient 0
         fl = sorted(((e, n) for n, e in floor.items() if not n.endswith(("linear_k.bias", "attention.2.bias"))),
                     reverse=True)
-        bound_audio = max(1e-2, fl[0][0] + 1e-3)
+        # per draw: + 0.3 points over the floor (a single draw carries about +-0.2 points of
+        # realisation noise, profiles/r5_seed_sweep.jsonl); the draws' MEAN excess is bounded at
+        # 0.1 points by test_full_size_mean_excess
+        bound_audio = max(1e-2, fl[0][0] + 3e-3)
         aud = [(e, n) for e, n in errs if n.startswith(("audio_encoder.", "audio_pooling."))]
         rest = [(e, n) for e, n in errs if not n.startswith(("audio_encoder.", "audio_pooling."))]
-        print(f"[{cname}] same-instance bf16 floor (audio, emulated): worst {fl[:4]}, median "
+        excess = aud[0][0] - fl[0][0]
+        EXCESS.setdefault(cname, {})[draw] = excess
+        print(f"[{tag}] same-instance bf16 floor (audio, emulated): worst {fl[:4]}, median "
               f"{fl[len(fl) // 2][0]:.2e}; emulation-vs-oracle fp32 {emul_err:.1e}; audio bound {bound_audio:.4f}")
-        print(f"[{cname}] HIP vs floor on HIP's worst audio tensors: "
+        print(f"[{tag}] HIP worst audio {aud[0][0]:.4f} ({aud[0][1]}), floor worst {fl[0][0]:.4f} ({fl[0][1]}): "
+              f"excess {excess * 100:+.3f} points")
+        print(f"[{tag}] HIP vs floor on HIP's worst audio tensors: "
               + ", ".join(f"{n.replace('audio_encoder.encoder.', '')} {e:.4f}/{floor.get(n, float('nan')):.4f}"
                           for e, n in aud[:8]))
         assert emul_err < 1e-4, emul_err
@@ -281,3 +335,16 @@ def test_full_size_vs_oracle(cname):
         # tensors by 1.33 % worst, and under bf16 autocast by 4.8 % (profiles/r4_bf16_floor.txt)
         assert median < 1e-2, median
         assert errs[0][0] < 2.5e-2, errs[:5]
+
+
+@pytest.mark.parametrize("cname", [c for c in DRAWS if DRAWS[c] > 1])
+def test_full_size_mean_excess(cname):
+    """Over the config's seeded draws, HIP's worst audio tensor sits at the same-instance bf16
+    floor on average: mean excess <= 0.1 points (each draw: <= 0.3, checked above)."""
+    ex = EXCESS.get(cname, {})
+    if len(ex) < DRAWS[cname]:
+        pytest.skip(f"needs all {DRAWS[cname]} draws of {cname} in this session (ran {sorted(ex)})")
+    mean = sum(ex.values()) / len(ex)
+    print(f"[{cname}] excess over the floor per draw (points): "
+          + ", ".join(f"d{d} {e * 100:+.3f}" for d, e in sorted(ex.items())) + f"; mean {mean * 100:+.3f}")
+    assert mean <= 1e-3, ex

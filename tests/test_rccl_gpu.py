@@ -12,7 +12,8 @@ them) and runs one full-dims TrainStep (w2v-bert-2.0 Conformer + XLM-R, B = 2, 1
     word-table slice are snapshotted (on the step's stream) right before their collective is
     enqueued, and compared after GradSync.finish() — a one-rank AVG / gather / reduce-scatter /
     row re-accumulation must be the identity;
-  * the word-table capacity is the configured one (no per-step agreement collective).
+  * the word-table capacity is the configured one (no per-step agreement collective); without
+    one, the per-step MAX agreement is a single asynchronous all-reduce (GradSync.start_capacity).
 """
 import os
 import socket
@@ -90,8 +91,18 @@ def _child(port, q):
         out["n_grad"] = gs.store.n_grad
         out["bitwise"] = all(torch.equal(g[a:b], s) for (a, b), s in snaps)
         out["nonzero"] = bool(g[: gs.store.n_grad].abs().sum() > 0)
-        out["calls"] = calls
+        out["calls"] = list(calls)
         out["metrics"] = step.epoch_metrics()
+        # capacity NOT configured: agreed per optimizer step by an async MAX all-reduce on a stream of
+        # its own (GradSync.start_capacity), read back at the text stage without a host drain
+        del calls[:]
+        step2 = TR.TrainStep(model, lr=1e-3, warmup=1, total_steps=10)
+        gs2, caps = step2.gradsync, []
+        sparse2 = gs2._sparse_words
+        gs2._sparse_words = lambda ids, cap: (caps.append(cap), sparse2(ids, cap))[1]
+        out["loss2_finite"] = bool(torch.isfinite(step2(*data)).all())
+        torch.cuda.synchronize()
+        out["calls2"], out["caps2"] = list(calls), caps
         q.put(out)
     except Exception:
         import traceback
@@ -126,3 +137,7 @@ def test_rccl_world1_full_step():
     assert out["covered"] >= 0.95 * out["n_grad"], (out["covered"], out["n_grad"])
     assert out["nonzero"] and out["loss_finite"]
     assert out["metrics"]["samples"] == 2 and out["metrics"]["optimizer_steps"] == 1
+    # unconfigured capacity: one asynchronous MAX all-reduce per optimizer step, the agreed value used
+    assert [c for c in out["calls2"] if c[0] == "all_reduce" and c[1] is not None and "MAX" in c[1]] == \
+        [("all_reduce", str(torch.distributed.ReduceOp.MAX), True, True)], out["calls2"]
+    assert out["caps2"] == [2 * 2 * 64] and out["loss2_finite"]
