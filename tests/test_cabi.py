@@ -147,6 +147,34 @@ def test_gemm_mx8_plan(lib):
     assert k(C.byref(a), 0) == 0
 
 
+def test_gemm_plan_min_tiles(lib):
+    """ste_gemm_plan_min_tiles (host-only): the tile counts from which the persistent 8-phase bf16 /
+    MX-fp8 kernels are planned (240 by default); the parity tests lower them to 1 (ops.bench_gemm_plan)
+    so that a B <= 4 instance runs the compile-time epilogue instantiations of the b = 64 step, then
+    restore them."""
+    f = lib.fn("ste_gemm_plan_min_tiles")
+    pb, pm = C.c_int(), C.c_int()
+    assert f(0, 0, C.byref(pb), C.byref(pm)) == 0
+    assert (pb.value, pm.value) == (240, 240)
+    k, km = lib.fn("ste_gemm_kernel"), lib.fn("ste_gemm_mx8_kernel")
+    a = lib.GemmArgs()   # FFN-in of a B = 2 c2 instance: 998 rows, 4 x 16 tiles, bias + swish + C2, bf16 out
+    a.M, a.N, a.K, a.batch, a.a_kc, a.b_kc, a.lda, a.ldb = 998, 4096, 1024, 1, 1, 1, 1024, 1024
+    a.C, a.c_bf16, a.bias, a.C2, a.act = 1, 1, 1, 1, 1
+    b = lib.GemmArgs()   # MX-fp8 FFN-out of a B = 1 c5 instance: 1,499 rows, 6 x 4 tiles, bias + residual
+    b.M, b.N, b.K, b.batch, b.a_kc, b.b_kc, b.lda, b.ldb = 1499, 1024, 4096, 1, 1, 1, 4096, 4096
+    b.C, b.bias, b.R = 1, 1, 1
+    assert k(C.byref(a)) == 0 and km(C.byref(b), 0) == 0
+    f(1, 1, None, None)
+    try:
+        assert k(C.byref(a)) == 8 and km(C.byref(b), 0) == 1
+        buf = C.create_string_buffer(128)
+        lib.fn("ste_gemm_kernel_name")(C.byref(a), buf, 128)
+        assert buf.value == b"gemm_8ph_kernel<true, true, 515, 1>"
+    finally:
+        f(pb.value, pm.value, None, None)
+    assert k(C.byref(a)) == 0 and km(C.byref(b), 0) == 0
+
+
 def test_argument_errors_return_status_without_launch(lib):
     """Shape/alignment contract violations come back as non-zero status (-> SteError), never a launch."""
     a = lib.GemmArgs()
