@@ -16,7 +16,8 @@ slabs, ordered column sums over another tiling, 16 accumulated micro-batches), a
 the backward can round the other way, and the rounding then travels like any other bf16 rounding
 of the step.  So the comparison is stated at two levels:
   * random output cotangents (the autograd path, gradients accumulated over the micro-batches):
-    agreement to that rounding — measured on the GPU and bounded in the test;
+    agreement to that rounding (embeddings within ~one bf16 rounding, gradients at the bf16
+    floor's level) — measured on the GPU and bounded in the test;
   * the loss-derived TrainStep gradients: the loss's near-cancelling clean / corrupted difference
     amplifies any bf16 difference (the mini loss-derived elementwise errors are
     1.2-1.85 %), so two bf16 realizations of the step differ at the level of the bf16 floor itself;
@@ -107,9 +108,14 @@ def test_c2_batch64_plan_matches_micro_batches_random_cotangents():
     print(f"[plan equivalence, random cotangents] embeddings rel {emb:.2e}; per-tensor gradient rel err "
           f"b=64 vs 16x4: median {median:.2e}, worst {errs[:5]}, n={len(errs)}")
     assert len(errs) > 50
-    assert emb < 1e-5, emb
-    assert median < 1e-3, median
-    assert errs[0][0] < 1e-2, errs[:5]
+    # two bf16 realizations of the same forward (module docstring): the fp32 sums that run in another
+    # order round some bf16 activations the other way, and that travels through 24 layers.  Measured
+    # (profiles/r6f/tests.log): embeddings 5.9e-4, gradient median 6.9e-4, worst 1.12 % (the audio
+    # pooling scorer, the tensor whose own bf16 floor against the oracle is ~1 %); a broken
+    # instantiation gives O(1) errors (the round-3 MX scale-select bug: ~0 for 3/4 of every tile).
+    assert emb < 2e-3, emb          # ~ one bf16 rounding (2^-9) of the embedding
+    assert median < 2e-3, median
+    assert errs[0][0] < 2e-2, errs[:5]
 
 
 @pytest.mark.timeout(600)
