@@ -55,10 +55,21 @@ def main():
     tot = sum(g for g, _, _ in gaps if g > 0) / 1e3
     print(f"main queue: gaps between consecutive kernels {tot:.1f} ms ({tot / a.steps:.2f} ms/step), "
           f"{sum(1 for g, _, _ in gaps if g > 5)} gaps > 5 us")
+    def short(name):
+        name = name.replace("void ", "").replace("(anonymous namespace)::", "")
+        for cut in ("(", "<", " "):
+            if cut == "<" and name.startswith("gemm_8ph_kernel"):
+                name = name[:name.find(">") + 1] if ">" in name else name
+                continue
+            i = name.find(cut)
+            if i > 0 and not (cut == "<" and "gemm" in name):
+                name = name[:i]
+        return name[:70]
+
     hist = defaultdict(float)
     for g, p, n in gaps:
         if g > 0:
-            hist[(p.split('(')[0][-60:], n.split('(')[0][-60:])] += g
+            hist[(short(p), short(n))] += g
     for (p, n), g in sorted(hist.items(), key=lambda kv: -kv[1])[:15]:
         print(f"  {g / a.steps:8.1f} us/step  {p}  ->  {n}")
 
