@@ -34,7 +34,8 @@ def main():
             if m:
                 cur = m.group(1)
             t = TAG.search(raw.split(" PASSED")[0].split(" FAILED")[0])
-            if t and not raw.startswith("[r6] "):
+            if t and not raw.startswith("[r6] ") and not t.group(1).startswith("[c10d]") \
+                    and t.group(1).rstrip("] [").strip() not in ("[align", "[align]"):
                 lines.append(t.group(1))
             if re.search(r"=+ .*(passed|failed).* =+", raw):
                 lines.append(raw.strip("= "))
