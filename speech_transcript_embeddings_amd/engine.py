@@ -67,6 +67,9 @@ class Engine:
         # a Conformer layer's final LN and the next layer's FFN1 LN as one fused pass (forward and
         # backward, ste_layernorm_*_pair); STE_LN_PAIR=0: separate launches (A/B runs)
         self.ln_pair = _lib.ab_env("STE_LN_PAIR", "1") != "0"
+        # with the text stream: enqueue the text forward after the audio encoder's first layer instead
+        # of before it (Engine.forward); STE_TEXT_AFTER_LAYER=0: before (A/B runs)
+        self.text_after_first_layer = _lib.ab_env("STE_TEXT_AFTER_LAYER", "1") != "0"
         # the text encoder's forward to ~fp32 accuracy (split-bf16 GEMMs, fp32 attention): the loss
         # gradient differences the positive and corrupted transcripts' embeddings, so their bf16
         # forward rounding reappeared in every gradient downstream.  STE_TEXT_PRECISE=0:
@@ -230,6 +233,8 @@ class Engine:
             x, xb, sv, pre1 = self._conformer_fwd(i, x, b, T, maskf, mask32, train, _site_seed(base_seed, 100 + i),
                                                   last, save, pre1=pre1, nxt=nxt)
             layers[i] = sv if save else None
+            if k == 0 and "_text_enqueue" in ctx:   # Engine.forward: the side stream's text forward, now
+                ctx.pop("_text_enqueue")()          # that the main stream holds a layer of work
         if xb is None:  # the last layer was dropped (only the last layer writes the split image)
             xb = ops.split_bf16(x, 2, 2)
         ctx["a_layers"] = layers
@@ -1135,13 +1140,24 @@ class Engine:
         tmask = torch.cat([batch["attention_mask_pos"], batch["attention_mask_neg"]], 0).contiguous()
         ctx["_tmask_i64"] = tmask  # rows [0, b) = positive transcripts (alignment head's text mask)
         side = self._side_stream()
+        text = {}
         if side is not None:  # text encoder on the side stream, audio encoder on the main stream
             main = torch.cuda.current_stream(self.s.device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                th, thb = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx, save)
+            ready = torch.cuda.Event()
+            ready.record(main)   # the text inputs (and everything the main stream did before them)
+
+            def enqueue_text():
+                side.wait_event(ready)
+                with torch.cuda.stream(side):
+                    text["h"] = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx, save)
+            if self.text_after_first_layer:
+                # the host enqueues the text forward (~200 launches) after the audio encoder's first
+                # layer: enqueued first, it left the main stream idle for that long at every step start
+                ctx["_text_enqueue"] = enqueue_text
+            else:
+                enqueue_text()
         else:
-            th, thb = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx, save)
+            text["h"] = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx, save)
         amask = batch.get("attention_mask_audio")
         # host-known clip lengths in the mask's units (fbank frames / raw samples), for SpecAugment's
         # span sampling without a device sync: given by the caller, or summed from a host mask
@@ -1153,6 +1169,9 @@ class Engine:
         ah, ahb = self.audio_forward(batch["input_values"].contiguous(),
                                      None if amask is None else amask.contiguous(), train, _site_seed(base_seed, 3),
                                      ctx, save, lengths=None if alens is None else [int(n) for n in alens])
+        if "_text_enqueue" in ctx:   # an audio path that ran no Conformer layer loop (wav2vec2 front-end)
+            ctx.pop("_text_enqueue")()
+        th, thb = text["h"]
         if side is not None:
             main.wait_stream(side)
         ctx["_thb"], ctx["_ahb"] = thb, ahb
