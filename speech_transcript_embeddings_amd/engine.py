@@ -1152,7 +1152,8 @@ class Engine:
                     text["h"] = self.text_forward(ids.contiguous(), tmask, train, _site_seed(base_seed, 2), ctx, save)
             if self.text_after_first_layer:
                 # the host enqueues the text forward (~200 launches) after the audio encoder's first
-                # layer: enqueued first, it left the main stream idle for that long at every step start
+                # layer, so the main stream has work queued meanwhile (the kernel trace showed it idle
+                # at the step start; untraced the gain is ~0.2 %, DESIGN §3 "Two HIP streams")
                 ctx["_text_enqueue"] = enqueue_text
             else:
                 enqueue_text()
